@@ -1,0 +1,28 @@
+// Shared helpers for the dgx HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dgx.h"
+
+#define DGX_WAVE 64
+
+#define DGX_CHECK_LAUNCH()                                  \
+    do {                                                    \
+        if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH; \
+    } while (0)
+
+static inline hipStream_t dgx_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// XCD-aware block -> work-item map (MI355X_MICROARCH.md: blocks b and b+8 share
+// an XCD). Items are (cloud, tile) pairs; all tiles of one cloud get the same
+// block residue mod 8 so the cloud's rows are served from one XCD's L2.
+// grid = 8 * ceil(B/8) * tiles; returns false for padding blocks.
+__device__ __forceinline__ bool dgx_xcd_cloud_map(int block, int B, int tiles, int& b, int& tile) {
+    int xcd = block & 7, r = block >> 3;
+    int bl = r / tiles;
+    tile = r - bl * tiles;
+    b = bl * 8 + xcd;
+    return b < B;
+}
+static inline int dgx_xcd_cloud_grid(int B, int tiles) { return 8 * ((B + 7) / 8) * tiles; }

@@ -1,0 +1,98 @@
+"""ctypes binding of libdgx.so (the C ABI in include/dgx.h).
+
+The product path has exactly one implementation — the HIP kernels in this
+library. If the library is missing or a ROCm device is not available the ops
+raise; there is no CPU or eager-PyTorch fallback.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DGX_LIB", os.path.join(_HERE, "libdgx.so"))
+
+ORDER_STRIDED = 0
+ORDER_VEC8X4 = 1
+GF_CAT, GF_DISP, GF_KNN_ONLY = 0, 1, 2
+
+_lock = threading.Lock()
+_lib = None
+
+_vp, _i64, _i32, _f32, _f64, _sz = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float,
+                                    ctypes.c_double, ctypes.c_size_t)
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+_SIGS = {
+    "dgx_version": [],
+    "dgx_strerror": [_i32],
+    "dgx_knn_workspace_bytes": [_i32, _i32],
+    "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
+    "dgx_sqnorm_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp],
+    "dgx_knn_select_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp],
+    "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
+    "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
+    "dgx_edge_partials_blocks": [_i32, _i32, _i32],
+    "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
+    "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp],
+    "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
+    "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
+    "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
+    "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dgx_graph_reverse_workspace_bytes": [_i32, _i32, _i32],
+    "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
+    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp,
+                                 _vp, _vp],
+}
+_RESTYPES = {
+    "dgx_version": ctypes.c_char_p,
+    "dgx_strerror": ctypes.c_char_p,
+    "dgx_knn_workspace_bytes": _sz,
+    "dgx_graph_reverse_workspace_bytes": _sz,
+}
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def lib():
+    """Load libdgx.so once (thread-safe: nn.DataParallel calls ops from threads)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(
+                        f"dgx: HIP library not built ({LIB_PATH}); run `make -C dgcnn.pytorch_amd/csrc` "
+                        "or __graft_entry__.build()")
+                handle = ctypes.CDLL(LIB_PATH)
+                for name, argtypes in _SIGS.items():
+                    fn = getattr(handle, name)
+                    fn.argtypes = argtypes
+                    fn.restype = _RESTYPES.get(name, ctypes.c_int)
+                _lib = handle
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().dgx_strerror(rc).decode()
+        raise RuntimeError(f"dgx: {what} failed ({rc}: {msg})")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+            raise RuntimeError("dgx ops run on ROCm device tensors only (MI355X); got "
+                               f"{getattr(t, 'device', type(t))}")

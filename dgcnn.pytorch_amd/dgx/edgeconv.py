@@ -1,0 +1,203 @@
+"""Fused EdgeConv stack: the DGCNN block chain of reference models/dgcnn.py:84-100.
+
+Reference, per block l (dgcnn.py:84-98):
+    e = get_graph_feature(x_{l-1}, k)                     (B, 2C, N, k)
+    x_l = max_k LeakyReLU(BN(Conv2d_1x1(e)))               (B, Co, N)
+and then cat(x1..x4) (dgcnn.py:100).
+
+Engine: one autograd node for the whole chain. Activations live point-major in
+ONE concat buffer xcat (B*N, sum Co) in HBM; block l reads its input as a
+column slice of xcat and writes its output straight into its own slice, so the
+torch.cat of dgcnn.py:100 is free. Per block:
+    idx   = knn(x_{l-1})                      HIP (bit-exact with the reference)
+    PQ    = X [W1; W2]^T                      (B*N, 2Co) per-point GEMM
+    gather/finalize/apply                     HIP (edge max/min + BN stats + LReLU)
+Backward per block (reverse order):
+    dz, BN-bwd affine                         HIP
+    reverse kNN graph + dPQ                   HIP
+    dX += dPQ [W1; W2], dW = dPQ^T X          GEMM (accumulated into xcat's grad)
+"""
+import torch
+
+from . import _native as nat
+from .ops import knn_raw, reduction_order
+
+
+def _bn_factor(bn):
+    """Exponential-average factor nn.BatchNorm uses this step (and bump the counter)."""
+    if bn.momentum is None:
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+            return 1.0 / float(bn.num_batches_tracked.item())
+        return 0.0
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return float(bn.momentum)
+
+
+class _Layer:
+    """Non-tensor description of one block (weights are passed as tensors)."""
+
+    def __init__(self, cin, cout, bn, slope):
+        self.cin, self.cout, self.bn, self.slope = cin, cout, bn, slope
+
+
+def _split_weight(w, cin, cout):
+    w = w.reshape(cout, 2 * cin)
+    # rows [0,Co) produce P (neighbour half, channels [0,C)), rows [Co,2Co) Q (centre half)
+    return torch.cat([w[:, :cin], w[:, cin:]], dim=0)
+
+
+class _EdgeConvStack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, layers, training, *params):
+        dev = x.device
+        B, C0, N = x.shape
+        M = B * N
+        widths = [ly.cout for ly in layers]
+        total = sum(widths)
+        L = nat.lib()
+        stream = nat.stream_of(x)
+        xcat = torch.empty((M, total), dtype=torch.float32, device=dev)
+        x_pm = x.permute(0, 2, 1).reshape(M, C0)  # point-major input rows (copy only if needed)
+        nblk = L.dgx_edge_partials_blocks(B, N, max(widths))
+        saved = []
+        off_in = None
+        count = float(M * k)
+        for li, ly in enumerate(layers):
+            w, gamma, beta = params[3 * li: 3 * li + 3]
+            cin, co = ly.cin, ly.cout
+            if li == 0:
+                X = x_pm
+                idx = knn_raw(x, k, order=reduction_order(x), out_dtype=torch.int32)
+            else:
+                X = xcat[:, off_in:off_in + cin]
+                # the reference's blocks 2-4 see contiguous (B,C,N) features (max over
+                # dim -1 of a contiguous tensor), hence the strided rounding order
+                idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
+                              strides=(N * total, 1, total), shape=(B, cin, N))
+            wcat = _split_weight(w, cin, co)
+            PQ = torch.mm(X, wcat.t())  # (M, 2Co)
+            off = sum(widths[:li])
+            out = xcat[:, off:off + co]
+            bn = ly.bn
+            use_batch = training or bn.running_mean is None
+            scale = torch.empty(co, dtype=torch.float32, device=dev)
+            shift = torch.empty_like(scale)
+            with torch.cuda.device(dev):
+                if use_batch:
+                    ysel = torch.empty((M, co), dtype=torch.float32, device=dev)
+                    arg = torch.empty((M, co), dtype=torch.uint8, device=dev)
+                    sumP = torch.empty((M, co), dtype=torch.float32, device=dev)
+                    partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
+                    mean = torch.empty_like(scale)
+                    invstd = torch.empty_like(scale)
+                    nat.check(L.dgx_edge_fwd_gather_f32(
+                        nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(gamma), nat.ptr(ysel),
+                        nat.ptr(arg), nat.ptr(sumP), nat.ptr(partials), nblk, stream), "edge gather")
+                    update = training and bn.running_mean is not None
+                    factor = _bn_factor(bn) if update else 0.0
+                    nat.check(L.dgx_bn_finalize_f32(
+                        nat.ptr(partials), nblk, co, count, nat.ptr(gamma), nat.ptr(beta),
+                        nat.ptr(bn.running_mean) if update else None,
+                        nat.ptr(bn.running_var) if update else None, factor, float(bn.eps),
+                        nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), stream), "bn finalize")
+                    nat.check(L.dgx_bn_lrelu_apply_f32(nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift),
+                                                       float(ly.slope), nat.ptr(out), total, stream), "bn apply")
+                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd))
+                else:
+                    nat.check(L.dgx_bn_eval_affine_f32(
+                        co, nat.ptr(gamma), nat.ptr(beta), nat.ptr(bn.running_mean), nat.ptr(bn.running_var),
+                        float(bn.eps), nat.ptr(scale), nat.ptr(shift), stream), "bn eval affine")
+                    nat.check(L.dgx_edge_fwd_eval_f32(
+                        nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(scale), nat.ptr(shift),
+                        float(ly.slope), nat.ptr(out), total, stream), "edge eval")
+                    saved.append(None)
+            off_in = off
+        ctx.k = k
+        ctx.layers = layers
+        ctx.shape = (B, C0, N)
+        ctx.layer_state = saved
+        ctx.x_needs_grad = x.requires_grad
+        ctx.save_for_backward(x_pm, xcat, *params)
+        return xcat
+
+    @staticmethod
+    def backward(ctx, dxcat):
+        if any(s is None for s in ctx.layer_state):
+            raise RuntimeError("dgx EdgeConv: backward through an eval-mode (running-stats) forward is not supported")
+        x_pm, xcat, *params = ctx.saved_tensors
+        layers, k = ctx.layers, ctx.k
+        B, C0, N = ctx.shape
+        M = B * N
+        dev = xcat.device
+        L = nat.lib()
+        stream = nat.stream_of(xcat)
+        widths = [ly.cout for ly in layers]
+        total = sum(widths)
+        dxcat = dxcat.contiguous().clone()
+        grads = [None] * len(params)
+        dx_in = None
+        count = float(M * k)
+        rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
+        edges = torch.empty(M * k, dtype=torch.int32, device=dev)
+        rws = L.dgx_graph_reverse_workspace_bytes(B, N, k)
+        rev_ws = torch.empty(max(1, rws // 4), dtype=torch.int32, device=dev)
+        for li in reversed(range(len(layers))):
+            ly = layers[li]
+            cin, co = ly.cin, ly.cout
+            w = params[3 * li]
+            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd = ctx.layer_state[li]
+            off = sum(widths[:li])
+            X = x_pm if li == 0 else xcat[:, off - widths[li - 1]: off - widths[li - 1] + cin]
+            dY = dxcat[:, off:off + co]
+            nblk = max(1, min(1024, (M + 63) // 64))
+            dz = torch.empty((M, co), dtype=torch.float32, device=dev)
+            partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
+            dgamma = torch.empty(co, dtype=torch.float32, device=dev)
+            dbeta = torch.empty(co, dtype=torch.float32, device=dev)
+            c0 = torch.empty(co, dtype=torch.float32, device=dev)
+            c1 = torch.empty(co, dtype=torch.float32, device=dev)
+            dPQ = torch.empty((M, 2 * co), dtype=torch.float32, device=dev)
+            with torch.cuda.device(dev):
+                nat.check(L.dgx_edge_bwd_dz_f32(
+                    nat.ptr(dY), total, nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift), nat.ptr(mean),
+                    nat.ptr(invstd), float(ly.slope), nat.ptr(dz), nat.ptr(partials), nblk, stream), "edge bwd dz")
+                nat.check(L.dgx_bn_bwd_finalize_f32(
+                    nat.ptr(partials), nblk, co, count, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
+                    nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
+                nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
+                                              nat.ptr(rev_ws), rws, stream), "reverse graph")
+                nat.check(L.dgx_edge_bwd_scatter_f32(
+                    nat.ptr(PQ), 2 * co, nat.ptr(idx), nat.ptr(rowptr), nat.ptr(edges), nat.ptr(arg), nat.ptr(dz),
+                    nat.ptr(sumP), B, N, k, co, nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), stream),
+                    "edge bwd scatter")
+            wcat = _split_weight(w, cin, co)
+            dwcat = torch.mm(dPQ.t(), X)  # (2Co, C)
+            grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)
+            grads[3 * li + 1] = dgamma
+            grads[3 * li + 2] = dbeta
+            if li > 0:
+                prev = off - widths[li - 1]
+                dxcat[:, prev:prev + cin].addmm_(dPQ, wcat)
+            elif ctx.x_needs_grad:
+                dx_in = torch.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
+        return (dx_in, None, None, None, *grads)
+
+
+def edgeconv_stack(x, k, convs, training):
+    """Run the block chain. ``convs``: list of nn.Sequential(Conv2d(2C,Co,1,bias=False),
+    BatchNorm2d(Co), LeakyReLU) exactly as the reference builds them (dgcnn.py:54-73).
+    Returns the point-major concat buffer (B*N, sum Co)."""
+    nat.require_device(x)
+    if x.dtype != torch.float32:
+        x = x.float()
+    layers, params = [], []
+    for seq in convs:
+        conv, bn, act = seq[0], seq[1], seq[2]
+        co, c2 = conv.weight.shape[0], conv.weight.shape[1]
+        if bn.weight is None:
+            raise NotImplementedError("dgx EdgeConv expects affine BatchNorm (as the reference builds it)")
+        layers.append(_Layer(c2 // 2, co, bn, act.negative_slope))
+        params += [conv.weight, bn.weight, bn.bias]
+    return _EdgeConvStack.apply(x, k, layers, training, *params)

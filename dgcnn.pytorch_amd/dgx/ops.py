@@ -1,0 +1,125 @@
+"""Device ops behind the reference's graph functions (models/dgcnn.py:6-44).
+
+``knn`` and ``graph_feature`` keep the reference's argument meaning, return
+shapes and dtypes; the work is done by libdgx.so on the tensor's own device
+and current stream.
+"""
+import torch
+
+from . import _native as nat
+
+
+def reduction_order(x):
+    """Rounding order of the reference's ``sum(x**2, dim=1)`` (dgcnn.py:8) for a
+    (B,C,N) tensor with these strides: torch reduces a channel-innermost layout
+    with its vectorised inner reduction, an N-innermost one with the strided
+    cascade (see oracle/knn_oracle.c, pinned by tests/golden)."""
+    _, C, N = x.shape
+    _, sC, sN = x.stride()
+    if C > 1 and N > 1 and sC < sN:
+        return nat.ORDER_VEC8X4
+    return nat.ORDER_STRIDED
+
+
+def _as_f32(x):
+    # autocast may hand fp16/bf16 features; distances are always fp32
+    return x if x.dtype == torch.float32 else x.float()
+
+
+def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None):
+    """kNN on a (B,C,N) fp32 view. ``strides``/``shape`` let callers describe a
+    strided slice of a larger buffer (the engine's point-major concat buffer)."""
+    nat.require_device(x)
+    B, C, N = shape if shape is not None else x.shape
+    sB, sC, sN = strides if strides is not None else x.stride()
+    if order is None:
+        order = reduction_order(x)
+    if not (1 <= k <= N):
+        raise RuntimeError(f"knn: selected index k out of range (k={k}, N={N})")
+    if C > 128 or k > 64:
+        raise NotImplementedError(f"dgx knn kernels are built for C <= 128 and k <= 64 (C={C}, k={k})")
+    L = nat.lib()
+    idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
+    xx = torch.empty((B * N,), dtype=torch.float32, device=x.device)
+    stream = nat.stream_of(x)
+    with torch.cuda.device(x.device):
+        nat.check(L.dgx_sqnorm_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx), stream), "sqnorm")
+        rec = _timing is not None
+        if rec:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        rc = L.dgx_knn_select_f32(nat.ptr(x), sB, sC, sN, nat.ptr(xx), B, C, N, k,
+                                  nat.ptr(idx) if out_dtype == torch.int64 else None,
+                                  nat.ptr(idx) if out_dtype == torch.int32 else None, stream)
+        if rec:
+            ev1.record()
+            _timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
+    nat.check(rc, "knn")
+    return idx
+
+
+# Optional instrumentation (bench.py): when a list, every kNN selection launch
+# appends (start_event, end_event, gram_flops, shape) recorded on the launch stream.
+_timing = None
+
+
+def set_knn_timing(lst):
+    global _timing
+    _timing = lst
+
+
+def knn(x, k):
+    """Drop-in for reference ``knn(x, k)`` (models/dgcnn.py:6-12): int64 (B,N,k)
+    local indices, nearest first; ties in canonical (index ascending) order."""
+    x = _as_f32(x.detach())
+    return knn_raw(x, k)
+
+
+class _GraphFeature(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx32, mode):
+        B, C, N = x.shape
+        k = idx32.shape[-1]
+        if mode == nat.GF_CAT:
+            out = torch.empty((B, 2 * C, N, k), dtype=torch.float32, device=x.device)
+        elif mode == nat.GF_DISP:
+            out = torch.empty((B, C, N, k), dtype=torch.float32, device=x.device)
+        else:
+            out = torch.empty((B, N, k, C), dtype=torch.float32, device=x.device)
+        sB, sC, sN = x.stride()
+        with torch.cuda.device(x.device):
+            rc = nat.lib().dgx_graph_feature_f32(nat.ptr(x), sB, sC, sN, B, C, N, nat.ptr(idx32), k, mode,
+                                                 nat.ptr(out), nat.stream_of(x))
+        nat.check(rc, "graph_feature")
+        ctx.save_for_backward(idx32)
+        ctx.mode = mode
+        ctx.shape = (B, C, N)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx32,) = ctx.saved_tensors
+        B, C, N = ctx.shape
+        dout = dout.contiguous().float()
+        dx = torch.zeros((B, C, N), dtype=torch.float32, device=dout.device)
+        with torch.cuda.device(dout.device):
+            rc = nat.lib().dgx_graph_feature_bwd_f32(nat.ptr(dout), B, C, N, nat.ptr(idx32), idx32.shape[-1],
+                                                     ctx.mode, nat.ptr(dx), nat.stream_of(dout))
+        nat.check(rc, "graph_feature backward")
+        return dx, None, None
+
+
+def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
+    """Drop-in for reference ``get_graph_feature`` (models/dgcnn.py:15-44).
+
+    Default: (B,2C,N,k) fp32 contiguous, channels [0,C) = x_j, [C,2C) = x_i
+    (dgcnn.py:42). knn_only: (B,N,k,C) neighbour rows (dgcnn.py:37-38).
+    disp_only: (B,C,N,k) x_j - x_i (dgcnn.py:39-40). Differentiable w.r.t. x."""
+    nat.require_device(x)
+    x = _as_f32(x)
+    if idx is None:
+        idx = knn_raw(x.detach(), k, out_dtype=torch.int32)
+    elif idx.dtype != torch.int32:
+        idx = idx.to(torch.int32)
+    mode = nat.GF_KNN_ONLY if knn_only else (nat.GF_DISP if disp_only else nat.GF_CAT)
+    return _GraphFeature.apply(x, idx.contiguous(), mode)

@@ -1,0 +1,70 @@
+"""Drop-in for reference ``models/dgcnn.py``: ``knn``, ``get_graph_feature``, ``DGCNN``.
+
+Same names, signatures, defaults, return shapes/dtypes and ``state_dict`` keys
+as the reference (models/dgcnn.py:6-103), so ``from models.dgcnn import ...``
+sites (models/layers.py:6, models/model_partseg.py:11) bind to this module
+unchanged. The work runs in libdgx.so on the MI355X:
+
+* ``knn``  -> fused fp32 distance + top-k kernel, bit-exact distances, ties in
+  canonical order (the reference's CPU ``topk`` order for ties is arbitrary).
+* ``get_graph_feature`` -> gather kernel writing the reference's layout.
+* ``DGCNN.forward`` never materialises the (B,2C,N,k) edge tensors: the four
+  EdgeConv blocks run as one fused chain (dgx.edgeconv), conv5 is a GEMM on
+  the concat buffer the chain writes in place.
+"""
+import torch
+import torch.nn as nn
+
+from dgx import ops as _ops
+from dgx.edgeconv import edgeconv_stack
+
+
+def knn(x, k):
+    """(B,C,N) -> int64 (B,N,k) local indices of the k largest
+    ``-|x_i - x_j|^2`` per point (self included), reference dgcnn.py:6-12."""
+    return _ops.knn(x, k)
+
+
+def get_graph_feature(x, k=20, knn_only=False, disp_only=False):
+    """Edge features of reference dgcnn.py:15-44 (differentiable in x)."""
+    return _ops.graph_feature(x, k=k, knn_only=knn_only, disp_only=disp_only)
+
+
+def _edge_block(c_in, c_out):
+    # Conv2d(2C, Co, 1, bias=False) -> BatchNorm2d -> LeakyReLU(0.2), dgcnn.py:54-73
+    return nn.Sequential(nn.Conv2d(2 * c_in, c_out, kernel_size=1, bias=False),
+                         nn.BatchNorm2d(c_out),
+                         nn.LeakyReLU(negative_slope=0.2, inplace=True))
+
+
+class DGCNN(nn.Module):
+    """4 EdgeConv blocks (3->64->64->128->256) + conv5 (512->emb); input
+    (B,3,N), output (B,emb,N). Reads ``args.emb_dim`` and ``args.k``
+    (reference dgcnn.py:47-78)."""
+
+    WIDTHS = (64, 64, 128, 256)
+
+    def __init__(self, args):
+        super().__init__()
+        self.emb_dims = args.emb_dim
+        self.k = args.k
+        c_in = 3
+        for i, c_out in enumerate(self.WIDTHS, start=1):
+            setattr(self, f"conv{i}", _edge_block(c_in, c_out))
+            c_in = c_out
+        self.conv5 = nn.Sequential(nn.Conv2d(sum(self.WIDTHS), self.emb_dims, kernel_size=1, bias=False),
+                                   nn.BatchNorm2d(self.emb_dims),
+                                   nn.LeakyReLU(negative_slope=0.2, inplace=True))
+
+    def edge_blocks(self):
+        return [self.conv1, self.conv2, self.conv3, self.conv4]
+
+    def forward(self, x):
+        batch_size, _, num_points = x.size()
+        # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)
+        feats = edgeconv_stack(x, self.k, self.edge_blocks(), self.training)
+        feats = feats.view(batch_size, num_points, -1).transpose(1, 2)          # (B, 512, N) view
+        w5 = self.conv5[0].weight.view(self.emb_dims, -1)
+        z = torch.matmul(w5, feats)                                              # conv5 1x1, (B, emb, N)
+        z = self.conv5[2](self.conv5[1](z.unsqueeze(-1)))                        # BN2d + LeakyReLU
+        return z.view(batch_size, -1, num_points)

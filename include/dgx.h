@@ -1,0 +1,151 @@
+/*
+ * dgx — MI355X-native EdgeConv engine, C ABI (libdgx.so).
+ *
+ * The reference (QasimKhan5x/dgcnn.pytorch) is pure Python; its "operator API"
+ * for the hot path is the set of functions in models/dgcnn.py that every model
+ * binds by name (models/layers.py:6, models/model_partseg.py:11). Each entry
+ * point below replaces one step of that path and cites the reference lines it
+ * stands in for. The Python mirror (dgcnn.pytorch_amd/models/dgcnn.py) binds
+ * these through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers (HBM) except where noted; the ABI never
+ *     allocates, never synchronises, and enqueues on `stream` (a hipStream_t).
+ *   - Tensors are described by element strides, so permuted views work
+ *     (main_cls.py:91 feeds x as a permute(0,2,1) view).
+ *   - "point-major" buffers are (M = B*N rows) x (channels) with a row stride ld.
+ *   - Return value: DGX_OK or a negative DGX_E* code; never throws.
+ */
+#ifndef DGX_H
+#define DGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGX_OK 0
+#define DGX_EINVAL (-1)       /* bad shape / argument                          */
+#define DGX_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
+#define DGX_ELAUNCH (-3)      /* hipLaunch / runtime error                     */
+
+/* torch CPU reduction order of sum(x**2, dim=1) that the distances must follow */
+#define DGX_ORDER_STRIDED 0 /* N-contiguous x: cascade over 16-channel blocks  */
+#define DGX_ORDER_VEC8X4 1  /* C-contiguous x: 4x8 vector accumulators         */
+
+/* get_graph_feature output modes, reference models/dgcnn.py:37-44 */
+#define DGX_GF_CAT 0      /* (B,2C,N,k): [x_j ; x_i]          dgcnn.py:42-44 */
+#define DGX_GF_DISP 1     /* (B,C,N,k):  x_j - x_i            dgcnn.py:39-40 */
+#define DGX_GF_KNN_ONLY 2 /* (B,N,k,C):  x_j                  dgcnn.py:37-38 */
+
+const char* dgx_version(void);
+const char* dgx_strerror(int code);
+
+/* ---- a1: kNN, replaces models/dgcnn.py:6-12 (knn) -------------------------
+ * x: fp32 (B,C,N) with element strides (sB,sC,sN). For every point i returns
+ * the k points j with the largest pd_ij = (2 x_i.x_j - |x_j|^2) - |x_i|^2,
+ * rounded exactly as the reference's CPU arithmetic (FMA chain over c,
+ * `order` for |x|^2), sorted by pd descending, ties by index ascending.
+ * Outputs local indices 0..N-1 into idx64 (B,N,k) int64 and/or idx32 (either
+ * may be NULL). Workspace: dgx_knn_workspace_bytes(B,N). Supports C <= 128,
+ * 1 <= k <= min(N, 64). */
+size_t dgx_knn_workspace_bytes(int B, int N);
+int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
+                int B, int C, int N, int k, int order,
+                int64_t* idx64, int32_t* idx32,
+                void* workspace, size_t workspace_bytes, void* stream);
+
+/* The two launches of dgx_knn_f32, separately: |x_i|^2 in the reference's
+ * rounding order into xx (B*N fp32, dgcnn.py:8), then the fused distance +
+ * top-k pass given xx (dgcnn.py:7-11). */
+int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
+                   int B, int C, int N, int order, float* xx, void* stream);
+int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
+                       const float* xx, int B, int C, int N, int k,
+                       int64_t* idx64, int32_t* idx32, void* stream);
+
+/* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
+ * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in
+ * the layout of `mode` (see DGX_GF_*). */
+int dgx_graph_feature_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
+                          int B, int C, int N, const int32_t* idx, int k,
+                          int mode, float* out, void* stream);
+/* Backward of dgx_graph_feature_f32 (autograd of dgcnn.py:31-44): adds into
+ * dx (B,C,N) contiguous. Uses float atomics. */
+int dgx_graph_feature_bwd_f32(const float* dout, int B, int C, int N,
+                              const int32_t* idx, int k, int mode, float* dx,
+                              void* stream);
+
+/* ---- a3: decomposed EdgeConv block, replaces
+ *   get_graph_feature -> Conv2d(2C,Co,1,bias=False) -> BatchNorm2d -> LeakyReLU
+ *   -> max(dim=-1)                        (models/dgcnn.py:54-73, 84-98)
+ * With W = [W1 | W2] (Co x 2C), the conv on edge (i,j) is P_j + Q_i where
+ * P = X W1^T, Q = X W2^T (point-major, computed by the caller's GEMM into one
+ * buffer PQ (M x 2Co): columns [0,Co) = P, [Co,2Co) = Q).
+ *
+ * Forward (training BN), three launches:
+ *   dgx_edge_fwd_gather: per (i,o) max_k P (or min_k where gamma[o] < 0: BN's
+ *     affine is decreasing there), its argument, sum_k P, and per-block partial
+ *     (sum y, sum y^2) over all B*N*k edge outputs y = P_j + Q_i.
+ *   dgx_bn_finalize: batch mean/var (biased) -> scale a, shift b; running
+ *     stats updated with unbiased var (nn.BatchNorm semantics).
+ *   dgx_bn_lrelu_apply: out[i,o] = LeakyReLU(a_o * ysel[i,o] + b_o), written
+ *     with row stride ldo (straight into the caller's concat buffer,
+ *     models/dgcnn.py:100). */
+int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx,
+                            int B, int N, int k, int Co, const float* gamma,
+                            float* ysel, uint8_t* arg, float* sumP,
+                            float* partials, int nblk_hint, void* stream);
+int dgx_edge_partials_blocks(int B, int N, int Co);
+int dgx_bn_finalize_f32(const float* partials, int nblk, int Co, double count,
+                        const float* gamma, const float* beta,
+                        float* running_mean, float* running_var,
+                        double momentum, double eps,
+                        float* scale, float* shift, float* mean, float* invstd,
+                        void* stream);
+int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
+                           const float* shift, float slope, float* out, int ldo,
+                           void* stream);
+/* Eval-mode forward in one launch: out = LeakyReLU(a*sel + b), a,b from
+ * running stats (caller computes them with dgx_bn_eval_affine_f32). */
+int dgx_bn_eval_affine_f32(int Co, const float* gamma, const float* beta,
+                           const float* running_mean, const float* running_var,
+                           double eps, float* scale, float* shift, void* stream);
+int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx,
+                          int B, int N, int k, int Co, const float* scale,
+                          const float* shift, float slope, float* out, int ldo,
+                          void* stream);
+
+/* Backward of the block (autograd of dgcnn.py:84-98 through BN train mode):
+ *   dgx_edge_bwd_dz: dz = dY * LeakyReLU'(z) at the selected edge, per-block
+ *     partial (sum dz, sum dz*yhat) -> dgx_bn_bwd_finalize: dgamma, dbeta and
+ *     the per-channel affine c0 + c1*y of BN's input gradient.
+ *   dgx_graph_reverse: reverse kNN graph (CSR of in-edges per point).
+ *   dgx_edge_bwd_scatter: dPQ (M x 2Co): dP_j = a*sum_{argmax edges->j} dz +
+ *     sum_{edges->j}(c0 + c1*y_e),  dQ_i = a*dz_i + k*c0 + c1*sum_k y_ik.
+ * The caller's GEMMs then form dX += dPQ [W1;W2] and dW = dPQ^T X. */
+int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, int M,
+                        int Co, const float* scale, const float* shift,
+                        const float* mean, const float* invstd, float slope,
+                        float* dz, float* partials, int nblk_hint, void* stream);
+int dgx_bn_bwd_finalize_f32(const float* partials, int nblk, int Co,
+                            double count, const float* scale, const float* mean,
+                            const float* invstd, float* dgamma, float* dbeta,
+                            float* c0, float* c1, int accumulate, void* stream);
+size_t dgx_graph_reverse_workspace_bytes(int B, int N, int k);
+int dgx_graph_reverse(const int32_t* idx, int B, int N, int k,
+                      int32_t* rowptr, int32_t* edges, void* workspace,
+                      size_t workspace_bytes, void* stream);
+int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* idx,
+                             const int32_t* rowptr, const int32_t* edges,
+                             const uint8_t* arg, const float* dz,
+                             const float* sumP, int B, int N, int k, int Co,
+                             const float* scale, const float* c0,
+                             const float* c1, float* dPQ, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGX_H */

@@ -1,0 +1,193 @@
+"""a3/a5/a8 parity: fused EdgeConv chain and DGCNN vs the reference's goldens
+(1e-3 relative fp32)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import rel_err
+from oracle import reference as R
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+
+
+def _block(w, gamma, beta, dev):
+    co, c2 = w.shape[0], w.shape[1]
+    blk = torch.nn.Sequential(torch.nn.Conv2d(c2, co, 1, bias=False), torch.nn.BatchNorm2d(co),
+                              torch.nn.LeakyReLU(0.2, inplace=True)).to(dev)
+    with torch.no_grad():
+        blk[0].weight.copy_(torch.from_numpy(w))
+        blk[1].weight.copy_(torch.from_numpy(gamma))
+        blk[1].bias.copy_(torch.from_numpy(beta))
+    return blk
+
+
+def test_edgeconv_block_golden(golden, cuda):
+    from dgx.edgeconv import edgeconv_stack
+    g = golden("edgeconv_block.npz")
+    k = int(g["k"])
+    blk = _block(g["weight"], g["gamma"], g["beta"], cuda)
+    x = torch.from_numpy(g["x"]).to(cuda).requires_grad_(True)
+    B, C, N = x.shape
+    out = edgeconv_stack(x, k, [blk], True)                       # (B*N, Co) point-major
+    y = out.view(B, N, -1).permute(0, 2, 1)
+    assert rel_err(y.detach().cpu(), g["out"]) < TOL
+    y.backward(torch.from_numpy(g["gout"]).to(cuda))
+    assert rel_err(x.grad.cpu(), g["dx"]) < TOL
+    assert rel_err(blk[0].weight.grad.cpu(), g["dweight"]) < TOL
+    assert rel_err(blk[1].weight.grad.cpu(), g["dgamma"]) < TOL
+    assert rel_err(blk[1].bias.grad.cpu(), g["dbeta"]) < TOL
+    assert rel_err(blk[1].running_mean.cpu(), g["running_mean"]) < 1e-5
+    assert rel_err(blk[1].running_var.cpu(), g["running_var"]) < 1e-5
+    assert int(blk[1].num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("C,Co,N,k", [(3, 64, 300, 20), (64, 128, 256, 16), (128, 256, 130, 10)])
+def test_edgeconv_block_vs_oracle(cuda, C, Co, N, k):
+    """Random shapes (ragged N, negative gammas) against the torch-CPU restatement."""
+    from dgx.edgeconv import edgeconv_stack
+    from models.dgcnn import knn
+    torch.manual_seed(C + Co + N)
+    B = 2
+    x = torch.randn(B, C, N)
+    w = (torch.randn(Co, 2 * C, 1, 1) / (2 * C) ** 0.5).numpy()
+    gamma, beta = torch.randn(Co).numpy(), (0.1 * torch.randn(Co)).numpy()
+    blk = _block(w, gamma, beta, cuda)
+    xg = x.to(cuda).requires_grad_(True)
+    out = edgeconv_stack(xg, k, [blk], True).view(B, N, Co).permute(0, 2, 1)
+    gout = torch.randn(B, Co, N)
+    out.backward(gout.to(cuda))
+    idx = knn(x.to(cuda), k).cpu()
+    xc = x.clone().requires_grad_(True)
+    wc = torch.from_numpy(w).requires_grad_(True)
+    gc = torch.from_numpy(gamma).requires_grad_(True)
+    bc = torch.from_numpy(beta).requires_grad_(True)
+    bn = {"weight": gc, "bias": bc, "running_mean": torch.zeros(Co), "running_var": torch.ones(Co)}
+    ref = R.edgeconv_block(xc, k, wc, bn, True, idx=idx)
+    ref.backward(gout)
+    assert rel_err(out.detach().cpu(), ref.detach()) < TOL
+    assert rel_err(xg.grad.cpu(), xc.grad) < TOL
+    assert rel_err(blk[0].weight.grad.cpu(), wc.grad) < TOL
+    assert rel_err(blk[1].weight.grad.cpu(), gc.grad) < TOL
+    assert rel_err(blk[1].bias.grad.cpu(), bc.grad) < TOL
+    assert rel_err(blk[1].running_var.cpu(), bn["running_var"]) < 1e-5
+
+
+def _dgcnn_from_golden(g, dev, emb=64, k=10):
+    from models.dgcnn import DGCNN
+    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k))
+    m.load_state_dict({n[5:]: torch.from_numpy(g[n]) for n in g.files if n.startswith("init.")})
+    return m.to(dev)
+
+
+def test_dgcnn_train_golden(golden, cuda):
+    g = golden("dgcnn_small.npz")
+    m = _dgcnn_from_golden(g, cuda)
+    m.train()
+    x = torch.from_numpy(g["x"]).to(cuda)
+    y = m(x)
+    assert tuple(y.shape) == g["out"].shape
+    assert rel_err(y.detach().cpu(), g["out"]) < TOL
+    y.backward(torch.from_numpy(g["gout"]).to(cuda))
+    for n, p in m.named_parameters():
+        assert rel_err(p.grad.cpu(), g["grad." + n]) < TOL, n
+    for n, b in m.state_dict().items():
+        if "running" in n:
+            assert rel_err(b.cpu(), g["after." + n]) < 1e-4, n
+
+
+def test_dgcnn_eval_matches_oracle(golden, cuda):
+    g = golden("dgcnn_small.npz")
+    m = _dgcnn_from_golden(g, cuda)
+    with torch.no_grad():
+        for n, b in m.named_buffers():  # non-trivial running stats
+            if n.endswith("running_mean"):
+                b.copy_(torch.linspace(-0.2, 0.2, b.numel()))
+            if n.endswith("running_var"):
+                b.copy_(torch.linspace(0.5, 2.0, b.numel()))
+    m.eval()
+    x = torch.from_numpy(g["x"]).to(cuda)
+    with torch.no_grad():
+        y = m(x)
+    params = {n: t.detach().cpu().clone() for n, t in m.state_dict().items()}
+    ref, _ = R.dgcnn(torch.from_numpy(g["x"]), 10, params, training=False)
+    assert rel_err(y.cpu(), ref) < TOL
+
+
+def test_dgcnn_knn_bit_exact_per_layer(golden, cuda):
+    """Each feature-space kNN inside the fused chain equals the oracle's kNN of
+    the same (GPU-produced) features."""
+    from dgx.edgeconv import edgeconv_stack
+    g = golden("dgcnn_small.npz")
+    m = _dgcnn_from_golden(g, cuda)
+    x = torch.from_numpy(g["x"]).to(cuda)
+    with torch.no_grad():
+        feats = edgeconv_stack(x, 10, m.edge_blocks(), True).cpu()
+    B, N = x.shape[0], x.shape[2]
+    f = feats.view(B, N, -1)
+    off = 0
+    from models.dgcnn import knn
+    for w in (64, 64, 128):
+        xl = f[:, :, off:off + w].permute(0, 2, 1).contiguous()
+        np.testing.assert_array_equal(knn(xl.to(cuda), 10).cpu().numpy(), oracle.knn(xl, 10))
+        off += w
+
+
+def test_dgcnn_state_dict_keys(golden):
+    import json
+    import os
+    from conftest import GOLDEN
+    from models.dgcnn import DGCNN
+    from models.layers import PositionEmbedding
+    with open(os.path.join(GOLDEN, "hashes.json")) as f:
+        keys = json.load(f)["state_dict_keys"]
+    assert list(DGCNN(types.SimpleNamespace(emb_dim=1024, k=20)).state_dict().keys()) == keys["DGCNN"]
+    assert list(PositionEmbedding(types.SimpleNamespace(k=20)).state_dict().keys()) == keys["PositionEmbedding"]
+
+
+def test_position_embedding_golden(golden, cuda):
+    import hashlib
+    from models.layers import PositionEmbedding
+    g = golden("posemb_small.npz")
+    torch.manual_seed(5)
+    m = PositionEmbedding(types.SimpleNamespace(k=10))
+    with torch.no_grad():
+        m.transform.weight.normal_(0, 0.05)
+    sha = hashlib.sha256(b"".join(v.detach().numpy().tobytes() for v in m.state_dict().values())).hexdigest()
+    assert sha == str(g["init_sha256"])
+    m = m.to(cuda).train()
+    x = torch.from_numpy(g["x"]).to(cuda)
+    y = m(x)
+    assert rel_err(y.detach().cpu(), g["out"]) < TOL
+    y.backward(torch.from_numpy(g["gout"]).to(cuda))
+    for n, p in m.named_parameters():
+        key = "grad." + n
+        if key in g.files:
+            assert rel_err(p.grad.cpu(), g[key]) < TOL, n
+        elif "gradproj." + n in g.files:
+            from dgx import synth
+            r = synth.uniform(53, tuple(p.shape)) - 0.5
+            proj = g["gradproj." + n]
+            got = p.grad.cpu().double().numpy()
+            assert abs((got * r).sum() - proj[0]) <= TOL * abs(proj[1]) * np.sqrt(r.size) * 0.3 + 1e-9, n
+            assert abs(np.linalg.norm(got) - proj[1]) <= TOL * proj[1], n
+
+
+def test_dgcnn_full_size_train_step(cuda):
+    """cfg2 shape: finite outputs/grads, BN running stats move, layer-1 kNN
+    equals the oracle at full size (size-independent check)."""
+    from models.dgcnn import DGCNN
+    from dgx import synth
+    torch.manual_seed(0)
+    m = DGCNN(types.SimpleNamespace(emb_dim=1024, k=20)).to(cuda).train()
+    pts = torch.from_numpy(synth.cube_clouds(32, 1024, 0)).to(cuda)
+    y = m(pts.permute(0, 2, 1))
+    assert tuple(y.shape) == (32, 1024, 1024)
+    y.sum().backward()
+    assert torch.isfinite(y).all()
+    for p in m.parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all()
+    assert float(m.conv1[1].running_var.mean()) != 1.0

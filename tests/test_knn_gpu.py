@@ -1,0 +1,103 @@
+"""a1 parity: dgx kNN (HIP) vs the reference's goldens and the CPU oracle."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN, assert_knn_equivalent
+from dgx import synth
+
+pytestmark = pytest.mark.gpu
+
+KNN_CASES = ["c3", "c9", "c64", "c128", "c3k40", "c64k32", "c3n1000"]
+
+
+def _view(pts, layout, dev):
+    t = torch.from_numpy(pts).to(dev)
+    return t.permute(0, 2, 1) if layout == "perm" else t.permute(0, 2, 1).contiguous()
+
+
+def _cpu_view(pts, layout):
+    t = torch.from_numpy(pts)
+    return t.permute(0, 2, 1) if layout == "perm" else t.permute(0, 2, 1).contiguous()
+
+
+@pytest.mark.parametrize("layout", ["bcn", "perm"])
+@pytest.mark.parametrize("case", KNN_CASES)
+def test_knn_matches_reference_golden(golden, cuda, case, layout):
+    from models.dgcnn import knn
+    g = golden("knn_cases.npz")
+    key = f"{case}_{layout}"
+    k = g[key + "_idx"].shape[-1]
+    idx = knn(_view(g[key + "_x"], layout, cuda), k)
+    assert idx.dtype == torch.int64 and tuple(idx.shape) == g[key + "_idx"].shape
+    np.testing.assert_array_equal(idx.cpu().numpy(), g[key + "_idx"])
+
+
+def test_knn_ties_golden(golden, cuda):
+    from models.dgcnn import knn
+    g = golden("knn_cases.npz")
+    pts = g["ties_perm_x"]
+    idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
+    pd = oracle.pairwise(_cpu_view(pts, "perm"))
+    vals = np.take_along_axis(pd, idx, 2)
+    assert_knn_equivalent(idx, vals, g["ties_perm_idx"], g["ties_perm_val"])
+
+
+@pytest.mark.parametrize("B,C,N,k", [(1, 3, 16, 16), (2, 3, 77, 1), (2, 5, 129, 7), (3, 16, 200, 16),
+                                     (2, 31, 333, 20), (1, 64, 1000, 24), (2, 100, 257, 33), (1, 128, 520, 40),
+                                     (1, 3, 64, 64), (2, 12, 100, 50), (1, 9, 4096, 20)])
+@pytest.mark.parametrize("layout", ["bcn", "perm"])
+def test_knn_vs_oracle_ragged(cuda, B, C, N, k, layout):
+    from models.dgcnn import knn
+    pts = synth.relu_normal(B * 1000 + C * 10 + N, (B, N, C)) if C > 3 else synth.cube_clouds(B, N, N + k)
+    idx = knn(_view(pts, layout, cuda), k).cpu().numpy()
+    ref_idx, ref_vals = oracle.knn(_cpu_view(pts, layout), k, return_values=True)
+    pd = oracle.pairwise(_cpu_view(pts, layout)) if N <= 1024 else None
+    if pd is not None:
+        assert_knn_equivalent(idx, np.take_along_axis(pd, idx, 2), ref_idx, ref_vals)
+    else:
+        np.testing.assert_array_equal(idx, ref_idx)
+
+
+def test_knn_full_size_hashes(cuda):
+    """Size-independent parity at BASELINE.json's full sizes: the selected
+    distance values hash equal to the reference's, indices equal the oracle's."""
+    from models.dgcnn import knn
+    with open(os.path.join(GOLDEN, "hashes.json")) as f:
+        H = json.load(f)
+    gens = {"cfg2_layer1": lambda: synth.cube_clouds(32, 1024, 0),
+            "cfg3_layer1": lambda: synth.cube_clouds(32, 2048, 0),
+            "cfg5_layer1": lambda: synth.s3dis_blocks(24, 4096, 2),
+            "ties_layer1": lambda: synth.tie_clouds(32, 1024, 1)}
+    for name, gen in gens.items():
+        h = H[name]
+        pts = gen()
+        idx = knn(_view(pts, "perm", cuda), h["k"]).cpu().numpy()
+        ref_idx, ref_vals = oracle.knn(_cpu_view(pts, "perm"), h["k"], return_values=True)
+        np.testing.assert_array_equal(idx, ref_idx)   # canonical order is deterministic
+        assert hashlib.sha256(ref_vals.tobytes()).hexdigest() == h["val_sha256"], name
+        if not h["boundary_ties"]:
+            assert hashlib.sha256(idx.astype(np.int32).tobytes()).hexdigest() == h["idx_sha256"], name
+
+
+def test_knn_feature_space_sizes(cuda):
+    """Feature-space kNN shapes of DGCNN blocks 2-4 (C=64/128, contiguous) at cfg2 N."""
+    from models.dgcnn import knn
+    for C in (64, 128):
+        pts = synth.relu_normal(3 + C, (4, 1024, C))
+        idx = knn(_view(pts, "bcn", cuda), 20).cpu().numpy()
+        np.testing.assert_array_equal(idx, oracle.knn(_cpu_view(pts, "bcn"), 20))
+
+
+def test_knn_errors(cuda):
+    from models.dgcnn import knn
+    x = torch.zeros(1, 3, 8, device=cuda)
+    with pytest.raises(RuntimeError):
+        knn(x, 9)
+    with pytest.raises(RuntimeError):
+        knn(torch.zeros(1, 3, 8), 2)  # CPU tensors are not silently served

@@ -1,0 +1,60 @@
+"""CPU checks of the boundary: libdgx.so loads and exports every symbol that
+include/dgx.h declares; the Python mirror binds them; no silent CPU path."""
+import ctypes
+import os
+import re
+import types
+
+import pytest
+import torch
+
+from conftest import REPO
+
+
+def _declared():
+    with open(os.path.join(REPO, "include", "dgx.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(dgx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    from dgx import _native
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    declared = _declared()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(lib, name), name
+    # the Python binding declares a signature for every exported symbol
+    assert sorted(_native.exported_symbols()) == declared
+
+
+def test_version_and_errors():
+    from dgx import _native
+    L = _native.lib()
+    assert L.dgx_version().decode().startswith("dgx")
+    assert L.dgx_strerror(-1).decode() == "invalid argument"
+    # argument validation happens before any device work
+    assert L.dgx_knn_f32(None, 0, 0, 0, 1, 3, 8, 2, 0, None, None, None, 0, None) == -1
+    assert L.dgx_knn_workspace_bytes(2, 1024) == 2 * 1024 * 4
+
+
+def test_cpu_tensors_rejected():
+    from models.dgcnn import DGCNN, knn, get_graph_feature
+    x = torch.rand(2, 3, 32)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        knn(x, 4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        get_graph_feature(x, k=4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        DGCNN(types.SimpleNamespace(emb_dim=64, k=4))(x)
+
+
+def test_state_dict_keys_match_reference():
+    import json
+    from conftest import GOLDEN
+    from models.dgcnn import DGCNN
+    from models.layers import PositionEmbedding
+    with open(os.path.join(GOLDEN, "hashes.json")) as f:
+        keys = json.load(f)["state_dict_keys"]
+    assert list(DGCNN(types.SimpleNamespace(emb_dim=1024, k=20)).state_dict().keys()) == keys["DGCNN"]
+    assert list(PositionEmbedding(types.SimpleNamespace(k=20)).state_dict().keys()) == keys["PositionEmbedding"]
