@@ -19,6 +19,13 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef DGX_KNN_DEBUG
+__device__ float* dgx_knn_dbg;
+extern "C" int dgx_knn_set_debug(float* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(dgx_knn_dbg), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#endif
+
 namespace {
 
 constexpr int KQ_WAVES = 4;
@@ -93,20 +100,21 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ x
 // ahead of equal values: canonical tie order for free.
 template <int KMAX>
 __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[KMAX], float nv, int nj) {
-    // Bubble the carried candidate down the list: one compare per position,
-    // consumed at once (keeps a single lane-mask live; no SGPR pressure).
-    float cv = nv;
-    int cj = nj;
+    // Shift insert from the tail: slot q takes slot q-1 if the new value beats
+    // v[q-1], else the new value if it beats v[q], else keeps its own. Every
+    // compare uses the NEW value against the original list, so elements of
+    // equal value keep their relative order (a carried-element bubble would
+    // swap equal neighbours). One lane mask live per step.
+    bool gt_cur = nv > v[KMAX - 1];
 #pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-        bool s = cv > v[q];
-        float tv = v[q];
-        int tj = id[q];
-        v[q] = s ? cv : tv;
-        id[q] = s ? cj : tj;
-        cv = s ? tv : cv;
-        cj = s ? tj : cj;
+    for (int q = KMAX - 1; q > 0; --q) {
+        const bool gt_prev = nv > v[q - 1];
+        v[q] = gt_prev ? v[q - 1] : (gt_cur ? nv : v[q]);
+        id[q] = gt_prev ? id[q - 1] : (gt_cur ? nj : id[q]);
+        gt_cur = gt_prev;
     }
+    v[0] = gt_cur ? nv : v[0];
+    id[0] = gt_cur ? nj : id[0];
 }
 
 // Insert with the full canonical comparator (value desc, index asc): used when
@@ -146,7 +154,7 @@ template <int NSTEP, int KMAX, bool CMAJOR>
 __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
                                                     int64_t sN, const float* __restrict__ xx, int B, int C,
                                                     int N, int k, int nqb, int64_t* __restrict__ idx64,
-                                                    int32_t* __restrict__ idx32) {
+                                                    int32_t* __restrict__ idx32, float* __restrict__ vals) {
 #pragma clang fp contract(off)
     constexpr int CP = NSTEP * 4;
     constexpr int CHUNK = KnnSmem<NSTEP>::CHUNK;
@@ -256,6 +264,12 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
     flush();
     __syncthreads();
 
+#ifdef DGX_KNN_DEBUG
+    if (q < N && dgx_knn_dbg) {
+        float* d = dgx_knn_dbg + (((int64_t)b * N + q) * 4 + g) * KMAX * 2;
+        for (int t = 0; t < KMAX; ++t) { d[t] = lv[t]; d[KMAX + t] = (float)li[t]; }
+    }
+#endif
     // Merge the 4 partial lists of each query (lanes ql, ql+16, ql+32, ql+48):
     // g1 -> g0 and g3 -> g2, then g2 -> g0. Scratch per wave: 2 slots x 16
     // lists, element-major ([t][list]) so a wave's accesses are conflict-free.
@@ -289,6 +303,7 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
                 if (t >= kpad) {
                     if (idx64) idx64[row + t] = li[t];
                     if (idx32) idx32[row + t] = li[t];
+                    if (vals) vals[row + t] = lv[t];
                 }
             }
         }
@@ -297,26 +312,26 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
 
 template <int NSTEP, int KMAX>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-               int k, int64_t* idx64, int32_t* idx32, hipStream_t st) {
+               int k, int64_t* idx64, int32_t* idx32, float* vals, hipStream_t st) {
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
     dim3 grid(dgx_xcd_cloud_grid(B, nqb)), block(256);
     if (sN == 1)
         hipLaunchKernelGGL((knn_kernel<NSTEP, KMAX, true>), grid, block, 0, st, x, sB, sC, sN, xx, B, C, N, k,
-                           nqb, idx64, idx32);
+                           nqb, idx64, idx32, vals);
     else
         hipLaunchKernelGGL((knn_kernel<NSTEP, KMAX, false>), grid, block, 0, st, x, sB, sC, sN, xx, B, C, N, k,
-                           nqb, idx64, idx32);
+                           nqb, idx64, idx32, vals);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 template <int NSTEP>
 int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, hipStream_t st) {
-    if (k <= 16) return launch_knn<NSTEP, 16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    if (k <= 20) return launch_knn<NSTEP, 20>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    if (k <= 32) return launch_knn<NSTEP, 32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    if (k <= 40) return launch_knn<NSTEP, 40>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    return launch_knn<NSTEP, 64>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
+               int64_t* idx64, int32_t* idx32, float* vals, hipStream_t st) {
+    if (k <= 16) return launch_knn<NSTEP, 16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    if (k <= 20) return launch_knn<NSTEP, 20>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    if (k <= 32) return launch_knn<NSTEP, 32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    if (k <= 40) return launch_knn<NSTEP, 40>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    return launch_knn<NSTEP, 64>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
 }
 
 }  // namespace
@@ -337,17 +352,17 @@ int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
 size_t dgx_knn_workspace_bytes(int B, int N) { return (size_t)B * (size_t)N * sizeof(float); }
 
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                       int k, int64_t* idx64, int32_t* idx32, void* stream) {
+                       int k, int64_t* idx64, int32_t* idx32, float* vals, void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64) return DGX_EUNSUPPORTED;
     if (B == 0) return DGX_OK;
     hipStream_t st = dgx_stream(stream);
-    if (C <= 4) return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    if (C <= 12) return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    if (C <= 32) return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    if (C <= 64) return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
-    return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, st);
+    if (C <= 4) return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    if (C <= 12) return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    if (C <= 32) return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    if (C <= 64) return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
 }
 
 int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int k, int order,
@@ -360,7 +375,7 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C
     float* xx = static_cast<float*>(workspace);
     int rc = dgx_sqnorm_f32(x, sB, sC, sN, B, C, N, order, xx, stream);
     if (rc != DGX_OK) return rc;
-    return dgx_knn_select_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, stream);
+    return dgx_knn_select_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, nullptr, stream);
 }
 
 }  // extern "C"

@@ -23,6 +23,12 @@ from . import _native as nat
 from .ops import knn_raw, reduction_order
 
 
+# Optional capture for tests/tools: when a dict, forward stores each block's
+# routing decisions (idx, arg, zpos) under ("fwd", l) and backward stores
+# intermediates under l. Off (None) in normal use.
+_debug = None
+
+
 def _bn_factor(bn):
     """Exponential-average factor nn.BatchNorm uses this step (and bump the counter)."""
     if bn.momentum is None:
@@ -105,6 +111,9 @@ class _EdgeConvStack(torch.autograd.Function):
                     nat.check(L.dgx_bn_lrelu_apply_f32(nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift),
                                                        float(ly.slope), nat.ptr(out), total, stream), "bn apply")
                     saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd))
+                    if _debug is not None:
+                        zpos = (scale * ysel + shift) > 0
+                        _debug[("fwd", li)] = (idx.clone(), arg.clone(), zpos)
                 else:
                     nat.check(L.dgx_bn_eval_affine_f32(
                         co, nat.ptr(gamma), nat.ptr(beta), nat.ptr(bn.running_mean), nat.ptr(bn.running_var),
@@ -172,6 +181,13 @@ class _EdgeConvStack(torch.autograd.Function):
                     nat.ptr(PQ), 2 * co, nat.ptr(idx), nat.ptr(rowptr), nat.ptr(edges), nat.ptr(arg), nat.ptr(dz),
                     nat.ptr(sumP), B, N, k, co, nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), stream),
                     "edge bwd scatter")
+            if _debug is not None:
+                _debug[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
+                              "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.clone(), "partials": partials.clone(),
+                              "ysel": ysel.clone(), "scale": scale.clone(), "shift": shift.clone(),
+                              "arg": arg.clone(), "idx": idx.clone(), "PQ": PQ.clone(), "sumP": sumP.clone(),
+                              "mean": mean.clone(), "invstd": invstd.clone(), "X": X.clone(),
+                              "rowptr": rowptr.clone(), "edges": edges.clone()}
             wcat = _split_weight(w, cin, co)
             dwcat = torch.mm(dPQ.t(), X)  # (2Co, C)
             grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)

@@ -26,7 +26,7 @@ def _as_f32(x):
     return x if x.dtype == torch.float32 else x.float()
 
 
-def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None):
+def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False):
     """kNN on a (B,C,N) fp32 view. ``strides``/``shape`` let callers describe a
     strided slice of a larger buffer (the engine's point-major concat buffer)."""
     nat.require_device(x)
@@ -40,6 +40,7 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None):
         raise NotImplementedError(f"dgx knn kernels are built for C <= 128 and k <= 64 (C={C}, k={k})")
     L = nat.lib()
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
+    vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
     xx = torch.empty((B * N,), dtype=torch.float32, device=x.device)
     stream = nat.stream_of(x)
     with torch.cuda.device(x.device):
@@ -50,12 +51,12 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None):
             ev0.record()
         rc = L.dgx_knn_select_f32(nat.ptr(x), sB, sC, sN, nat.ptr(xx), B, C, N, k,
                                   nat.ptr(idx) if out_dtype == torch.int64 else None,
-                                  nat.ptr(idx) if out_dtype == torch.int32 else None, stream)
+                                  nat.ptr(idx) if out_dtype == torch.int32 else None, nat.ptr(vals), stream)
         if rec:
             ev1.record()
             _timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
     nat.check(rc, "knn")
-    return idx
+    return (idx, vals) if return_values else idx
 
 
 # Optional instrumentation (bench.py): when a list, every kNN selection launch

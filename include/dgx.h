@@ -59,12 +59,13 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
 
 /* The two launches of dgx_knn_f32, separately: |x_i|^2 in the reference's
  * rounding order into xx (B*N fp32, dgcnn.py:8), then the fused distance +
- * top-k pass given xx (dgcnn.py:7-11). */
+ * top-k pass given xx (dgcnn.py:7-11); vals (B,N,k), nullable, receives the
+ * selected pd values (what pd.topk(k)[0] would hold). */
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                    int B, int C, int N, int order, float* xx, void* stream);
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                        const float* xx, int B, int C, int N, int k,
-                       int64_t* idx64, int32_t* idx32, void* stream);
+                       int64_t* idx64, int32_t* idx32, float* vals, void* stream);
 
 /* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
  * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in

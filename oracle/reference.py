@@ -80,3 +80,43 @@ def _bn(params, prefix):
     return {"weight": params[prefix + ".weight"], "bias": params[prefix + ".bias"],
             "running_mean": params[prefix + ".running_mean"], "running_var": params[prefix + ".running_var"],
             "momentum": 0.1, "eps": 1e-5}
+
+
+# --------------------------------------------------------------------------
+# Decision-routed variants. max_k and LeakyReLU are non-smooth: at a near-tie
+# of the max or at z ~ 0, any change of fp32 summation order (GPU vs CPU, or
+# the engine's P_j + Q_i decomposition) can route a gradient differently. To
+# hold gradients to 1e-3 the oracle below re-uses the engine's DECISIONS (the
+# selected neighbour per (point, channel) and the sign of the selected BN
+# output) and recomputes everything else in fp64. The tests separately check
+# that each decision is valid (the chosen edge is a max up to rounding; a sign
+# only differs where |z| is at rounding level).
+
+def edgeconv_block_routed(x, weight, bn, idx, arg, zpos, slope=0.2):
+    """x (B,C,N); idx (B,N,k); arg (B*N,Co) chosen k-slot; zpos (B*N,Co) bool."""
+    e = graph_feature(x, idx=idx)
+    y = F.conv2d(e, weight)
+    z = F.batch_norm(y, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], True,
+                     bn.get("momentum", 0.1), bn.get("eps", 1e-5))
+    B, Co, N, _ = z.shape
+    a = arg.long().view(B, N, Co).permute(0, 2, 1).unsqueeze(-1)
+    zsel = torch.gather(z, 3, a).squeeze(-1)
+    m = zpos.view(B, N, Co).permute(0, 2, 1)
+    return torch.where(m, zsel, slope * zsel), z
+
+
+def dgcnn_routed(x, params, decisions, mask5, slope=0.2):
+    """DGCNN forward with the engine's decisions: decisions[l] = (idx, arg, zpos)
+    for blocks 1-4, mask5 (B,emb,N) bool = sign of conv5's BN output."""
+    B, _, N = x.shape
+    h, feats = x, []
+    for i in range(1, 5):
+        idx, arg, zpos = decisions[i - 1]
+        h, _ = edgeconv_block_routed(h, params[f"conv{i}.0.weight"], _bn(params, f"conv{i}.1"), idx, arg, zpos, slope)
+        feats.append(h)
+    z = torch.cat(feats, dim=1).unsqueeze(-1)
+    z = F.conv2d(z, params["conv5.0.weight"])
+    bn = _bn(params, "conv5.1")
+    z = F.batch_norm(z, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], True, 0.1, 1e-5)
+    z = z.view(B, -1, N)
+    return torch.where(mask5, z, slope * z)

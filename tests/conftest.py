@@ -52,6 +52,6 @@ def assert_knn_equivalent(idx, vals, ref_idx, ref_vals):
     kth = ref_vals[..., -1:]
     strict = ref_vals > kth
     np.testing.assert_array_equal(np.where(strict, idx, -1), np.where(strict, ref_idx, -1))
-    tie = ~strict
-    d = np.diff(np.where(tie, idx, -1), axis=-1)
-    assert (d[tie[..., 1:] & tie[..., :-1]] > 0).all()
+    # every run of equal values (anywhere in the row) must list indices ascending
+    eq = vals[..., 1:] == vals[..., :-1]
+    assert (np.diff(idx, axis=-1)[eq] > 0).all()
