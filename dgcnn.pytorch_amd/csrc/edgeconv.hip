@@ -1,0 +1,590 @@
+// a3/a8 — the decomposed EdgeConv block (reference models/dgcnn.py:54-98).
+//
+// Reference, per block: edge tensor (B,2C,N,k) -> Conv2d(2C,Co,1) -> BN2d ->
+// LeakyReLU -> max over k. Because the conv is linear and 1x1,
+//     y(i,j) = W1 x_j + W2 x_i = P_j + Q_i,   P = X W1^T, Q = X W2^T,
+// so the caller runs a per-point GEMM (k times fewer flops) into PQ (M x 2Co)
+// and these kernels do the rest without ever forming an edge tensor:
+//
+//   gather    per (i,o): max_k P_j (min_k where gamma_o < 0 — BN's affine is
+//             decreasing there), its slot, sum_k P_j, and partial sums of y and
+//             y^2 over all B*N*k edge values (BN batch statistics).
+//   finalize  statistics -> (a, b) affine, running stats (nn.BatchNorm rules).
+//   apply     LeakyReLU(a*ysel + b) into the caller's concat buffer.
+//   max_k LReLU(a y + b) = LReLU(a max_k y + b) for a >= 0 (min for a < 0).
+//
+// Backward follows BN's train-mode gradient: for every edge
+//   dy_e = a*dz_e + c0 + c1*y_e   (dz_e nonzero only at the selected edge),
+// so dQ_i = a*dz_i + k*c0 + c1*(sum_k P + k*Q_i) and dP_j sums over the
+// in-edges of j (reverse kNN graph, built per cloud as a CSR).
+//
+// Memory layout / LDS tiling: a workgroup owns (cloud b, channel slice of CS
+// channels, part of the points). It stages the cloud's whole slice of the
+// gathered operand (P forward; Q and packed dz|slot backward) in LDS once, then
+// every neighbour access is an LDS read: HBM/L2 traffic per block is the
+// compulsory M*Co*(bytes) instead of M*k*Co*(bytes).
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int EC_THREADS = 512;
+constexpr int EC_LDS_BYTES = 64 * 1024;   // per workgroup (2 workgroups per CU)
+
+__device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.f ? v : v * slope; }
+
+// dz with the selected k-slot packed into the 6 low mantissa bits (k <= 64):
+// one 4-byte word per (point, channel) in the backward's LDS image.
+__device__ __forceinline__ float pack_dz(float dz, int slot) {
+    return __uint_as_float((__float_as_uint(dz) & ~63u) | (unsigned)slot);
+}
+__device__ __forceinline__ float unpack_dz(float p) { return __uint_as_float(__float_as_uint(p) & ~63u); }
+__device__ __forceinline__ int unpack_slot(float p) { return (int)(__float_as_uint(p) & 63u); }
+
+// ------------------------------------------------------------- forward -----
+// grid (B * nparts, ceil(Co / CS)); partial-stat row = blockIdx.x.
+// Stage rows [0,N) x columns [col0, col0+CS) of a row-major matrix (row stride
+// ld floats) into LDS [N][CS]; 16-byte loads when the slice is 16-byte aligned.
+template <int CS, int THREADS>
+__device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float* __restrict__ src, int64_t ld,
+                                            int N, int col0, int ncols, bool vec4) {
+    const int t = threadIdx.x;
+    if (CS % 4 == 0 && vec4 && col0 + CS <= ncols) {
+        constexpr int Q = CS / 4;
+        const int total = N * Q;
+        int e = t;
+        for (; e + 3 * THREADS < total; e += 4 * THREADS) {  // 4 independent 16-byte loads in flight
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ee = e + u * THREADS, n = ee / Q, q = ee - n * Q;
+                v[u] = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * q);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) reinterpret_cast<float4*>(dst)[e + u * THREADS] = v[u];
+        }
+        for (; e < total; e += THREADS) {
+            const int n = e / Q, q = e - n * Q;
+            reinterpret_cast<float4*>(dst)[e] = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * q);
+        }
+    } else {
+        for (int e = t; e < N * CS; e += THREADS) {
+            const int n = e / CS, c = e - n * CS;
+            dst[e] = (col0 + c < ncols) ? src[(int64_t)n * ld + col0 + c] : 0.f;
+        }
+    }
+}
+
+template <int CS, bool EVAL>
+__global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int N, int k, int Co, int nparts,
+    const float* __restrict__ sel_sign, const float* __restrict__ shift, float slope, float* __restrict__ ysel,
+    uint8_t* __restrict__ arg, float* __restrict__ sumP, float* __restrict__ partials, float* __restrict__ out,
+    int ldo) {
+    extern __shared__ float lds[];  // [N][CS] slice of P, then [2][EC_THREADS] reduction
+    const int b = blockIdx.x / nparts, part = blockIdx.x - b * nparts;
+    const int o0 = blockIdx.y * CS;
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)b * N;
+    const int per = (N + nparts - 1) / nparts;
+    const int n_beg = part * per, n_end = min(N, n_beg + per);
+    stage_slice<CS, EC_THREADS>(lds, PQ + base * ldpq, ldpq, N, o0, Co, (ldpq % 4) == 0 && (o0 % 4) == 0);
+    __syncthreads();
+
+    const int c = t % CS;
+    const int o = o0 + c;
+    const bool ok = o < Co;
+    const bool k4 = (k & 3) == 0;
+    float acc1 = 0.f, acc2 = 0.f;
+    if (ok) {
+        const float sgn = sel_sign[o];
+        const bool take_min = sgn < 0.f;
+        for (int n = n_beg + t / CS; n < n_end; n += EC_THREADS / CS) {
+            const int64_t i = base + n;
+            const int32_t* __restrict__ row = idx + i * k;
+            float best = take_min ? INFINITY : -INFINITY, s = 0.f, s2 = 0.f;
+            int barg = 0;
+#define DGX_TAKE(J, K)                                                   \
+    {                                                                    \
+        const float v = lds[(J) * CS + c];                               \
+        const bool better = take_min ? v < best : v > best;              \
+        best = better ? v : best;                                        \
+        barg = better ? (K) : barg;                                      \
+        s += v;                                                          \
+        s2 = fmaf(v, v, s2);                                             \
+    }
+            int kk = 0;
+            if (k4) {
+                for (; kk < k; kk += 4) {
+                    const int4 j4 = *reinterpret_cast<const int4*>(row + kk);
+                    DGX_TAKE(j4.x, kk) DGX_TAKE(j4.y, kk + 1) DGX_TAKE(j4.z, kk + 2) DGX_TAKE(j4.w, kk + 3)
+                }
+            } else {
+                for (; kk < k; ++kk) DGX_TAKE(row[kk], kk)
+            }
+#undef DGX_TAKE
+            const float q = PQ[i * ldpq + Co + o];
+            const float y = best + q;
+            if (EVAL) {
+                out[i * ldo + o] = lrelu(fmaf(sgn, y, shift[o]), slope);
+            } else {
+                ysel[i * Co + o] = y;
+                arg[i * Co + o] = (uint8_t)barg;
+                sumP[i * Co + o] = s;
+                acc1 += fmaf((float)k, q, s);                     // sum_k y
+                acc2 += s2 + q * fmaf(2.f, s, (float)k * q);     // sum_k y^2
+            }
+        }
+    }
+    if (EVAL) return;
+    // reduce the EC_THREADS/CS threads that share channel c
+    __syncthreads();
+    float* red = lds;
+    red[t] = acc1;
+    red[EC_THREADS + t] = acc2;
+    __syncthreads();
+    if (t < CS && ok) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int u = t; u < EC_THREADS; u += CS) {
+            s1 += red[u];
+            s2 += red[EC_THREADS + u];
+        }
+        partials[(int64_t)blockIdx.x * 2 * Co + o] = s1;
+        partials[(int64_t)blockIdx.x * 2 * Co + Co + o] = s2;
+    }
+}
+
+// one block per channel: fp64 tree reduction of the partial rows
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ partials, int nrows, int Co,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar, double momentum, double eps,
+                                                          float* __restrict__ scale, float* __restrict__ shift,
+                                                          float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out) {
+    __shared__ double r1[256], r2[256];
+    const int o = blockIdx.x, t = threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = t; i < nrows; i += 256) {
+        s1 += (double)partials[(int64_t)i * 2 * Co + o];
+        s2 += (double)partials[(int64_t)i * 2 * Co + Co + o];
+    }
+    r1[t] = s1;
+    r2[t] = s2;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) { r1[t] += r1[t + w]; r2[t] += r2[t + w]; }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    const double mean = r1[0] / count;
+    double var = r2[0] / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const double invstd = 1.0 / sqrt(var + eps);
+    const double a = (gamma ? (double)gamma[o] : 1.0) * invstd;
+    scale[o] = (float)a;
+    shift[o] = (float)((beta ? (double)beta[o] : 0.0) - mean * a);
+    if (mean_out) mean_out[o] = (float)mean;
+    if (invstd_out) invstd_out[o] = (float)invstd;
+    if (rmean) rmean[o] = (float)((1.0 - momentum) * (double)rmean[o] + momentum * mean);
+    if (rvar) {
+        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        rvar[o] = (float)((1.0 - momentum) * (double)rvar[o] + momentum * unbiased);
+    }
+}
+
+__global__ void bn_eval_affine_kernel(int Co, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                      const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                      double eps, float* __restrict__ scale, float* __restrict__ shift) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= Co) return;
+    const float invstd = 1.0f / sqrtf(rvar[o] + (float)eps);
+    const float a = (gamma ? gamma[o] : 1.f) * invstd;
+    scale[o] = a;
+    shift[o] = (beta ? beta[o] : 0.f) - rmean[o] * a;
+}
+
+__global__ void bn_lrelu_apply_kernel(const float* __restrict__ ysel, int M, int Co,
+                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                      float slope, float* __restrict__ out, int ldo) {
+    const int64_t total = (int64_t)M * Co;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int o = (int)(t % Co);
+        const int64_t i = t / Co;
+        out[i * ldo + o] = lrelu(fmaf(scale[o], ysel[t], shift[o]), slope);
+    }
+}
+
+// ------------------------------------------------------------ backward -----
+// dz at the selected edge (packed with its slot) and per-row-block partial
+// (sum dz, sum dz*yhat). grid (nrows, ceil(Co/64)).
+__global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
+    const float* __restrict__ dY, int lddy, const float* __restrict__ ysel, const uint8_t* __restrict__ arg,
+    int M, int Co, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float slope, float* __restrict__ dzp,
+    float* __restrict__ partials, int rows_per_blk) {
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int o = blockIdx.y * 64 + lane;
+    const bool ok = o < Co;
+    float acc1 = 0.f, acc2 = 0.f;
+    if (ok) {
+        const float a = scale[o], sh = shift[o], mu = mean[o], is = invstd[o];
+        const int64_t i0 = (int64_t)blockIdx.x * rows_per_blk;
+        for (int r = wave; r < rows_per_blk; r += 4) {
+            const int64_t i = i0 + r;
+            if (i >= M) break;
+            const float y = ysel[i * Co + o];
+            const float z = fmaf(a, y, sh);
+            const float d = dY[i * lddy + o] * (z > 0.f ? 1.f : slope);
+            dzp[i * Co + o] = pack_dz(d, arg[i * Co + o]);
+            acc1 += d;
+            acc2 = fmaf(d, (y - mu) * is, acc2);
+        }
+    }
+    red[0][wave][lane] = acc1;
+    red[1][wave][lane] = acc2;
+    __syncthreads();
+    if (wave == 0 && ok) {
+        partials[(int64_t)blockIdx.x * 2 * Co + o] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+        partials[(int64_t)blockIdx.x * 2 * Co + Co + o] =
+            red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partials, int nrows,
+                                                              int Co, double count, const float* __restrict__ scale,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ c0, float* __restrict__ c1,
+                                                              int accumulate) {
+    __shared__ double r1[256], r2[256];
+    const int o = blockIdx.x, t = threadIdx.x;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = t; i < nrows; i += 256) {
+        s1 += (double)partials[(int64_t)i * 2 * Co + o];
+        s2 += (double)partials[(int64_t)i * 2 * Co + Co + o];
+    }
+    r1[t] = s1;
+    r2[t] = s2;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) { r1[t] += r1[t + w]; r2[t] += r2[t + w]; }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    s1 = r1[0];
+    s2 = r2[0];
+    if (dbeta) dbeta[o] = (float)(accumulate ? (double)dbeta[o] + s1 : s1);
+    if (dgamma) dgamma[o] = (float)(accumulate ? (double)dgamma[o] + s2 : s2);
+    const double a = scale[o], mu = mean[o], is = invstd[o];
+    const double g1 = s1 / count, g2 = s2 / count;
+    c0[o] = (float)(a * (-g1 + g2 * mu * is));
+    c1[o] = (float)(-a * g2 * is);
+}
+
+// Reverse kNN graph, one workgroup per cloud (in-edges stay inside a cloud):
+// count -> scan -> fill with LDS atomics, then every list sorted by edge id so
+// the backward's summation order is deterministic. Edge id = (i << 6) | slot.
+// With LDS_LISTS the cloud's N*k edge ids are built and sorted in LDS and
+// written out once (coalesced); otherwise they are sorted in place in HBM.
+template <bool LDS_LISTS>
+__global__ __launch_bounds__(1024) void rev_graph_kernel(const int32_t* __restrict__ idx, int N, int k,
+                                                         int32_t* __restrict__ rowptr, int32_t* __restrict__ edges) {
+    extern __shared__ int32_t cnt[];  // [N] counts -> cursors | [N] list starts | [1024] scan | [N*k] lists
+    int32_t* start = cnt + N;
+    int32_t* scan = start + N;
+    int32_t* lists = scan + 1024;
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int64_t base = (int64_t)b * N;
+    const int32_t* __restrict__ ib = idx + base * k;
+    const int32_t ebase = (int32_t)(base * k);
+    int32_t* out = LDS_LISTS ? lists : edges + ebase;
+    for (int n = t; n < N; n += 1024) cnt[n] = 0;
+    __syncthreads();
+    for (int e = t; e < N * k; e += 1024) atomicAdd(&cnt[ib[e]], 1);
+    __syncthreads();
+    const int per = (N + 1023) / 1024;
+    const int lo = min(N, t * per), hi = min(N, lo + per);
+    int32_t s = 0;
+    for (int n = lo; n < hi; ++n) s += cnt[n];
+    scan[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int32_t v = t >= off ? scan[t - off] : 0;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+    }
+    int32_t run = (t == 0 ? 0 : scan[t - 1]);
+    for (int n = lo; n < hi; ++n) {
+        const int32_t c = cnt[n];
+        rowptr[base + n] = ebase + run;
+        start[n] = run;
+        cnt[n] = run;  // fill cursor
+        run += c;
+    }
+    if (b == gridDim.x - 1 && t == 0) rowptr[base + N] = (int32_t)((base + N) * k);
+    __syncthreads();
+    for (int e = t; e < N * k; e += 1024) {
+        const int32_t pos = atomicAdd(&cnt[ib[e]], 1);
+        out[pos] = ((int32_t)(base + e / k) << 6) | (e % k);
+    }
+    __syncthreads();
+    for (int n = t; n < N; n += 1024) {  // insertion sort of each (short) list
+        const int32_t beg = start[n], end = cnt[n];
+        for (int32_t a = beg + 1; a < end; ++a) {
+            const int32_t v = out[a];
+            int32_t p = a - 1;
+            while (p >= beg && out[p] > v) { out[p + 1] = out[p]; --p; }
+            out[p + 1] = v;
+        }
+    }
+    if (LDS_LISTS) {
+        __syncthreads();
+        for (int e = t; e < N * k; e += 1024) edges[ebase + e] = lists[e];
+    }
+}
+
+// dPQ for every point: grid (B * nparts, ceil(Co / CS)). The cloud's Q slice
+// and packed dz|slot slice live in LDS; each (point, channel) thread walks
+// the point's in-edges.
+template <int CS>
+__global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
+    const float* __restrict__ dzp, const float* __restrict__ sumP, int N, int k, int Co, int nparts,
+    const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
+    float* __restrict__ dPQ) {
+    extern __shared__ float lds[];  // [N][CS] Q slice, [N][CS] packed dz
+    float* qs = lds;
+    float* ds = lds + N * CS;
+    const int b = blockIdx.x / nparts, part = blockIdx.x - b * nparts;
+    const int o0 = blockIdx.y * CS;
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)b * N;
+    stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
+    stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+    __syncthreads();
+    const int c = t % CS;
+    const int o = o0 + c;
+    if (o >= Co) return;
+    const float a = scale[o], k0 = c0[o], k1 = c1[o], kf = (float)k;
+    const int per = (N + nparts - 1) / nparts;
+    const int n_beg = part * per, n_end = min(N, n_beg + per);
+    const int32_t ibase = (int32_t)base;
+    for (int n = n_beg + t / CS; n < n_end; n += EC_THREADS / CS) {
+        const int64_t j = base + n;
+        const int32_t beg = rowptr[j], end = rowptr[j + 1];
+        float sq = 0.f, sd = 0.f;
+        int32_t u = beg;
+#define DGX_EDGE(E)                                                      \
+    {                                                                    \
+        const int il = ((E) >> 6) - ibase;                               \
+        sq += qs[il * CS + c];                                           \
+        const float p = ds[il * CS + c];                                 \
+        sd += unpack_slot(p) == ((E) & 63) ? unpack_dz(p) : 0.f;         \
+    }
+        for (; u + 4 <= end; u += 4) {
+            const int32_t e0 = edges[u], e1 = edges[u + 1], e2 = edges[u + 2], e3 = edges[u + 3];
+            DGX_EDGE(e0) DGX_EDGE(e1) DGX_EDGE(e2) DGX_EDGE(e3)
+        }
+        for (; u < end; ++u) {
+            const int32_t e0 = edges[u];
+            DGX_EDGE(e0)
+        }
+#undef DGX_EDGE
+        const float deg = (float)(end - beg);
+        const float pj = PQ[j * ldpq + o];
+        const float qj = qs[n * CS + c];
+        dPQ[j * 2 * Co + o] = fmaf(a, sd, fmaf(k0, deg, k1 * fmaf(deg, pj, sq)));
+        dPQ[j * 2 * Co + Co + o] = fmaf(a, unpack_dz(ds[n * CS + c]), fmaf(k0, kf, k1 * fmaf(kf, qj, sumP[j * Co + o])));
+    }
+}
+
+inline int grid_for(int64_t total, int block) {
+    int64_t g = (total + block - 1) / block;
+    return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
+}
+
+// channels per LDS slice: the cloud's slice (words_per_elem x N x CS floats)
+// must fit EC_LDS_BYTES
+inline int slice_channels(int N, int words_per_elem) {
+    int cs = 32;
+    while (cs > 1 && (size_t)words_per_elem * N * cs * sizeof(float) > (size_t)EC_LDS_BYTES) cs >>= 1;
+    return cs;
+}
+
+// split the points of a cloud over `parts` workgroups so the grid reaches ~2
+// workgroups per CU (each restages the slice: redundancy = parts)
+inline int point_parts(int B, int slices, int N) {
+    int parts = 1;
+    while ((int64_t)B * slices * parts < 512 && parts * 64 < N) parts <<= 1;
+    return parts;
+}
+
+template <bool EVAL>
+int launch_gather(int cs, dim3 grid, size_t lds, hipStream_t st, const float* PQ, int ldpq, const int32_t* idx, int N,
+                  int k, int Co, int nparts, const float* sel, const float* shift, float slope, float* ysel,
+                  uint8_t* arg, float* sumP, float* partials, float* out, int ldo) {
+#define DGX_GATHER_CASE(CSV)                                                                                      \
+    case CSV:                                                                                                    \
+        hipLaunchKernelGGL((edge_gather_lds_kernel<CSV, EVAL>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, idx, N, \
+                           k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo);                \
+        break;
+    switch (cs) {
+        DGX_GATHER_CASE(32)
+        DGX_GATHER_CASE(16)
+        DGX_GATHER_CASE(8)
+        DGX_GATHER_CASE(4)
+        DGX_GATHER_CASE(2)
+        DGX_GATHER_CASE(1)
+        default: return DGX_EUNSUPPORTED;
+    }
+#undef DGX_GATHER_CASE
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+struct GatherGeom {
+    int cs, slices, parts;
+    size_t lds;
+};
+
+inline GatherGeom gather_geom(int B, int N, int Co) {
+    GatherGeom g;
+    g.cs = slice_channels(N, 1);
+    g.slices = (Co + g.cs - 1) / g.cs;
+    g.parts = point_parts(B, g.slices, N);
+    size_t stage = (size_t)N * g.cs * sizeof(float);
+    size_t red = 2 * EC_THREADS * sizeof(float);
+    g.lds = stage > red ? stage : red;
+    return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgx_edge_partials_rows(int B, int N, int Co) {
+    if (B < 1 || N < 1 || Co < 1) return DGX_EINVAL;
+    return B * gather_geom(B, N, Co).parts;
+}
+
+int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int Co,
+                            const float* gamma, float* ysel, uint8_t* arg, float* sumP, float* partials, int nrows,
+                            void* stream) {
+    if (!PQ || !idx || !gamma || !ysel || !arg || !sumP || !partials) return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
+    const GatherGeom g = gather_geom(B, N, Co);
+    if (nrows != B * g.parts) return DGX_EINVAL;
+    if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
+    return launch_gather<false>(g.cs, dim3(B * g.parts, g.slices), g.lds, dgx_stream(stream), PQ, ldpq, idx, N, k, Co,
+                                g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials, nullptr, 0);
+}
+
+int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int Co,
+                          const float* scale, const float* shift, float slope, float* out, int ldo, void* stream) {
+    if (!PQ || !idx || !scale || !shift || !out) return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || Co < 1 || ldpq < 2 * Co || ldo < Co) return DGX_EINVAL;
+    if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
+    const GatherGeom g = gather_geom(B, N, Co);
+    return launch_gather<true>(g.cs, dim3(B * g.parts, g.slices), g.lds, dgx_stream(stream), PQ, ldpq, idx, N, k, Co,
+                               g.parts, scale, shift, slope, nullptr, nullptr, nullptr, nullptr, out, ldo);
+}
+
+int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, double momentum, double eps,
+                        float* scale, float* shift, float* mean, float* invstd, void* stream) {
+    if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co, count,
+                       gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_bn_eval_affine_f32(int Co, const float* gamma, const float* beta, const float* running_mean,
+                           const float* running_var, double eps, float* scale, float* shift, void* stream) {
+    if (Co < 1 || !running_mean || !running_var || !scale || !shift) return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((Co + 255) / 256), dim3(256), 0, dgx_stream(stream), Co, gamma,
+                       beta, running_mean, running_var, eps, scale, shift);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale, const float* shift, float slope,
+                           float* out, int ldo, void* stream) {
+    if (!ysel || !scale || !shift || !out || M < 0 || Co < 1 || ldo < Co) return DGX_EINVAL;
+    const int64_t total = (int64_t)M * Co;
+    if (total == 0) return DGX_OK;
+    hipLaunchKernelGGL(bn_lrelu_apply_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), ysel, M,
+                       Co, scale, shift, slope, out, ldo);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, const uint8_t* arg, int M, int Co,
+                        const float* scale, const float* shift, const float* mean, const float* invstd, float slope,
+                        float* dzp, float* partials, int nrows, void* stream) {
+    if (!dY || !ysel || !arg || !scale || !shift || !mean || !invstd || !dzp || !partials) return DGX_EINVAL;
+    if (M < 1 || Co < 1 || lddy < Co || nrows < 1) return DGX_EINVAL;
+    const int rows = (M + nrows - 1) / nrows;
+    hipLaunchKernelGGL(edge_bwd_dz_kernel, dim3(nrows, (Co + 63) / 64), dim3(256), 0, dgx_stream(stream), dY, lddy,
+                       ysel, arg, M, Co, scale, shift, mean, invstd, slope, dzp, partials, rows);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co, double count, const float* scale,
+                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* c0,
+                            float* c1, int accumulate, void* stream) {
+    if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !mean || !invstd || !c0 || !c1)
+        return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
+                       count, scale, mean, invstd, dgamma, dbeta, c0, c1, accumulate);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_graph_reverse(const int32_t* idx, int B, int N, int k, int32_t* rowptr, int32_t* edges, void* stream) {
+    if (!idx || !rowptr || !edges || B < 1 || N < 1 || k < 1 || k > 64) return DGX_EINVAL;
+    if ((int64_t)B * N >= (1LL << 25)) return DGX_EUNSUPPORTED;
+    const size_t small = ((size_t)2 * N + 1024) * sizeof(int32_t);
+    const size_t full = small + (size_t)N * k * sizeof(int32_t);
+    if (small > 160 * 1024) return DGX_EUNSUPPORTED;
+    if (full <= 160 * 1024)
+        hipLaunchKernelGGL((rev_graph_kernel<true>), dim3(B), dim3(1024), full, dgx_stream(stream), idx, N, k, rowptr,
+                           edges);
+    else
+        hipLaunchKernelGGL((rev_graph_kernel<false>), dim3(B), dim3(1024), small, dgx_stream(stream), idx, N, k,
+                           rowptr, edges);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
+                             const float* dzp, const float* sumP, int B, int N, int k, int Co, const float* scale,
+                             const float* c0, const float* c1, float* dPQ, void* stream) {
+    if (!PQ || !rowptr || !edges || !dzp || !sumP || !scale || !c0 || !c1 || !dPQ) return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
+    const int cs = slice_channels(N, 2);
+    if ((size_t)2 * N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
+    const int slices = (Co + cs - 1) / cs;
+    const int parts = point_parts(B, slices, N);
+    const dim3 grid(B * parts, slices);
+    const size_t lds = (size_t)2 * N * cs * sizeof(float);
+    hipStream_t st = dgx_stream(stream);
+#define DGX_BWD_CASE(CSV)                                                                                         \
+    case CSV:                                                                                                    \
+        hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, edges, dzp, \
+                           sumP, N, k, Co, parts, scale, c0, c1, dPQ);                                            \
+        break;
+    switch (cs) {
+        DGX_BWD_CASE(32)
+        DGX_BWD_CASE(16)
+        DGX_BWD_CASE(8)
+        DGX_BWD_CASE(4)
+        DGX_BWD_CASE(2)
+        DGX_BWD_CASE(1)
+        default: return DGX_EUNSUPPORTED;
+    }
+#undef DGX_BWD_CASE
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+}  // extern "C"

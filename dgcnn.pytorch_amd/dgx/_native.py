@@ -33,24 +33,21 @@ _SIGS = {
     "dgx_knn_select_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
     "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
-    "dgx_edge_partials_blocks": [_i32, _i32, _i32],
+    "dgx_edge_partials_rows": [_i32, _i32, _i32],
     "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp],
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
     "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
-    "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
+    "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
-    "dgx_graph_reverse_workspace_bytes": [_i32, _i32, _i32],
-    "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
-    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp,
-                                 _vp, _vp],
+    "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {
     "dgx_version": ctypes.c_char_p,
     "dgx_strerror": ctypes.c_char_p,
     "dgx_knn_workspace_bytes": _sz,
-    "dgx_graph_reverse_workspace_bytes": _sz,
 }
 
 

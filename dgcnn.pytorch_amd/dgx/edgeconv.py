@@ -66,7 +66,6 @@ class _EdgeConvStack(torch.autograd.Function):
         stream = nat.stream_of(x)
         xcat = torch.empty((M, total), dtype=torch.float32, device=dev)
         x_pm = x.permute(0, 2, 1).reshape(M, C0)  # point-major input rows (copy only if needed)
-        nblk = L.dgx_edge_partials_blocks(B, N, max(widths))
         saved = []
         off_in = None
         count = float(M * k)
@@ -95,16 +94,17 @@ class _EdgeConvStack(torch.autograd.Function):
                     ysel = torch.empty((M, co), dtype=torch.float32, device=dev)
                     arg = torch.empty((M, co), dtype=torch.uint8, device=dev)
                     sumP = torch.empty((M, co), dtype=torch.float32, device=dev)
-                    partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
+                    prow = L.dgx_edge_partials_rows(B, N, co)
+                    partials = torch.empty((prow, 2, co), dtype=torch.float32, device=dev)
                     mean = torch.empty_like(scale)
                     invstd = torch.empty_like(scale)
                     nat.check(L.dgx_edge_fwd_gather_f32(
                         nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(gamma), nat.ptr(ysel),
-                        nat.ptr(arg), nat.ptr(sumP), nat.ptr(partials), nblk, stream), "edge gather")
+                        nat.ptr(arg), nat.ptr(sumP), nat.ptr(partials), prow, stream), "edge gather")
                     update = training and bn.running_mean is not None
                     factor = _bn_factor(bn) if update else 0.0
                     nat.check(L.dgx_bn_finalize_f32(
-                        nat.ptr(partials), nblk, co, count, nat.ptr(gamma), nat.ptr(beta),
+                        nat.ptr(partials), prow, co, count, nat.ptr(gamma), nat.ptr(beta),
                         nat.ptr(bn.running_mean) if update else None,
                         nat.ptr(bn.running_var) if update else None, factor, float(bn.eps),
                         nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), stream), "bn finalize")
@@ -150,8 +150,6 @@ class _EdgeConvStack(torch.autograd.Function):
         count = float(M * k)
         rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
         edges = torch.empty(M * k, dtype=torch.int32, device=dev)
-        rws = L.dgx_graph_reverse_workspace_bytes(B, N, k)
-        rev_ws = torch.empty(max(1, rws // 4), dtype=torch.int32, device=dev)
         for li in reversed(range(len(layers))):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
@@ -161,7 +159,7 @@ class _EdgeConvStack(torch.autograd.Function):
             X = x_pm if li == 0 else xcat[:, off - widths[li - 1]: off - widths[li - 1] + cin]
             dY = dxcat[:, off:off + co]
             nblk = max(1, min(1024, (M + 63) // 64))
-            dz = torch.empty((M, co), dtype=torch.float32, device=dev)
+            dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dz with packed slot
             partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
             dgamma = torch.empty(co, dtype=torch.float32, device=dev)
             dbeta = torch.empty(co, dtype=torch.float32, device=dev)
@@ -170,17 +168,17 @@ class _EdgeConvStack(torch.autograd.Function):
             dPQ = torch.empty((M, 2 * co), dtype=torch.float32, device=dev)
             with torch.cuda.device(dev):
                 nat.check(L.dgx_edge_bwd_dz_f32(
-                    nat.ptr(dY), total, nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift), nat.ptr(mean),
-                    nat.ptr(invstd), float(ly.slope), nat.ptr(dz), nat.ptr(partials), nblk, stream), "edge bwd dz")
+                    nat.ptr(dY), total, nat.ptr(ysel), nat.ptr(arg), M, co, nat.ptr(scale), nat.ptr(shift),
+                    nat.ptr(mean), nat.ptr(invstd), float(ly.slope), nat.ptr(dz), nat.ptr(partials), nblk, stream),
+                    "edge bwd dz")
                 nat.check(L.dgx_bn_bwd_finalize_f32(
                     nat.ptr(partials), nblk, co, count, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
                     nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
-                nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
-                                              nat.ptr(rev_ws), rws, stream), "reverse graph")
+                nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges), stream),
+                          "reverse graph")
                 nat.check(L.dgx_edge_bwd_scatter_f32(
-                    nat.ptr(PQ), 2 * co, nat.ptr(idx), nat.ptr(rowptr), nat.ptr(edges), nat.ptr(arg), nat.ptr(dz),
-                    nat.ptr(sumP), B, N, k, co, nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), stream),
-                    "edge bwd scatter")
+                    nat.ptr(PQ), 2 * co, nat.ptr(rowptr), nat.ptr(edges), nat.ptr(dz), nat.ptr(sumP), B, N, k, co,
+                    nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), stream), "edge bwd scatter")
             if _debug is not None:
                 _debug[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
                               "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.clone(), "partials": partials.clone(),

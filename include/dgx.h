@@ -84,23 +84,25 @@ int dgx_graph_feature_bwd_f32(const float* dout, int B, int C, int N,
  *   -> max(dim=-1)                        (models/dgcnn.py:54-73, 84-98)
  * With W = [W1 | W2] (Co x 2C), the conv on edge (i,j) is P_j + Q_i where
  * P = X W1^T, Q = X W2^T (point-major, computed by the caller's GEMM into one
- * buffer PQ (M x 2Co): columns [0,Co) = P, [Co,2Co) = Q).
+ * buffer PQ (M x 2Co, row stride ldpq): columns [0,Co) = P, [Co,2Co) = Q).
+ * idx: (B,N,k) int32 local neighbour indices from dgx_knn_*; M = B*N.
  *
  * Forward (training BN), three launches:
- *   dgx_edge_fwd_gather: per (i,o) max_k P (or min_k where gamma[o] < 0: BN's
- *     affine is decreasing there), its argument, sum_k P, and per-block partial
- *     (sum y, sum y^2) over all B*N*k edge outputs y = P_j + Q_i.
- *   dgx_bn_finalize: batch mean/var (biased) -> scale a, shift b; running
- *     stats updated with unbiased var (nn.BatchNorm semantics).
+ *   dgx_edge_fwd_gather: per (i,o) max_k P (min_k where gamma[o] < 0: BN's
+ *     affine is decreasing there), its slot `arg`, sum_k P `sumP`, and
+ *     per-row partial (sum y, sum y^2) over all B*N*k edge outputs y = P_j+Q_i
+ *     into partials (nrows x 2 x Co), nrows = dgx_edge_partials_rows(B,N,Co).
+ *   dgx_bn_finalize: batch mean/var (biased) -> scale a, shift b, mean,
+ *     invstd; running stats updated with unbiased var (nn.BatchNorm rules).
  *   dgx_bn_lrelu_apply: out[i,o] = LeakyReLU(a_o * ysel[i,o] + b_o), written
  *     with row stride ldo (straight into the caller's concat buffer,
  *     models/dgcnn.py:100). */
+int dgx_edge_partials_rows(int B, int N, int Co);
 int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx,
                             int B, int N, int k, int Co, const float* gamma,
                             float* ysel, uint8_t* arg, float* sumP,
-                            float* partials, int nblk_hint, void* stream);
-int dgx_edge_partials_blocks(int B, int N, int Co);
-int dgx_bn_finalize_f32(const float* partials, int nblk, int Co, double count,
+                            float* partials, int nrows, void* stream);
+int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         const float* gamma, const float* beta,
                         float* running_mean, float* running_var,
                         double momentum, double eps,
@@ -110,7 +112,7 @@ int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
                            const float* shift, float slope, float* out, int ldo,
                            void* stream);
 /* Eval-mode forward in one launch: out = LeakyReLU(a*sel + b), a,b from
- * running stats (caller computes them with dgx_bn_eval_affine_f32). */
+ * running stats (dgx_bn_eval_affine_f32). */
 int dgx_bn_eval_affine_f32(int Co, const float* gamma, const float* beta,
                            const float* running_mean, const float* running_var,
                            double eps, float* scale, float* shift, void* stream);
@@ -120,28 +122,29 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx,
                           void* stream);
 
 /* Backward of the block (autograd of dgcnn.py:84-98 through BN train mode):
- *   dgx_edge_bwd_dz: dz = dY * LeakyReLU'(z) at the selected edge, per-block
- *     partial (sum dz, sum dz*yhat) -> dgx_bn_bwd_finalize: dgamma, dbeta and
- *     the per-channel affine c0 + c1*y of BN's input gradient.
- *   dgx_graph_reverse: reverse kNN graph (CSR of in-edges per point).
- *   dgx_edge_bwd_scatter: dPQ (M x 2Co): dP_j = a*sum_{argmax edges->j} dz +
+ *   dgx_edge_bwd_dz: dz = dY * LeakyReLU'(z) at the selected edge, stored in
+ *     dzp (M x Co) with the selected slot packed into its 6 low mantissa bits
+ *     (relative perturbation <= 2^-17), and per-row partials (sum dz,
+ *     sum dz*yhat) -> dgx_bn_bwd_finalize: dgamma, dbeta (accumulate != 0
+ *     adds to them) and the per-channel affine c0 + c1*y of BN's input grad.
+ *   dgx_graph_reverse: reverse kNN graph: rowptr (M+1), edges (M*k), edge id
+ *     = (i << 6) | slot, lists sorted (deterministic summation order).
+ *   dgx_edge_bwd_scatter: dPQ (M x 2Co): dP_j = a*sum_{selected edges->j} dz +
  *     sum_{edges->j}(c0 + c1*y_e),  dQ_i = a*dz_i + k*c0 + c1*sum_k y_ik.
  * The caller's GEMMs then form dX += dPQ [W1;W2] and dW = dPQ^T X. */
-int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, int M,
-                        int Co, const float* scale, const float* shift,
-                        const float* mean, const float* invstd, float slope,
-                        float* dz, float* partials, int nblk_hint, void* stream);
-int dgx_bn_bwd_finalize_f32(const float* partials, int nblk, int Co,
+int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel,
+                        const uint8_t* arg, int M, int Co, const float* scale,
+                        const float* shift, const float* mean,
+                        const float* invstd, float slope, float* dzp,
+                        float* partials, int nrows, void* stream);
+int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co,
                             double count, const float* scale, const float* mean,
                             const float* invstd, float* dgamma, float* dbeta,
                             float* c0, float* c1, int accumulate, void* stream);
-size_t dgx_graph_reverse_workspace_bytes(int B, int N, int k);
 int dgx_graph_reverse(const int32_t* idx, int B, int N, int k,
-                      int32_t* rowptr, int32_t* edges, void* workspace,
-                      size_t workspace_bytes, void* stream);
-int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* idx,
-                             const int32_t* rowptr, const int32_t* edges,
-                             const uint8_t* arg, const float* dz,
+                      int32_t* rowptr, int32_t* edges, void* stream);
+int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
+                             const int32_t* edges, const float* dzp,
                              const float* sumP, int B, int N, int k, int Co,
                              const float* scale, const float* c0,
                              const float* c1, float* dPQ, void* stream);
