@@ -31,6 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "dgcnn.pytorch_amd"))
 
 from dgx import ops as dgx_ops  # noqa: E402
+from dgx import precision as dgx_prec  # noqa: E402
 from dgx import synth  # noqa: E402
 from dgx.edgeconv import edgeconv_stack  # noqa: E402
 from models.dgcnn import DGCNN  # noqa: E402
@@ -53,6 +54,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-eager-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=8, help="clouds in the CPU baseline sample")
+    p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
+                   help="GEMM operand precision (BASELINE cfg2 is bf16; fp32 is the parity mode)")
+    p.add_argument("--no-fp32-leg", action="store_true", help="skip the extra fp32-mode timing")
     return p.parse_args()
 
 
@@ -193,6 +197,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    dgx_prec.set(args.precision)
     torch.manual_seed(0)
     model = DGCNN(types.SimpleNamespace(emb_dim=args.emb, k=args.k)).to(dev).train()
     net = model
@@ -241,7 +246,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": args.precision,
         "data": "synthetic (splitmix64 uniform-cube clouds, random-init weights)",
         "config": {"workload": "DGCNN(emb=1024,k=20) train step fwd+bwd+SGD, cfg2",
                    "model": "DGCNN", "global_batch": args.batch * world, "points": args.points,
@@ -254,6 +259,17 @@ def main():
                      "avg_launch_ms": round(avg_ms, 4), "algorithmic_flops_per_launch": avg_flops,
                      "launches_timed": len(knn_ms), "knn_ms_by_layer": per_layer},
     }
+    if args.precision != "fp32" and not args.no_fp32_leg:
+        dgx_prec.set("fp32")  # same model, parity-mode GEMMs
+        for _ in range(2):
+            step()
+        el32 = timed_region(step, args.steps, world)
+        t32 = torch.tensor([el32], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t32, op=dist.ReduceOp.MAX)
+        result["fp32_mode"] = {"ms_per_step": round(float(t32.item()) / args.steps * 1e3, 3),
+                               "value": round(args.batch * world * args.steps / float(t32.item()), 2)}
+        dgx_prec.set(args.precision)
     if rank == 0 and world == 1:
         result["edgeconv_fwd_bwd_ms"] = round(edgeconv_only_ms(model, x), 3)
         if not args.no_eager_baseline:

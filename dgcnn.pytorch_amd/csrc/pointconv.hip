@@ -1,0 +1,210 @@
+// a4 — pointwise Conv(1x1) + BatchNorm + LeakyReLU on point-major features
+// (reference models/dgcnn.py:74-78, 100-102: conv5 over cat(x1..x4)).
+//
+// The GEMM Z = X W^T (M x Co, M = B*N points) is done by the caller; these
+// kernels are the memory-bound rest, each one pass over Z:
+//   colstats   per-row-block partial (sum z, sum z^2) per channel -> the
+//              shared bn_finalize (edgeconv.hip) turns them into a, b.
+//   apply_T    out(b, o, n) = LeakyReLU(a_o z(b*N+n, o) + b_o), transposed
+//              through a 64x64 LDS tile so both the point-major read and the
+//              channel-major (B,Co,N) write of the reference layout coalesce.
+//   bwd_T      dz = dout * LeakyReLU'(a z + b) read from (B,Co,N), written
+//              point-major, + partial (sum dz, sum dz*zhat)   [tile transpose]
+//   bwd_dZ     dZ = a*dz + c0 + c1*z (BN train-mode input gradient), written
+//              fp32 or bf16 (the operand of the caller's two weight GEMMs).
+#include "common.h"
+
+namespace {
+
+constexpr int PT = 64;  // tile edge (points x channels)
+
+__device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.f ? v : v * slope; }
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+// grid (nrows, ceil(C/64)), block 256: lanes over 64 channels, 4 waves over rows
+__global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__ Z, int ldz, int64_t M, int C,
+                                                       int rows_per_blk, float* __restrict__ partials) {
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int o = blockIdx.y * 64 + lane;
+    float s1 = 0.f, s2 = 0.f;
+    if (o < C) {
+        const int64_t i0 = (int64_t)blockIdx.x * rows_per_blk;
+        for (int r = wave; r < rows_per_blk; r += 4) {
+            const int64_t i = i0 + r;
+            if (i >= M) break;
+            const float z = Z[i * ldz + o];
+            s1 += z;
+            s2 = fmaf(z, z, s2);
+        }
+    }
+    red[0][wave][lane] = s1;
+    red[1][wave][lane] = s2;
+    __syncthreads();
+    if (wave == 0 && o < C) {
+        partials[(int64_t)blockIdx.x * 2 * C + o] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+        partials[(int64_t)blockIdx.x * 2 * C + C + o] = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    }
+}
+
+// grid (B * ceil(N/64), ceil(C/64)), block 256
+__global__ __launch_bounds__(256) void apply_T_kernel(const float* __restrict__ Z, int ldz, int N, int C,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, float slope,
+                                                      float* __restrict__ out) {
+    __shared__ float tile[PT][PT + 1];
+    const int ntile = (N + PT - 1) / PT;
+    const int b = blockIdx.x / ntile, n0 = (blockIdx.x - b * ntile) * PT, o0 = blockIdx.y * PT;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int o = o0 + tx;
+    const float a = o < C ? scale[o] : 0.f, sh = o < C ? shift[o] : 0.f;
+    for (int r = ty; r < PT; r += 4) {  // read 64 points x 64 channels, channel-contiguous
+        const int n = n0 + r;
+        tile[r][tx] = (n < N && o < C) ? lrelu(fmaf(a, Z[((int64_t)b * N + n) * ldz + o], sh), slope) : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < PT; r += 4) {  // write channel rows, point-contiguous
+        const int oo = o0 + r, n = n0 + tx;
+        if (oo < C && n < N) out[((int64_t)b * C + oo) * N + n] = tile[tx][r];
+    }
+}
+
+// dz (point-major) from dout (B,C,N); partial row = blockIdx.x (one 64-point tile)
+__global__ __launch_bounds__(256) void bwd_T_kernel(const float* __restrict__ dout, const float* __restrict__ Z,
+                                                    int ldz, int N, int C, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ invstd, float slope,
+                                                    float* __restrict__ dz, float* __restrict__ partials) {
+    __shared__ float tile[PT][PT + 1];
+    __shared__ float red[2][4][64];
+    const int ntile = (N + PT - 1) / PT;
+    const int b = blockIdx.x / ntile, n0 = (blockIdx.x - b * ntile) * PT, o0 = blockIdx.y * PT;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < PT; r += 4) {  // dout rows: channel o0+r, points n0..n0+63
+        const int oo = o0 + r, n = n0 + tx;
+        tile[tx][r] = (oo < C && n < N) ? dout[((int64_t)b * C + oo) * N + n] : 0.f;
+    }
+    __syncthreads();
+    const int o = o0 + tx;
+    float s1 = 0.f, s2 = 0.f;
+    if (o < C) {
+        const float a = scale[o], sh = shift[o], mu = mean[o], is = invstd[o];
+        for (int r = ty; r < PT; r += 4) {
+            const int n = n0 + r;
+            if (n >= N) break;
+            const int64_t i = (int64_t)b * N + n;
+            const float z = Z[i * ldz + o];
+            const float d = tile[r][tx] * (fmaf(a, z, sh) > 0.f ? 1.f : slope);
+            dz[i * C + o] = d;
+            s1 += d;
+            s2 = fmaf(d, (z - mu) * is, s2);
+        }
+    }
+    red[0][ty][tx] = s1;
+    red[1][ty][tx] = s2;
+    __syncthreads();
+    if (ty == 0 && o < C) {
+        partials[(int64_t)blockIdx.x * 2 * C + o] = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
+        partials[(int64_t)blockIdx.x * 2 * C + C + o] = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    }
+}
+
+template <bool BF16>
+__global__ void bwd_dZ_kernel(const float* __restrict__ dz, const float* __restrict__ Z, int ldz, int64_t M, int C,
+                              const float* __restrict__ scale, const float* __restrict__ c0,
+                              const float* __restrict__ c1, void* __restrict__ dZ) {
+    const int64_t total = M * C;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int o = (int)(t % C);
+        const int64_t i = t / C;
+        const float v = fmaf(scale[o], dz[t], fmaf(c1[o], Z[i * ldz + o], c0[o]));
+        if (BF16) static_cast<uint16_t*>(dZ)[t] = f32_to_bf16_rne(v);
+        else static_cast<float*>(dZ)[t] = v;
+    }
+}
+
+// fp32 -> bf16 (RNE) copy of a strided row-major matrix into a dense one
+__global__ void to_bf16_kernel(const float* __restrict__ src, int64_t lds_, int64_t rows, int cols,
+                               uint16_t* __restrict__ dst) {
+    const int64_t total = rows * cols;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / cols;
+        const int c = (int)(t - r * cols);
+        dst[t] = f32_to_bf16_rne(src[r * lds_ + c]);
+    }
+}
+
+inline int grid_for(int64_t total, int block) {
+    int64_t g = (total + block - 1) / block;
+    return (int)(g < 16384 ? (g < 1 ? 1 : g) : 16384);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgx_colstats_rows(int64_t M) {
+    if (M < 1) return DGX_EINVAL;
+    return (int)((M + 127) / 128);
+}
+
+int dgx_colstats_f32(const float* Z, int ldz, int64_t M, int C, float* partials, int nrows, void* stream) {
+    if (!Z || !partials || M < 1 || C < 1 || ldz < C || nrows != dgx_colstats_rows(M)) return DGX_EINVAL;
+    hipLaunchKernelGGL(colstats_kernel, dim3(nrows, (C + 63) / 64), dim3(256), 0, dgx_stream(stream), Z, ldz, M, C,
+                       128, partials);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_pointconv_apply_f32(const float* Z, int ldz, int B, int N, int C, const float* scale, const float* shift,
+                              float slope, float* out, void* stream) {
+    if (!Z || !scale || !shift || !out || B < 1 || N < 1 || C < 1 || ldz < C) return DGX_EINVAL;
+    dim3 grid(B * ((N + PT - 1) / PT), (C + PT - 1) / PT);
+    hipLaunchKernelGGL(apply_T_kernel, grid, dim3(256), 0, dgx_stream(stream), Z, ldz, N, C, scale, shift, slope, out);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_pointconv_bwd_rows(int B, int N) {
+    if (B < 1 || N < 1) return DGX_EINVAL;
+    return B * ((N + PT - 1) / PT);
+}
+
+int dgx_pointconv_bwd_f32(const float* dout, const float* Z, int ldz, int B, int N, int C, const float* scale,
+                            const float* shift, const float* mean, const float* invstd, float slope, float* dz,
+                            float* partials, void* stream) {
+    if (!dout || !Z || !scale || !shift || !mean || !invstd || !dz || !partials) return DGX_EINVAL;
+    if (B < 1 || N < 1 || C < 1 || ldz < C) return DGX_EINVAL;
+    dim3 grid(B * ((N + PT - 1) / PT), (C + PT - 1) / PT);
+    hipLaunchKernelGGL(bwd_T_kernel, grid, dim3(256), 0, dgx_stream(stream), dout, Z, ldz, N, C, scale, shift, mean,
+                       invstd, slope, dz, partials);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M, int C, const float* scale,
+                         const float* c0, const float* c1, void* dZ, int bf16, void* stream) {
+    if (!dz || !Z || !scale || !c0 || !c1 || !dZ || M < 1 || C < 1 || ldz < C) return DGX_EINVAL;
+    const int g = grid_for(M * C, 256);
+    if (bf16)
+        hipLaunchKernelGGL(bwd_dZ_kernel<true>, dim3(g), dim3(256), 0, dgx_stream(stream), dz, Z, ldz, M, C, scale, c0,
+                           c1, dZ);
+    else
+        hipLaunchKernelGGL(bwd_dZ_kernel<false>, dim3(g), dim3(256), 0, dgx_stream(stream), dz, Z, ldz, M, C, scale,
+                           c0, c1, dZ);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_to_bf16(const float* src, int64_t ld, int64_t rows, int cols, void* dst, void* stream) {
+    if (!src || !dst || rows < 0 || cols < 1 || ld < cols) return DGX_EINVAL;
+    if (rows == 0) return DGX_OK;
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, dgx_stream(stream), src, ld,
+                       rows, cols, static_cast<uint16_t*>(dst));
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+}  // extern "C"

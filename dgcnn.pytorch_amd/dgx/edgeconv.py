@@ -20,6 +20,7 @@ Backward per block (reverse order):
 import torch
 
 from . import _native as nat
+from . import precision as prec
 from .ops import knn_raw, reduction_order
 
 
@@ -82,7 +83,7 @@ class _EdgeConvStack(torch.autograd.Function):
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
                               strides=(N * total, 1, total), shape=(B, cin, N))
             wcat = _split_weight(w, cin, co)
-            PQ = torch.mm(X, wcat.t())  # (M, 2Co)
+            PQ = prec.mm(X, wcat.t())  # (M, 2Co) fp32 out
             off = sum(widths[:li])
             out = xcat[:, off:off + co]
             bn = ly.bn
@@ -187,15 +188,15 @@ class _EdgeConvStack(torch.autograd.Function):
                               "mean": mean.clone(), "invstd": invstd.clone(), "X": X.clone(),
                               "rowptr": rowptr.clone(), "edges": edges.clone()}
             wcat = _split_weight(w, cin, co)
-            dwcat = torch.mm(dPQ.t(), X)  # (2Co, C)
+            dwcat = prec.mm(dPQ.t(), X)  # (2Co, C)
             grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)
             grads[3 * li + 1] = dgamma
             grads[3 * li + 2] = dbeta
             if li > 0:
                 prev = off - widths[li - 1]
-                dxcat[:, prev:prev + cin].addmm_(dPQ, wcat)
+                dxcat[:, prev:prev + cin] += prec.mm(dPQ, wcat)
             elif ctx.x_needs_grad:
-                dx_in = torch.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
+                dx_in = prec.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
         return (dx_in, None, None, None, *grads)
 
 

@@ -1,0 +1,108 @@
+"""Pointwise Conv(1x1) + BatchNorm + LeakyReLU on point-major features.
+
+Replaces conv5 of reference models/dgcnn.py:74-78, 100-102: the reference
+concatenates x1..x4 into (B,512,N,1) and runs Conv2d -> BatchNorm2d ->
+LeakyReLU -> view(B,emb,N). Here the input is the EdgeConv chain's point-major
+concat buffer (B*N, 512) as is; Z = X W^T is one GEMM (precision.mm), BN
+statistics / affine / LeakyReLU and the transpose to the reference's (B,emb,N)
+layout are libdgx passes (pointconv.hip). BN follows nn.BatchNorm rules
+(biased batch var for normalisation, unbiased for running_var, momentum or
+cumulative average).
+"""
+import torch
+
+from . import _native as nat
+from . import precision as prec
+from .edgeconv import _bn_factor
+
+
+class _PointConvBNLReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, B, N, bn, slope, training, weight, gamma, beta):
+        L = nat.lib()
+        dev = X.device
+        stream = nat.stream_of(X)
+        M, K = X.shape
+        Co = weight.shape[0]
+        W = weight.reshape(Co, K)
+        Xop = prec.operand(X)
+        Z = prec.mm(Xop, prec.operand(W).t())  # (M, Co) fp32
+        scale = torch.empty(Co, dtype=torch.float32, device=dev)
+        shift = torch.empty_like(scale)
+        mean = torch.empty_like(scale)
+        invstd = torch.empty_like(scale)
+        out = torch.empty((B, Co, N), dtype=torch.float32, device=dev)
+        use_batch = training or bn.running_mean is None
+        with torch.cuda.device(dev):
+            if use_batch:
+                rows = L.dgx_colstats_rows(M)
+                partials = torch.empty((rows, 2, Co), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_colstats_f32(nat.ptr(Z), Co, M, Co, nat.ptr(partials), rows, stream), "colstats")
+                update = training and bn.running_mean is not None
+                factor = _bn_factor(bn) if update else 0.0
+                nat.check(L.dgx_bn_finalize_f32(
+                    nat.ptr(partials), rows, Co, float(M), nat.ptr(gamma), nat.ptr(beta),
+                    nat.ptr(bn.running_mean) if update else None, nat.ptr(bn.running_var) if update else None,
+                    factor, float(bn.eps), nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), stream),
+                    "bn finalize")
+            else:
+                nat.check(L.dgx_bn_eval_affine_f32(
+                    Co, nat.ptr(gamma), nat.ptr(beta), nat.ptr(bn.running_mean), nat.ptr(bn.running_var),
+                    float(bn.eps), nat.ptr(scale), nat.ptr(shift), stream), "bn eval affine")
+            nat.check(L.dgx_pointconv_apply_f32(nat.ptr(Z), Co, B, N, Co, nat.ptr(scale), nat.ptr(shift),
+                                                  float(slope), nat.ptr(out), stream), "pointconv apply")
+        ctx.meta = (B, N, float(slope), use_batch)
+        ctx.save_for_backward(Xop, W, Z, scale, shift, mean, invstd)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        Xop, W, Z, scale, shift, mean, invstd = ctx.saved_tensors
+        B, N, slope, use_batch = ctx.meta
+        L = nat.lib()
+        dev = Z.device
+        stream = nat.stream_of(Z)
+        M, Co = Z.shape
+        dout = dout.contiguous()
+        dz = torch.empty((M, Co), dtype=torch.float32, device=dev)
+        rows = L.dgx_pointconv_bwd_rows(B, N)
+        partials = torch.empty((rows, 2, Co), dtype=torch.float32, device=dev)
+        dgamma = torch.empty(Co, dtype=torch.float32, device=dev)
+        dbeta = torch.empty_like(dgamma)
+        c0 = torch.zeros_like(dgamma)
+        c1 = torch.zeros_like(dgamma)
+        bf16 = prec.get() == "bf16"
+        dZ = torch.empty((M, Co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            nat.check(L.dgx_pointconv_bwd_f32(nat.ptr(dout), nat.ptr(Z), Co, B, N, Co, nat.ptr(scale),
+                                                nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), slope, nat.ptr(dz),
+                                                nat.ptr(partials), stream), "pointconv bwd")
+            if use_batch:
+                nat.check(L.dgx_bn_bwd_finalize_f32(nat.ptr(partials), rows, Co, float(M), nat.ptr(scale),
+                                                    nat.ptr(mean), nat.ptr(invstd), nat.ptr(dgamma), nat.ptr(dbeta),
+                                                    nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
+            else:  # running-stats BN: affine only; dgamma needs z-hat of the running stats
+                sums = partials.sum(0)
+                dbeta.copy_(sums[0])
+                dgamma.copy_(sums[1])
+            nat.check(L.dgx_pointconv_input_grad(nat.ptr(dz), nat.ptr(Z), Co, M, Co, nat.ptr(scale), nat.ptr(c0),
+                                             nat.ptr(c1), nat.ptr(dZ), int(bf16), stream), "pointconv dZ")
+        Wop = prec.operand(W)
+        if bf16:
+            dW = torch.mm(dZ.t(), Xop, out_dtype=torch.float32)
+            dX = torch.mm(dZ, Wop, out_dtype=torch.float32)
+        else:
+            dW = torch.mm(dZ.t(), Xop)
+            dX = torch.mm(dZ, Wop)
+        return dX, None, None, None, None, None, dW.view(Co, -1, 1, 1), dgamma, dbeta
+
+
+def pointconv_bn_lrelu(X, B, N, seq, training):
+    """X (B*N, K) point-major -> (B, Co, N) = LeakyReLU(BN(Conv1x1(X))) with the
+    modules of ``seq`` = nn.Sequential(Conv2d(K,Co,1,bias=False), BatchNorm2d,
+    LeakyReLU) (reference dgcnn.py:74-78)."""
+    nat.require_device(X)
+    conv, bn, act = seq[0], seq[1], seq[2]
+    if conv.bias is not None or bn.weight is None:
+        raise NotImplementedError("dgx pointconv expects Conv(bias=False) + affine BatchNorm")
+    return _PointConvBNLReLU.apply(X, B, N, bn, act.negative_slope, training, conv.weight, bn.weight, bn.bias)

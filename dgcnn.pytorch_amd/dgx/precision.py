@@ -1,0 +1,41 @@
+"""GEMM operand precision of the engine.
+
+"fp32" (default): every GEMM in fp32 (f32 MFMA, exact f32 products) — the
+parity mode the tests hold to 1e-3 against the reference.
+"bf16": the per-point and conv5 GEMM operands are rounded to bf16, products
+accumulate in fp32 and outputs stay fp32 (BASELINE.json cfg2 "bf16"). kNN
+distances, BN statistics and every elementwise stage stay fp32 either way.
+
+Set with ``dgx.precision.set("bf16")`` or the environment variable
+``DGX_PRECISION=bf16``.
+"""
+import os
+
+import torch
+
+_mode = os.environ.get("DGX_PRECISION", "fp32").lower()
+if _mode not in ("fp32", "bf16"):
+    raise ValueError(f"DGX_PRECISION must be fp32 or bf16, got {_mode!r}")
+
+
+def get():
+    return _mode
+
+
+def set(mode):  # noqa: A001 (mirrors get)
+    global _mode
+    if mode not in ("fp32", "bf16"):
+        raise ValueError(mode)
+    _mode = mode
+
+
+def operand(t):
+    """GEMM operand in the current precision (bf16 copies are dense)."""
+    return t.to(torch.bfloat16) if _mode == "bf16" else t
+
+
+def mm(a, b):
+    """a @ b with fp32 output; bf16 operands when the mode says so."""
+    if _mode == "bf16":
+        return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
+    return torch.mm(a, b)

@@ -10,13 +10,14 @@ unchanged. The work runs in libdgx.so on the MI355X:
 * ``get_graph_feature`` -> gather kernel writing the reference's layout.
 * ``DGCNN.forward`` never materialises the (B,2C,N,k) edge tensors: the four
   EdgeConv blocks run as one fused chain (dgx.edgeconv), conv5 is a GEMM on
-  the concat buffer the chain writes in place.
+  the concat buffer the chain writes in place (dgx.pointconv).
 """
 import torch
 import torch.nn as nn
 
 from dgx import ops as _ops
 from dgx.edgeconv import edgeconv_stack
+from dgx.pointconv import pointconv_bn_lrelu
 
 
 def knn(x, k):
@@ -62,9 +63,6 @@ class DGCNN(nn.Module):
     def forward(self, x):
         batch_size, _, num_points = x.size()
         # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)
-        feats = edgeconv_stack(x, self.k, self.edge_blocks(), self.training)
-        feats = feats.view(batch_size, num_points, -1).transpose(1, 2)          # (B, 512, N) view
-        w5 = self.conv5[0].weight.view(self.emb_dims, -1)
-        z = torch.matmul(w5, feats)                                              # conv5 1x1, (B, emb, N)
-        z = self.conv5[2](self.conv5[1](z.unsqueeze(-1)))                        # BN2d + LeakyReLU
-        return z.view(batch_size, -1, num_points)
+        feats = edgeconv_stack(x, self.k, self.edge_blocks(), self.training)   # (B*N, 512)
+        # conv5 -> BN -> LeakyReLU (dgcnn.py:100-102), written as (B, emb, N)
+        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training)

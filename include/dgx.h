@@ -149,6 +149,36 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
                              const float* scale, const float* c0,
                              const float* c1, float* dPQ, void* stream);
 
+/* ---- a4: pointwise Conv1x1 + BatchNorm + LeakyReLU, replaces conv5 of
+ * models/dgcnn.py:74-78, 100-102 (cat(x1..x4) -> Conv2d(512,emb,1) -> BN ->
+ * LeakyReLU -> view(B,emb,N)). The caller's GEMM gives Z = X W^T point-major
+ * (M x C, row stride ldz); these passes finish the block:
+ *   dgx_colstats: per-row-block (sum z, sum z^2), nrows = dgx_colstats_rows(M)
+ *     -> dgx_bn_finalize_f32 (shared with a3) gives scale/shift/mean/invstd.
+ *   dgx_pointconv_apply: out (B,C,N) = LeakyReLU(a z + b), LDS-transposed.
+ *   dgx_pointconv_bwd: dz = dout * LeakyReLU'(a z + b) (dout (B,C,N)) into
+ *     dz (M x C) + partials (nrows = dgx_pointconv_bwd_rows(B,N)) ->
+ *     dgx_bn_bwd_finalize_f32 -> c0, c1.
+ *   dgx_pointconv_input_grad: dZ = a*dz + c0 + c1*z as fp32 or bf16 (bf16 != 0).
+ *   dgx_to_bf16: strided fp32 -> dense bf16 (RNE) operand copy. */
+int dgx_colstats_rows(int64_t M);
+int dgx_colstats_f32(const float* Z, int ldz, int64_t M, int C, float* partials,
+                     int nrows, void* stream);
+int dgx_pointconv_apply_f32(const float* Z, int ldz, int B, int N, int C,
+                              const float* scale, const float* shift,
+                              float slope, float* out, void* stream);
+int dgx_pointconv_bwd_rows(int B, int N);
+int dgx_pointconv_bwd_f32(const float* dout, const float* Z, int ldz, int B,
+                            int N, int C, const float* scale,
+                            const float* shift, const float* mean,
+                            const float* invstd, float slope, float* dz,
+                            float* partials, void* stream);
+int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M,
+                         int C, const float* scale, const float* c0,
+                         const float* c1, void* dZ, int bf16, void* stream);
+int dgx_to_bf16(const float* src, int64_t ld, int64_t rows, int cols, void* dst,
+                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -272,3 +272,36 @@ def test_dgcnn_full_size_train_step(cuda):
     for p in m.parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all()
     assert float(m.conv1[1].running_var.mean()) != 1.0
+
+
+def test_dgcnn_bf16_mode_routed(cuda):
+    """bf16 GEMM operands (BASELINE cfg2 precision): output and gradients stay
+    within bf16 operand rounding (3e-2) of the fp64 routed oracle."""
+    from dgx import precision, synth
+    from models.dgcnn import DGCNN
+    torch.manual_seed(7)
+    emb, N, k, B = 256, 512, 20, 2
+    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k))
+    init = {n: t.detach().clone() for n, t in m.state_dict().items()}
+    m = m.to(cuda).train()
+    pts = synth.cube_clouds(B, N, 77)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1)
+    precision.set("bf16")
+    try:
+        with Capture() as cap:
+            y = m(x)
+        gout = torch.from_numpy(synth.uniform(78, tuple(y.shape)) - 0.5)
+        y.backward(gout.to(cuda))
+    finally:
+        precision.set("fp32")
+    decisions = [tuple(t.cpu() for t in cap[("fwd", l)]) for l in range(4)]
+    decisions = [(i.long(), a, z) for (i, a, z) in decisions]
+    params = {n: (t.double() if t.is_floating_point() else t) for n, t in init.items()}
+    for n, t in params.items():
+        if t.is_floating_point() and "running" not in n:
+            t.requires_grad_(True)
+    ref = R.dgcnn_routed(torch.from_numpy(pts).double().permute(0, 2, 1), params, decisions, y.detach().cpu() > 0)
+    ref.backward(gout.double())
+    assert rel_err(y.detach().cpu(), ref.detach()) < 3e-2
+    for n, p in m.named_parameters():
+        assert rel_err(p.grad.cpu(), params[n].grad) < 3e-2, n

@@ -14,7 +14,7 @@ from conftest import REPO
 def _declared():
     with open(os.path.join(REPO, "include", "dgx.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"\b(dgx_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(dgx_[A-Za-z0-9_]+)\s*\(", src)))
 
 
 def test_header_symbols_exported():
