@@ -15,6 +15,9 @@ Fixtures
                      dbeta, running stats.
   dgcnn_small.npz    DGCNN(emb=64) train-mode fwd + bwd on (2,3,128), k=10.
   posemb_small.npz   PositionEmbedding fwd + bwd on (2,3,128), k=10.
+  partseg_small.npz  compute_hog_1x1 (model_partseg.py:15-92, use_cpu=True) on
+                     (2,3,128) k=10, and Net (emb=64, 1 block, dropout 0) fwd +
+                     bwd with its initial state_dict.
   hashes.json        SHA-256 of the canonical int32 kNN of the full-size bench
                      inputs (cfg2/cfg3/cfg5 first layer) + state_dict key lists.
 """
@@ -41,6 +44,7 @@ sys.dont_write_bytecode = True
 sys.path.insert(0, REF)
 from models.dgcnn import knn as ref_knn, get_graph_feature as ref_ggf, DGCNN as RefDGCNN  # noqa: E402
 from models.layers import PositionEmbedding as RefPosEmb  # noqa: E402
+import models.model_partseg as ref_partseg  # noqa: E402
 
 torch.set_num_threads(8)
 
@@ -174,6 +178,51 @@ def posemb_case():
                         gout=gy.numpy(), init_sha256=np.array(init_sha), **grads, **proj)
 
 
+PARTSEG_BIG = ("pos_mlp.0.conv3.0.weight", "pos_mlp.0.linear.0.weight")
+
+
+def partseg_big_init(i, shape):
+    """Deterministic init of the large PositionEmbedding weights (tests redo this)."""
+    return ((synth.uniform(63 + i, shape) - 0.5) * (2.0 / np.sqrt(shape[1]))).astype(np.float32)
+
+
+def partseg_case():
+    """HOG on its own, then a small Net. The reference's Net.forward calls
+    compute_hog_1x1 with use_cpu=False (.cuda()); for this CPU-only run the
+    module attribute is rebound in memory to the use_cpu=True variant."""
+    x = torch.from_numpy(synth.cube_clouds(2, 128, 61)).permute(0, 2, 1).contiguous()
+    hog = ref_partseg.compute_hog_1x1(x, 10, use_cpu=True)
+    orig = ref_partseg.compute_hog_1x1
+    ref_partseg.compute_hog_1x1 = lambda xx, k: orig(xx, k, use_cpu=True)
+    try:
+        torch.manual_seed(6)
+        args = types.SimpleNamespace(emb_dim=64, k=10, n_heads=4, n_blocks=1, ff_dims=128, dropout=0.0,
+                                     nclasses=50)
+        model = ref_partseg.Net(args).train()
+        with torch.no_grad():  # the two large weights come from the repo generator (not stored)
+            for i, n in enumerate(PARTSEG_BIG):
+                w = model.get_parameter(n)
+                w.copy_(torch.from_numpy(partseg_big_init(i, tuple(w.shape))))
+        state0 = {"init." + k_: v.detach().clone().numpy() for k_, v in model.state_dict().items()
+                  if k_ not in PARTSEG_BIG and k_.replace("bn3", "conv3.1") not in PARTSEG_BIG}
+        lbl = torch.zeros(2, 16)
+        lbl[0, 3] = 1
+        lbl[1, 11] = 1
+        y = model(x, lbl)
+        gy = torch.from_numpy(synth.uniform(62, tuple(y.shape)) - 0.5)
+        y.backward(gy)
+        grads = {"grad." + n: p.grad.numpy() for n, p in model.named_parameters()
+                 if p.grad is not None and n not in PARTSEG_BIG}
+        for i, n in enumerate(PARTSEG_BIG):
+            gr = model.get_parameter(n).grad.numpy().astype(np.float64)
+            r = synth.uniform(70 + i, gr.shape) - 0.5
+            grads["gradproj." + n] = np.array([(gr * r).sum(), np.linalg.norm(gr)])
+    finally:
+        ref_partseg.compute_hog_1x1 = orig
+    np.savez_compressed(os.path.join(HERE, "partseg_small.npz"), x=x.numpy(), hog=hog.numpy(), lbl=lbl.numpy(),
+                        out=y.detach().numpy(), gout=gy.numpy(), **state0, **grads)
+
+
 def hashes():
     res = {}
     for name, B, N, k, gen in (("cfg2_layer1", 32, 1024, 20, lambda: synth.cube_clouds(32, 1024, 0)),
@@ -201,11 +250,15 @@ def hashes():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["partseg"]:
+        partseg_case()
+        sys.exit(0)
     knn_cases()
     graph_feature_cases()
     edgeconv_block_case()
     dgcnn_case()
     posemb_case()
+    partseg_case()
     hashes()
     for f in sorted(os.listdir(HERE)):
         print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -1,0 +1,27 @@
+"""Standalone kNN kernel driver for profiling (cfg2 layer shapes)."""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "dgcnn.pytorch_amd")]
+from dgx import synth  # noqa: E402
+from dgx.ops import knn_raw  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+dev = torch.device("cuda:0")
+x3 = torch.from_numpy(synth.cube_clouds(32, 1024, 0)).to(dev).permute(0, 2, 1)
+f64 = torch.from_numpy(synth.relu_normal(3, (32, 64, 1024))).to(dev)
+f128 = torch.from_numpy(synth.relu_normal(4, (32, 128, 1024))).to(dev)
+for name, x in (("C3", x3), ("C64", f64), ("C128", f128)):
+    for _ in range(3):
+        knn_raw(x, 20, out_dtype=torch.int32)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        knn_raw(x, 20, out_dtype=torch.int32)
+    ev1.record()
+    torch.cuda.synchronize()
+    print(name, "%.1f us/call (incl. sqnorm)" % (ev0.elapsed_time(ev1) / reps * 1e3))
