@@ -101,3 +101,34 @@ def test_knn_errors(cuda):
         knn(x, 9)
     with pytest.raises(RuntimeError):
         knn(torch.zeros(1, 3, 8), 2)  # CPU tensors are not silently served
+
+
+def _lane_clustered(N, C, seed):
+    """Points whose index has (j >> 2) & 3 == 0 sit in a tight cluster, the rest
+    far away: every cluster query's true top-k lies in ONE of the kernel's four
+    per-lane candidate quarters, which overflows the per-lane lists and forces
+    the exact fix-up pass (knn_fix_kernel)."""
+    pts = synth.uniform(seed, (1, N, C)).astype(np.float32) * 100.0 + 50.0
+    near = ((np.arange(N) >> 2) & 3) == 0
+    pts[0, near] = synth.uniform(seed + 1, (int(near.sum()), C)).astype(np.float32) * 1e-2
+    return pts
+
+
+@pytest.mark.parametrize("C,N,k", [(3, 256, 20), (3, 1024, 40), (64, 512, 20), (128, 300, 64), (9, 2048, 16)])
+def test_knn_list_overflow_fixup(cuda, C, N, k):
+    from dgx.ops import knn_raw
+    pts = _lane_clustered(N, C, C + N)
+    for layout in ("bcn", "perm"):
+        idx, vals = knn_raw(_view(pts, layout, cuda), k, return_values=True)
+        ref_idx, ref_vals = oracle.knn(_cpu_view(pts, layout), k, return_values=True)
+        np.testing.assert_array_equal(idx.cpu().numpy(), ref_idx)
+        np.testing.assert_array_equal(vals.cpu().numpy(), ref_vals)
+
+
+def test_knn_all_points_equal(cuda):
+    """Every distance ties: the canonical answer is indices 0..k-1 for every row."""
+    from models.dgcnn import knn
+    pts = np.full((2, 300, 3), 0.25, np.float32)
+    idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
+    np.testing.assert_array_equal(idx, oracle.knn(_cpu_view(pts, "perm"), 20))
+    np.testing.assert_array_equal(idx[0, 7], np.arange(20))

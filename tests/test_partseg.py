@@ -88,13 +88,16 @@ def test_net_golden(golden, cuda):
     assert rel_err(y.detach().cpu(), g["out"]) < TOL
     y.backward(torch.from_numpy(g["gout"]).to(cuda))
     # gradients pass through max_k / LeakyReLU kinks: all but
-    # a few elements per tensor agree to 1e-3 of the tensor's scale
+    # a few elements per tensor agree to 1e-3 of the tensor's scale. Tensors
+    # whose true gradient is ~0 (e.g. attention.out_proj.bias: a BatchNorm in
+    # the head cancels any per-channel constant) use the model-wide scale.
     from dgx import synth
+    gscale = max(np.abs(g[k]).max() for k in g.files if k.startswith("grad."))
     for n, p in net.named_parameters():
         if "grad." + n in g.files:
             ref = g["grad." + n]
             got = p.grad.cpu().numpy()
-            close = (np.abs(got - ref) <= TOL * max(np.abs(ref).max(), 1e-6)).mean()
+            close = (np.abs(got - ref) <= TOL * max(np.abs(ref).max(), 1e-3 * gscale)).mean()
             assert close >= 0.98, (n, close)
         elif "gradproj." + n in g.files:
             i = BIG.index(n)
