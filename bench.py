@@ -57,6 +57,7 @@ def parse():
     p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
                    help="GEMM operand precision (BASELINE cfg2 is bf16; fp32 is the parity mode)")
     p.add_argument("--no-fp32-leg", action="store_true", help="skip the extra fp32-mode timing")
+    p.add_argument("--no-edgeconv-leg", action="store_true", help="skip the EdgeConv-only fwd+bwd timing")
     return p.parse_args()
 
 
@@ -271,7 +272,8 @@ def main():
                                "value": round(args.batch * world * args.steps / float(t32.item()), 2)}
         dgx_prec.set(args.precision)
     if rank == 0 and world == 1:
-        result["edgeconv_fwd_bwd_ms"] = round(edgeconv_only_ms(model, x), 3)
+        if not args.no_edgeconv_leg:
+            result["edgeconv_fwd_bwd_ms"] = round(edgeconv_only_ms(model, x), 3)
         if not args.no_eager_baseline:
             try:
                 ms = eager_reference_step_ms(x, args.k, args.emb)

@@ -27,10 +27,18 @@
 
 #include "common.h"
 
+#ifndef DGX_EXP
+#define DGX_EXP 0  // experiment switch for profiling builds (0 = product)
+#endif
+
 namespace {
 
 constexpr int EC_THREADS = 512;
-constexpr int EC_LDS_BYTES = 64 * 1024;   // per workgroup (2 workgroups per CU)
+constexpr int EC_LDS_BYTES = 64 * 1024;   // operand slices per workgroup (2 workgroups per CU)
+constexpr int GF_IPT = 8;                    // idx ints per thread per pass
+constexpr int GF_ICAP = GF_IPT * EC_THREADS;
+constexpr int GB_EPT = 6;                    // CSR edges per thread per pass (LDS total <= 80 KB)
+constexpr int GB_ECAP = GB_EPT * EC_THREADS;  // edges staged per pass (else read from HBM)
 
 __device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.f ? v : v * slope; }
 
@@ -41,6 +49,84 @@ __device__ __forceinline__ float pack_dz(float dz, int slot) {
 }
 __device__ __forceinline__ float unpack_dz(float p) { return __uint_as_float(__float_as_uint(p) & ~63u); }
 __device__ __forceinline__ int unpack_slot(float p) { return (int)(__float_as_uint(p) & 63u); }
+
+// V consecutive floats from LDS in one ds_read (b32 / b64 / b128).
+template <int V>
+__device__ __forceinline__ void lds_vec(const float* __restrict__ p, float (&r)[V]) {
+    if constexpr (V == 1) {
+        r[0] = p[0];
+    } else if constexpr (V == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p);
+        r[0] = t.x;
+        r[1] = t.y;
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; u += 4) {
+            const float4 t = *reinterpret_cast<const float4*>(p + u);
+            r[u] = t.x;
+            r[u + 1] = t.y;
+            r[u + 2] = t.z;
+            r[u + 3] = t.w;
+        }
+    }
+}
+
+// V consecutive floats / bytes to or from HBM in 16/8-byte accesses (the
+// caller guarantees V-alignment of the element offset and of the row stride).
+template <int V>
+__device__ __forceinline__ void gld_vec(const float* __restrict__ p, float (&r)[V]) {
+    if constexpr (V == 1) {
+        r[0] = p[0];
+    } else if constexpr (V == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p);
+        r[0] = t.x;
+        r[1] = t.y;
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; u += 4) {
+            const float4 t = *reinterpret_cast<const float4*>(p + u);
+            r[u] = t.x;
+            r[u + 1] = t.y;
+            r[u + 2] = t.z;
+            r[u + 3] = t.w;
+        }
+    }
+}
+template <int V>
+__device__ __forceinline__ void gst_vec(float* __restrict__ p, const float (&r)[V]) {
+    if constexpr (V == 1) {
+        p[0] = r[0];
+    } else if constexpr (V == 2) {
+        *reinterpret_cast<float2*>(p) = make_float2(r[0], r[1]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; u += 4)
+            *reinterpret_cast<float4*>(p + u) = make_float4(r[u], r[u + 1], r[u + 2], r[u + 3]);
+    }
+}
+template <int V>
+__device__ __forceinline__ void gst_u8(uint8_t* __restrict__ p, const int (&r)[V]) {
+    if constexpr (V == 1) {
+        p[0] = (uint8_t)r[0];
+    } else if constexpr (V == 2) {
+        *reinterpret_cast<uint16_t*>(p) = (uint16_t)(r[0] | (r[1] << 8));
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; u += 4)
+            *reinterpret_cast<uint32_t*>(p + u) =
+                (uint32_t)r[u] | ((uint32_t)r[u + 1] << 8) | ((uint32_t)r[u + 2] << 16) | ((uint32_t)r[u + 3] << 24);
+    }
+}
+
+// Work split inside a channel slice of CS channels: TPP threads per point,
+// V = CS / TPP consecutive channels per thread (one vector LDS read per
+// neighbour), PP_MAX points per pass.
+template <int CS>
+struct SliceSplit {
+    static constexpr int TPP = CS >= 4 ? 4 : CS;
+    static constexpr int V = CS / TPP;
+    static constexpr int PP_MAX = EC_THREADS / TPP;
+};
 
 // ------------------------------------------------------------- forward -----
 // grid (B * nparts, ceil(Co / CS)); partial-stat row = blockIdx.x.
@@ -82,76 +168,165 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     const float* __restrict__ sel_sign, const float* __restrict__ shift, float slope, float* __restrict__ ysel,
     uint8_t* __restrict__ arg, float* __restrict__ sumP, float* __restrict__ partials, float* __restrict__ out,
     int ldo) {
-    extern __shared__ float lds[];  // [N][CS] slice of P, then [2][EC_THREADS] reduction
+    constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V;
+    extern __shared__ float lds[];  // [N][CS] slice of P | idx rows of a pass; then the stat reduction
     const int b = blockIdx.x / nparts, part = blockIdx.x - b * nparts;
     const int o0 = blockIdx.y * CS;
     const int t = threadIdx.x;
     const int64_t base = (int64_t)b * N;
     const int per = (N + nparts - 1) / nparts;
     const int n_beg = part * per, n_end = min(N, n_beg + per);
+#if DGX_EXP != 2
     stage_slice<CS, EC_THREADS>(lds, PQ + base * ldpq, ldpq, N, o0, Co, (ldpq % 4) == 0 && (o0 % 4) == 0);
-    __syncthreads();
+#endif
 
-    const int c = t % CS;
-    const int o = o0 + c;
-    const bool ok = o < Co;
-    const bool k4 = (k & 3) == 0;
-    float acc1 = 0.f, acc2 = 0.f;
-    if (ok) {
-        const float sgn = sel_sign[o];
-        const bool take_min = sgn < 0.f;
-        for (int n = n_beg + t / CS; n < n_end; n += EC_THREADS / CS) {
-            const int64_t i = base + n;
-            const int32_t* __restrict__ row = idx + i * k;
-            float best = take_min ? INFINITY : -INFINITY, s = 0.f, s2 = 0.f;
-            int barg = 0;
-#define DGX_TAKE(J, K)                                                   \
-    {                                                                    \
-        const float v = lds[(J) * CS + c];                               \
-        const bool better = take_min ? v < best : v > best;              \
-        best = better ? v : best;                                        \
-        barg = better ? (K) : barg;                                      \
-        s += v;                                                          \
-        s2 = fmaf(v, v, s2);                                             \
+    // Pass = PP consecutive points; their idx rows (PP*k ints, contiguous in
+    // HBM) are staged in LDS, the next pass's rows prefetched into registers
+    // while the current pass computes.
+    const int PP = min(SliceSplit<CS>::PP_MAX, GF_ICAP / k);
+    int* gbuf = reinterpret_cast<int*>(lds + N * CS);
+    const int npass = n_end > n_beg ? (n_end - n_beg + PP - 1) / PP : 0;
+    const int gtot = PP * k;
+    int pre[GF_IPT];
+    auto load_rows = [&](int p) {
+        const int64_t r0 = (base + n_beg + (int64_t)p * PP) * k;
+        const int lim = (min(n_end, n_beg + (p + 1) * PP) - n_beg - p * PP) * k;
+#pragma unroll
+        for (int u = 0; u < GF_IPT; ++u) {
+            const int e = t + u * EC_THREADS;
+            pre[u] = (e < gtot && e < lim) ? idx[r0 + e] : 0;
+        }
+    };
+    auto store_rows = [&]() {
+#pragma unroll
+        for (int u = 0; u < GF_IPT; ++u) {
+            const int e = t + u * EC_THREADS;
+            if (e < gtot) gbuf[e] = pre[u];
+        }
+    };
+
+    const int tp = t % TPP, pl = t / TPP;
+    const int c0 = tp * V;          // first channel of this thread within the slice
+    float sgn[V], shv[V];
+    bool okc[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+        okc[u] = o0 + c0 + u < Co;
+        sgn[u] = okc[u] ? sel_sign[o0 + c0 + u] : 1.f;
+        shv[u] = (EVAL && okc[u]) ? shift[o0 + c0 + u] : 0.f;
     }
-            int kk = 0;
-            if (k4) {
-                for (; kk < k; kk += 4) {
-                    const int4 j4 = *reinterpret_cast<const int4*>(row + kk);
-                    DGX_TAKE(j4.x, kk) DGX_TAKE(j4.y, kk + 1) DGX_TAKE(j4.z, kk + 2) DGX_TAKE(j4.w, kk + 3)
+    // whole-vector HBM accesses when all V channels exist and rows stay aligned
+    const bool vec = okc[V - 1] && (Co % 4) == 0 && (ldpq % 4) == 0;
+    float acc1[V], acc2[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) { acc1[u] = 0.f; acc2[u] = 0.f; }
+    if (npass > 0) load_rows(0);
+    __syncthreads();  // slice staged
+    if (npass > 0) store_rows();
+    __syncthreads();
+    for (int p = 0; p < npass; ++p) {
+        if (p + 1 < npass) load_rows(p + 1);
+        const int n = n_beg + p * PP + pl;
+        if (pl < PP && n < n_end && okc[0]) {
+            const int64_t i = base + n;
+            const int* __restrict__ row = gbuf + pl * k;
+            float qv[V];  // HBM read issued before the neighbour loop
+            if (vec) {
+                gld_vec<V>(PQ + i * ldpq + Co + o0 + c0, qv);
+            } else {
+#pragma unroll
+                for (int u = 0; u < V; ++u) qv[u] = okc[u] ? PQ[i * ldpq + Co + o0 + c0 + u] : 0.f;
+            }
+            float best[V], s[V], s2[V];
+            int barg[V];
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                best[u] = sgn[u] < 0.f ? INFINITY : -INFINITY;
+                s[u] = 0.f;
+                s2[u] = 0.f;
+                barg[u] = 0;
+            }
+            auto take = [&](int j, int kk) {
+                float v[V];
+                lds_vec<V>(lds + j * CS + c0, v);
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    const bool better = sgn[u] < 0.f ? v[u] < best[u] : v[u] > best[u];
+                    best[u] = better ? v[u] : best[u];
+                    barg[u] = better ? kk : barg[u];
+                    s[u] += v[u];
+                    s2[u] = fmaf(v[u], v[u], s2[u]);
                 }
-            } else {
-                for (; kk < k; ++kk) DGX_TAKE(row[kk], kk)
+            };
+            int kk = 0;
+#if DGX_EXP == 1
+            kk = k;
+#endif
+            for (; kk + 4 <= k; kk += 4) {
+                const int j0 = row[kk], j1 = row[kk + 1], j2 = row[kk + 2], j3 = row[kk + 3];
+                take(j0, kk);
+                take(j1, kk + 1);
+                take(j2, kk + 2);
+                take(j3, kk + 3);
             }
-#undef DGX_TAKE
-            const float q = PQ[i * ldpq + Co + o];
-            const float y = best + q;
-            if (EVAL) {
-                out[i * ldo + o] = lrelu(fmaf(sgn, y, shift[o]), slope);
-            } else {
-                ysel[i * Co + o] = y;
-                arg[i * Co + o] = (uint8_t)barg;
-                sumP[i * Co + o] = s;
-                acc1 += fmaf((float)k, q, s);                     // sum_k y
-                acc2 += s2 + q * fmaf(2.f, s, (float)k * q);     // sum_k y^2
+            for (; kk < k; ++kk) take(row[kk], kk);
+            float yv[V];
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                const float q = qv[u];
+                yv[u] = best[u] + q;
+                if (EVAL) {
+                    yv[u] = lrelu(fmaf(sgn[u], yv[u], shv[u]), slope);
+                } else if (okc[u]) {
+                    acc1[u] += fmaf((float)k, q, s[u]);                      // sum_k y
+                    acc2[u] += s2[u] + q * fmaf(2.f, s[u], (float)k * q);    // sum_k y^2
+                }
             }
+            const int oc = o0 + c0;
+            if (vec && !EVAL) {
+                gst_vec<V>(ysel + i * Co + oc, yv);
+                gst_vec<V>(sumP + i * Co + oc, s);
+                gst_u8<V>(arg + i * Co + oc, barg);
+            } else if (vec && (ldo % 4) == 0) {
+                gst_vec<V>(out + i * ldo + oc, yv);
+            } else {
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    if (!okc[u]) continue;
+                    if (EVAL) {
+                        out[i * ldo + oc + u] = yv[u];
+                    } else {
+                        ysel[i * Co + oc + u] = yv[u];
+                        arg[i * Co + oc + u] = (uint8_t)barg[u];
+                        sumP[i * Co + oc + u] = s[u];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (p + 1 < npass) {
+            store_rows();
+            __syncthreads();
         }
     }
     if (EVAL) return;
-    // reduce the EC_THREADS/CS threads that share channel c
-    __syncthreads();
+    // reduce over the threads that share a channel: red[(2u + s)][thread]
     float* red = lds;
-    red[t] = acc1;
-    red[EC_THREADS + t] = acc2;
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+        red[(2 * u) * EC_THREADS + t] = acc1[u];
+        red[(2 * u + 1) * EC_THREADS + t] = acc2[u];
+    }
     __syncthreads();
-    if (t < CS && ok) {
-        float s1 = 0.f, s2 = 0.f;
-        for (int u = t; u < EC_THREADS; u += CS) {
-            s1 += red[u];
-            s2 += red[EC_THREADS + u];
+    if (t < CS && o0 + t < Co) {
+        const int tpc = t / V, uc = t % V;
+        float r1 = 0.f, r2 = 0.f;
+        for (int w = tpc; w < EC_THREADS; w += TPP) {
+            r1 += red[(2 * uc) * EC_THREADS + w];
+            r2 += red[(2 * uc + 1) * EC_THREADS + w];
         }
-        partials[(int64_t)blockIdx.x * 2 * Co + o] = s1;
-        partials[(int64_t)blockIdx.x * 2 * Co + Co + o] = s2;
+        partials[(int64_t)blockIdx.x * 2 * Co + o0 + t] = r1;
+        partials[(int64_t)blockIdx.x * 2 * Co + Co + o0 + t] = r2;
     }
 }
 
@@ -358,49 +533,143 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
     const float* __restrict__ dzp, const float* __restrict__ sumP, int N, int k, int Co, int nparts,
     const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
     float* __restrict__ dPQ) {
-    extern __shared__ float lds[];  // [N][CS] Q slice, [N][CS] packed dz
+    constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V, PP = SliceSplit<CS>::PP_MAX;
+    extern __shared__ float lds[];  // [N][CS] Q slice | [N][CS] packed dz | edges [GB_ECAP] | rowptr [PP+1]
     float* qs = lds;
     float* ds = lds + N * CS;
+    int* ebuf = reinterpret_cast<int*>(ds + N * CS);
+    int* rps = ebuf + GB_ECAP;
     const int b = blockIdx.x / nparts, part = blockIdx.x - b * nparts;
     const int o0 = blockIdx.y * CS;
     const int t = threadIdx.x;
     const int64_t base = (int64_t)b * N;
-    stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
-    stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
-    __syncthreads();
-    const int c = t % CS;
-    const int o = o0 + c;
-    if (o >= Co) return;
-    const float a = scale[o], k0 = c0[o], k1 = c1[o], kf = (float)k;
     const int per = (N + nparts - 1) / nparts;
     const int n_beg = part * per, n_end = min(N, n_beg + per);
-    const int32_t ibase = (int32_t)base;
-    for (int n = n_beg + t / CS; n < n_end; n += EC_THREADS / CS) {
-        const int64_t j = base + n;
-        const int32_t beg = rowptr[j], end = rowptr[j + 1];
-        float sq = 0.f, sd = 0.f;
-        int32_t u = beg;
-#define DGX_EDGE(E)                                                      \
-    {                                                                    \
-        const int il = ((E) >> 6) - ibase;                               \
-        sq += qs[il * CS + c];                                           \
-        const float p = ds[il * CS + c];                                 \
-        sd += unpack_slot(p) == ((E) & 63) ? unpack_dz(p) : 0.f;         \
+    const int npass = n_end > n_beg ? (n_end - n_beg + PP - 1) / PP : 0;
+
+    // The pass's in-edge lists (a contiguous CSR range) and row pointers are
+    // staged in LDS; the next pass's are prefetched into registers while the
+    // current pass computes. A pass with more than GB_ECAP in-edges (hubs)
+    // reads its lists from HBM instead.
+    int pe[GB_EPT], prp = 0, pre_lo = 0, pre_hi = 0;
+    auto load_pass = [&](int p) {
+        const int n0 = n_beg + p * PP, n1 = min(n_end, n0 + PP);
+        pre_lo = rowptr[base + n0];
+        pre_hi = rowptr[base + n1];
+        if (t <= PP) prp = rowptr[base + min(n0 + t, n1)];
+#pragma unroll
+        for (int u = 0; u < GB_EPT; ++u) {
+            const int e = pre_lo + t + u * EC_THREADS;
+            pe[u] = e < pre_hi ? edges[e] : 0;
+        }
+    };
+    auto store_pass = [&]() {
+#pragma unroll
+        for (int u = 0; u < GB_EPT; ++u) ebuf[t + u * EC_THREADS] = pe[u];
+        if (t <= PP) rps[t] = prp;
+    };
+
+    if (npass > 0) load_pass(0);
+#if DGX_EXP != 2
+    stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
+    stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+#endif
+    if (npass > 0) store_pass();
+    __syncthreads();
+    const int tp = t % TPP, pl = t / TPP;
+    const int cc = tp * V;
+    float a[V], k0[V], k1[V];
+    bool okc[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+        const int o = o0 + cc + u;
+        okc[u] = o < Co;
+        a[u] = okc[u] ? scale[o] : 0.f;
+        k0[u] = okc[u] ? c0[o] : 0.f;
+        k1[u] = okc[u] ? c1[o] : 0.f;
     }
-        for (; u + 4 <= end; u += 4) {
-            const int32_t e0 = edges[u], e1 = edges[u + 1], e2 = edges[u + 2], e3 = edges[u + 3];
-            DGX_EDGE(e0) DGX_EDGE(e1) DGX_EDGE(e2) DGX_EDGE(e3)
+    const bool vec = okc[V - 1] && (Co % 4) == 0 && (ldpq % 4) == 0;
+    const float kf = (float)k;
+    const int32_t ibase = (int32_t)base;
+    for (int p = 0; p < npass; ++p) {
+        const int lo = pre_lo, hi = pre_hi;
+        if (p + 1 < npass) load_pass(p + 1);
+        const int n = n_beg + p * PP + pl;
+        if (okc[0] && n < n_end) {
+            const int64_t j = base + n;
+            const int32_t beg = rps[pl] - lo, end = rps[pl + 1] - lo;
+            const int* __restrict__ el = (hi - lo <= GB_ECAP) ? ebuf : edges + lo;
+            float pjv[V], spv[V];  // HBM reads issued before the edge loop hides their latency
+            if (vec) {
+                gld_vec<V>(PQ + j * ldpq + o0 + cc, pjv);
+                gld_vec<V>(sumP + j * Co + o0 + cc, spv);
+            } else {
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    pjv[u] = okc[u] ? PQ[j * ldpq + o0 + cc + u] : 0.f;
+                    spv[u] = okc[u] ? sumP[j * Co + o0 + cc + u] : 0.f;
+                }
+            }
+            float sq[V], sd[V];
+#pragma unroll
+            for (int u = 0; u < V; ++u) { sq[u] = 0.f; sd[u] = 0.f; }
+            auto edge = [&](int32_t e) {
+                const int il = (e >> 6) - ibase, slot = e & 63;
+                float q[V], d[V];
+                lds_vec<V>(qs + il * CS + cc, q);
+                lds_vec<V>(ds + il * CS + cc, d);
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    sq[u] += q[u];
+                    sd[u] += unpack_slot(d[u]) == slot ? unpack_dz(d[u]) : 0.f;
+                }
+            };
+            int32_t u0 = beg;
+#if DGX_EXP == 1
+            u0 = end;
+#endif
+            for (; u0 + 8 <= end; u0 += 8) {
+                int32_t e[8];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) e[w] = el[u0 + w];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) edge(e[w]);
+            }
+            for (; u0 + 4 <= end; u0 += 4) {
+                const int32_t e0 = el[u0], e1 = el[u0 + 1], e2 = el[u0 + 2], e3 = el[u0 + 3];
+                edge(e0);
+                edge(e1);
+                edge(e2);
+                edge(e3);
+            }
+            for (; u0 < end; ++u0) edge(el[u0]);
+            const float deg = (float)(end - beg);
+            float qn[V], dn[V];
+            lds_vec<V>(qs + n * CS + cc, qn);
+            lds_vec<V>(ds + n * CS + cc, dn);
+            float dp[V], dq[V];
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
+                dq[u] = fmaf(a[u], unpack_dz(dn[u]), fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
+            }
+            if (vec) {
+                gst_vec<V>(dPQ + j * 2 * Co + o0 + cc, dp);
+                gst_vec<V>(dPQ + j * 2 * Co + Co + o0 + cc, dq);
+            } else {
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    if (!okc[u]) continue;
+                    dPQ[j * 2 * Co + o0 + cc + u] = dp[u];
+                    dPQ[j * 2 * Co + Co + o0 + cc + u] = dq[u];
+                }
+            }
         }
-        for (; u < end; ++u) {
-            const int32_t e0 = edges[u];
-            DGX_EDGE(e0)
+        __syncthreads();
+        if (p + 1 < npass) {
+            store_pass();
+            __syncthreads();
         }
-#undef DGX_EDGE
-        const float deg = (float)(end - beg);
-        const float pj = PQ[j * ldpq + o];
-        const float qj = qs[n * CS + c];
-        dPQ[j * 2 * Co + o] = fmaf(a, sd, fmaf(k0, deg, k1 * fmaf(deg, pj, sq)));
-        dPQ[j * 2 * Co + Co + o] = fmaf(a, unpack_dz(ds[n * CS + c]), fmaf(k0, kf, k1 * fmaf(kf, qj, sumP[j * Co + o])));
     }
 }
 
@@ -457,8 +726,9 @@ inline GatherGeom gather_geom(int B, int N, int Co) {
     g.cs = slice_channels(N, 1);
     g.slices = (Co + g.cs - 1) / g.cs;
     g.parts = point_parts(B, g.slices, N);
-    size_t stage = (size_t)N * g.cs * sizeof(float);
-    size_t red = 2 * EC_THREADS * sizeof(float);
+    size_t stage = (size_t)N * g.cs * sizeof(float) + GF_ICAP * sizeof(int);
+    const int v = g.cs >= 4 ? g.cs / 4 : 1;
+    size_t red = (size_t)2 * v * EC_THREADS * sizeof(float);
     g.lds = stage > red ? stage : red;
     return g;
 }
@@ -567,7 +837,7 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, c
     const int slices = (Co + cs - 1) / cs;
     const int parts = point_parts(B, slices, N);
     const dim3 grid(B * parts, slices);
-    const size_t lds = (size_t)2 * N * cs * sizeof(float);
+    const size_t lds = (size_t)2 * N * cs * sizeof(float) + (GB_ECAP + EC_THREADS + 1) * sizeof(int);
     hipStream_t st = dgx_stream(stream);
 #define DGX_BWD_CASE(CSV)                                                                                         \
     case CSV:                                                                                                    \

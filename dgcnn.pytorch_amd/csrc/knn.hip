@@ -72,9 +72,13 @@ constexpr int SQ_THREADS = 64;
 __device__ __forceinline__ float sqnorm_point(const float* __restrict__ p, int64_t sC, int C, int order,
                                               bool tail, float* sq) {
 #pragma clang fp contract(off)
-    for (int c = 0; c < C; ++c) {
-        float v = p[c * sC];
-        sq[c * SQ_THREADS] = v * v;
+    for (int c0 = 0; c0 < C; c0 += 16) {  // 16 loads in flight per thread
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = c0 + u < C ? p[(c0 + u) * sC] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (c0 + u < C) sq[(c0 + u) * SQ_THREADS] = v[u] * v[u];
     }
     if (order == DGX_ORDER_VEC8X4) {
         if (C < 8) return rowsum4(sq, SQ_THREADS, C);
