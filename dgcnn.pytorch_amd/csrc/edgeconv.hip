@@ -25,6 +25,8 @@
 // compulsory M*Co*(bytes) instead of M*k*Co*(bytes).
 #include <math.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 #ifndef DGX_EXP
@@ -115,6 +117,19 @@ __device__ __forceinline__ void gst_u8(uint8_t* __restrict__ p, const int (&r)[V
         for (int u = 0; u < V; u += 4)
             *reinterpret_cast<uint32_t*>(p + u) =
                 (uint32_t)r[u] | ((uint32_t)r[u + 1] << 8) | ((uint32_t)r[u + 2] << 16) | ((uint32_t)r[u + 3] << 24);
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void gst_bf16(__bf16* __restrict__ p, const float (&r)[V]) {
+    typedef __bf16 h4 __attribute__((ext_vector_type(4)));
+    if constexpr (V % 4 == 0) {
+#pragma unroll
+        for (int u = 0; u < V; u += 4) *reinterpret_cast<h4*>(p + u) = h4{(__bf16)r[u], (__bf16)r[u + 1],
+                                                                          (__bf16)r[u + 2], (__bf16)r[u + 3]};
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; ++u) p[u] = (__bf16)r[u];
     }
 }
 
@@ -380,15 +395,20 @@ __global__ void bn_eval_affine_kernel(int Co, const float* __restrict__ gamma, c
     shift[o] = (beta ? beta[o] : 0.f) - rmean[o] * a;
 }
 
+// out16 (optional): the same values rounded to bf16 (RNE) at the same
+// position of a bf16 twin of the output buffer — the GEMM operand copy of the
+// concat buffer, written here so no conversion pass re-reads HBM.
 __global__ void bn_lrelu_apply_kernel(const float* __restrict__ ysel, int M, int Co,
                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                      float slope, float* __restrict__ out, int ldo) {
+                                      float slope, float* __restrict__ out, int ldo, __bf16* __restrict__ out16) {
     const int64_t total = (int64_t)M * Co;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
         const int o = (int)(t % Co);
         const int64_t i = t / Co;
-        out[i * ldo + o] = lrelu(fmaf(scale[o], ysel[t], shift[o]), slope);
+        const float v = lrelu(fmaf(scale[o], ysel[t], shift[o]), slope);
+        out[i * ldo + o] = v;
+        if (out16) out16[i * ldo + o] = (__bf16)v;
     }
 }
 
@@ -461,78 +481,154 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     c1[o] = (float)(-a * g2 * is);
 }
 
-// Reverse kNN graph, one workgroup per cloud (in-edges stay inside a cloud):
-// count -> scan -> fill with LDS atomics, then every list sorted by edge id so
-// the backward's summation order is deterministic. Edge id = (i << 6) | slot.
-// With LDS_LISTS the cloud's N*k edge ids are built and sorted in LDS and
-// written out once (coalesced); otherwise they are sorted in place in HBM.
-template <bool LDS_LISTS>
-__global__ __launch_bounds__(1024) void rev_graph_kernel(const int32_t* __restrict__ idx, int N, int k,
-                                                         int32_t* __restrict__ rowptr, int32_t* __restrict__ edges) {
-    extern __shared__ int32_t cnt[];  // [N] counts -> cursors | [N] list starts | [1024] scan | [N*k] lists
-    int32_t* start = cnt + N;
-    int32_t* scan = start + N;
-    int32_t* lists = scan + 1024;
-    const int b = blockIdx.x, t = threadIdx.x;
+// Reverse graph, parallel form: P workgroups per cloud, workgroup p owns the
+// targets j in [p*R, p*R + R). It reads the cloud's whole index list (L2
+// resident), counts its own targets' in-edges and the edges that land before
+// its range (its global list offset), places edge ids with LDS atomics, then
+// orders every list by a rank sort (rank = number of smaller ids in the same
+// list: independent LDS reads, no serial chain), so the lists come out
+// ascending and the backward's summation order is deterministic. A workgroup
+// whose range holds more than RG_CAP edges (degenerate clouds, e.g. all points
+// equal) places them in HBM and sorts each list there instead.
+constexpr int RG_THREADS = 512;
+constexpr int RG_CAP = 12288;
+constexpr int RG_U = 8;  // independent index loads in flight per thread
+
+__device__ __forceinline__ int32_t block_sum_rg(int32_t v, int32_t* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    int32_t t = 0;
+    for (int u = 0; u < RG_THREADS / 64; ++u) t += red[u];
+    return t;
+}
+
+__global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(const int32_t* __restrict__ idx, int N, int k,
+                                                                   int P, int cap, int32_t* __restrict__ rowptr,
+                                                                   int32_t* __restrict__ edges) {
+    extern __shared__ int32_t rg[];
+    const int R = (N + P - 1) / P;
+    int32_t* cnt = rg;                 // [R] in-degree -> fill cursor
+    int32_t* start = cnt + R;          // [R] local list starts
+    int32_t* red = start + R;          // [RG_THREADS / 64 + 2]
+    int32_t* list = red + RG_THREADS / 64 + 2;   // [cap] edge ids
+    int32_t* ltg = list + cap;                    // [cap] local target of each slot
+    const int b = blockIdx.x / P, p = blockIdx.x - b * P;
+    const int t = threadIdx.x;
+    const int j0 = p * R, j1 = min(N, j0 + R), nr = max(0, j1 - j0);
     const int64_t base = (int64_t)b * N;
     const int32_t* __restrict__ ib = idx + base * k;
+    const int E = N * k;
     const int32_t ebase = (int32_t)(base * k);
-    int32_t* out = LDS_LISTS ? lists : edges + ebase;
-    for (int n = t; n < N; n += 1024) cnt[n] = 0;
+    for (int r = t; r < nr; r += RG_THREADS) cnt[r] = 0;
     __syncthreads();
-    for (int e = t; e < N * k; e += 1024) atomicAdd(&cnt[ib[e]], 1);
-    __syncthreads();
-    const int per = (N + 1023) / 1024;
-    const int lo = min(N, t * per), hi = min(N, lo + per);
-    int32_t s = 0;
-    for (int n = lo; n < hi; ++n) s += cnt[n];
-    scan[t] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int32_t v = t >= off ? scan[t - off] : 0;
-        __syncthreads();
-        scan[t] += v;
-        __syncthreads();
-    }
-    int32_t run = (t == 0 ? 0 : scan[t - 1]);
-    for (int n = lo; n < hi; ++n) {
-        const int32_t c = cnt[n];
-        rowptr[base + n] = ebase + run;
-        start[n] = run;
-        cnt[n] = run;  // fill cursor
-        run += c;
-    }
-    if (b == gridDim.x - 1 && t == 0) rowptr[base + N] = (int32_t)((base + N) * k);
-    __syncthreads();
-    for (int e = t; e < N * k; e += 1024) {
-        const int32_t pos = atomicAdd(&cnt[ib[e]], 1);
-        out[pos] = ((int32_t)(base + e / k) << 6) | (e % k);
-    }
-    __syncthreads();
-    for (int n = t; n < N; n += 1024) {  // insertion sort of each (short) list
-        const int32_t beg = start[n], end = cnt[n];
-        for (int32_t a = beg + 1; a < end; ++a) {
-            const int32_t v = out[a];
-            int32_t p = a - 1;
-            while (p >= beg && out[p] > v) { out[p + 1] = out[p]; --p; }
-            out[p + 1] = v;
+    int32_t before = 0;
+    // the cloud's index list is read in batches of RG_U independent loads per
+    // thread (a dependent load per iteration would leave the loop latency-bound)
+    for (int e0 = 0; e0 < E; e0 += RG_U * RG_THREADS) {
+        int32_t jv[RG_U];
+#pragma unroll
+        for (int u = 0; u < RG_U; ++u) {
+            const int e = e0 + u * RG_THREADS + t;
+            jv[u] = e < E ? ib[e] : INT32_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < RG_U; ++u) {
+            const int j = jv[u];
+            if (j < j0) ++before;
+            else if (j < j1) atomicAdd(&cnt[j - j0], 1);
         }
     }
-    if (LDS_LISTS) {
-        __syncthreads();
-        for (int e = t; e < N * k; e += 1024) edges[ebase + e] = lists[e];
+    before = block_sum_rg(before, red);
+    // exclusive scan of cnt over the range: thread-contiguous chunks + block scan of chunk sums
+    const int per = (nr + RG_THREADS - 1) / RG_THREADS;
+    const int lo = min(nr, t * per), hi = min(nr, lo + per);
+    int32_t s = 0;
+    for (int r = lo; r < hi; ++r) s += cnt[r];
+    // block exclusive scan of s (wave scan + wave totals)
+    const int lane = t & 63, w = t >> 6;
+    int32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t v = __shfl_up(inc, o);
+        if (lane >= o) inc += v;
+    }
+    __syncthreads();
+    if (lane == 63) red[w] = inc;
+    __syncthreads();
+    int32_t wofs = 0;
+    for (int u = 0; u < w; ++u) wofs += red[u];
+    int32_t total = 0;
+    for (int u = 0; u < RG_THREADS / 64; ++u) total += red[u];
+    int32_t run = wofs + inc - s;
+    for (int r = lo; r < hi; ++r) {
+        const int32_t c = cnt[r];
+        rowptr[base + j0 + r] = ebase + before + run;
+        start[r] = run;
+        cnt[r] = run;  // fill cursor
+        run += c;
+    }
+    if (b == (int)(gridDim.x / P) - 1 && p == P - 1 && t == 0) rowptr[base + N] = (int32_t)((base + N) * k);
+    __syncthreads();
+    const bool in_lds = total <= cap;
+    int32_t* out = in_lds ? list : edges + ebase + before;
+    for (int e0 = 0; e0 < E; e0 += RG_U * RG_THREADS) {
+        int32_t jv[RG_U];
+#pragma unroll
+        for (int u = 0; u < RG_U; ++u) {
+            const int e = e0 + u * RG_THREADS + t;
+            jv[u] = e < E ? ib[e] : INT32_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < RG_U; ++u) {
+            const int j = jv[u];
+            if (j >= j0 && j < j1) {
+                const int e = e0 + u * RG_THREADS + t;
+                const int32_t pos = atomicAdd(&cnt[j - j0], 1);
+                out[pos] = ((int32_t)(base + e / k) << 6) | (e % k);
+                if (in_lds) ltg[pos] = j - j0;
+            }
+        }
+    }
+    __syncthreads();
+    if (in_lds) {
+        int32_t* dst = edges + ebase + before;
+        for (int q = t; q < total; q += RG_THREADS) {
+            const int32_t a = list[q];
+            const int r = ltg[q];
+            const int32_t beg = start[r], end = cnt[r];
+            int32_t rank = 0;
+            for (int32_t u = beg; u < end; ++u) rank += list[u] < a ? 1 : 0;
+            dst[beg + rank] = a;
+        }
+    } else {
+        for (int r = t; r < nr; r += RG_THREADS) {  // degenerate range: insertion sort in HBM
+            const int32_t beg = start[r], end = cnt[r];
+            for (int32_t a = beg + 1; a < end; ++a) {
+                const int32_t v = out[a];
+                int32_t q = a - 1;
+                while (q >= beg && out[q] > v) { out[q + 1] = out[q]; --q; }
+                out[q + 1] = v;
+            }
+        }
     }
 }
 
 // dPQ for every point: grid (B * nparts, ceil(Co / CS)). The cloud's Q slice
 // and packed dz|slot slice live in LDS; each (point, channel) thread walks
 // the point's in-edges.
-template <int CS>
+template <int CS, bool OUT16>
 __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
     const float* __restrict__ dzp, const float* __restrict__ sumP, int N, int k, int Co, int nparts,
     const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
-    float* __restrict__ dPQ) {
+    void* __restrict__ dPQv) {
+    // dPQ fp32, or bf16 when it only feeds the bf16 GEMMs (dX, dW)
+    float* __restrict__ dPQ = static_cast<float*>(dPQv);
+    __bf16* __restrict__ dPQh = static_cast<__bf16*>(dPQv);
     constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V, PP = SliceSplit<CS>::PP_MAX;
     extern __shared__ float lds[];  // [N][CS] Q slice | [N][CS] packed dz | edges [GB_ECAP] | rowptr [PP+1]
     float* qs = lds;
@@ -653,7 +749,17 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
                 dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
                 dq[u] = fmaf(a[u], unpack_dz(dn[u]), fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
             }
-            if (vec) {
+            if (OUT16 && vec) {
+                gst_bf16<V>(dPQh + j * 2 * Co + o0 + cc, dp);
+                gst_bf16<V>(dPQh + j * 2 * Co + Co + o0 + cc, dq);
+            } else if (OUT16) {
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    if (!okc[u]) continue;
+                    dPQh[j * 2 * Co + o0 + cc + u] = (__bf16)dp[u];
+                    dPQh[j * 2 * Co + Co + o0 + cc + u] = (__bf16)dq[u];
+                }
+            } else if (vec) {
                 gst_vec<V>(dPQ + j * 2 * Co + o0 + cc, dp);
                 gst_vec<V>(dPQ + j * 2 * Co + Co + o0 + cc, dq);
             } else {
@@ -782,12 +888,12 @@ int dgx_bn_eval_affine_f32(int Co, const float* gamma, const float* beta, const 
 }
 
 int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale, const float* shift, float slope,
-                           float* out, int ldo, void* stream) {
+                           float* out, int ldo, void* out_bf16, void* stream) {
     if (!ysel || !scale || !shift || !out || M < 0 || Co < 1 || ldo < Co) return DGX_EINVAL;
     const int64_t total = (int64_t)M * Co;
     if (total == 0) return DGX_OK;
     hipLaunchKernelGGL(bn_lrelu_apply_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), ysel, M,
-                       Co, scale, shift, slope, out, ldo);
+                       Co, scale, shift, slope, out, ldo, static_cast<__bf16*>(out_bf16));
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -815,21 +921,22 @@ int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co, double cou
 int dgx_graph_reverse(const int32_t* idx, int B, int N, int k, int32_t* rowptr, int32_t* edges, void* stream) {
     if (!idx || !rowptr || !edges || B < 1 || N < 1 || k < 1 || k > 64) return DGX_EINVAL;
     if ((int64_t)B * N >= (1LL << 25)) return DGX_EUNSUPPORTED;
-    const size_t small = ((size_t)2 * N + 1024) * sizeof(int32_t);
-    const size_t full = small + (size_t)N * k * sizeof(int32_t);
-    if (small > 160 * 1024) return DGX_EUNSUPPORTED;
-    if (full <= 160 * 1024)
-        hipLaunchKernelGGL((rev_graph_kernel<true>), dim3(B), dim3(1024), full, dgx_stream(stream), idx, N, k, rowptr,
-                           edges);
-    else
-        hipLaunchKernelGGL((rev_graph_kernel<false>), dim3(B), dim3(1024), small, dgx_stream(stream), idx, N, k,
-                           rowptr, edges);
+    // workgroups per cloud: enough to fill the chip and to keep a range's
+    // edges (about N*k/P) well inside the LDS list capacity
+    int P = 1;
+    while (P < N && ((int64_t)B * P < 512 || (int64_t)N * k / P > RG_CAP / 2)) P *= 2;
+    const int R = (N + P - 1) / P;
+    const int cap = (int)std::min<int64_t>(RG_CAP, std::max<int64_t>(1024, 4 * ((int64_t)N * k / P)));
+    const size_t lds = ((size_t)2 * R + RG_THREADS / 64 + 2 + 2 * (size_t)cap) * sizeof(int32_t);
+    if (lds > 160 * 1024) return DGX_EUNSUPPORTED;
+    hipLaunchKernelGGL(rev_graph_par_kernel, dim3((unsigned)(B * P)), dim3(RG_THREADS), lds, dgx_stream(stream), idx,
+                       N, k, P, cap, rowptr, edges);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
                              const float* dzp, const float* sumP, int B, int N, int k, int Co, const float* scale,
-                             const float* c0, const float* c1, float* dPQ, void* stream) {
+                             const float* c0, const float* c1, void* dPQ, int out_bf16, void* stream) {
     if (!PQ || !rowptr || !edges || !dzp || !sumP || !scale || !c0 || !c1 || !dPQ) return DGX_EINVAL;
     if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
     const int cs = slice_channels(N, 2);
@@ -839,10 +946,14 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, c
     const dim3 grid(B * parts, slices);
     const size_t lds = (size_t)2 * N * cs * sizeof(float) + (GB_ECAP + EC_THREADS + 1) * sizeof(int);
     hipStream_t st = dgx_stream(stream);
-#define DGX_BWD_CASE(CSV)                                                                                         \
-    case CSV:                                                                                                    \
-        hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, edges, dzp, \
-                           sumP, N, k, Co, parts, scale, c0, c1, dPQ);                                            \
+#define DGX_BWD_CASE(CSV)                                                                                    \
+    case CSV:                                                                                               \
+        if (out_bf16)                                                                                       \
+            hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, true>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
+                               edges, dzp, sumP, N, k, Co, parts, scale, c0, c1, dPQ);                       \
+        else                                                                                                \
+            hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, false>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
+                               edges, dzp, sumP, N, k, Co, parts, scale, c0, c1, dPQ);                       \
         break;
     switch (cs) {
         DGX_BWD_CASE(32)

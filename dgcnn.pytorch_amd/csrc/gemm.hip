@@ -1,0 +1,672 @@
+// bf16 MFMA GEMMs of the EdgeConv chain and conv5 (v_mfma_f32_16x16x32_bf16).
+//
+// Replaces the Conv2d(1x1) GEMMs of reference models/dgcnn.py:54-78 (forward
+// K11/K15 of SURVEY §2.3 and their autograd dgrad/wgrad). After the EdgeConv
+// decomposition every GEMM of the chain is a per-point GEMM over
+// M = B*N rows:
+//   forward   PQ = X [W1;W2]^T            (M x 2Co),  K = C
+//             Z  = Xcat W5^T  + BN stats  (M x emb),  K = 512
+//   backward  dX += dPQ Wcat / dZ W5      (M x C),    K = 2Co / emb
+//             dW  = dPQ^T X / dZ^T Xcat   (small),    K = M  (split-K)
+//
+// One kernel template computes   C[i][j] = sum_k opA(i,k) * opB(j,k)
+// where opA(i,k) is A[i*lda+k] ("KC": k contiguous) or A[k*lda+i] ("IC": i
+// contiguous), the same for B. Operands are fp32 or bf16 in HBM and are
+// converted to bf16 (round-to-nearest-even) while being staged into LDS, so no
+// separate conversion pass touches HBM. LDS holds both tiles k-contiguous
+// ([row][BK + 8] bf16, 80-byte rows: the 16-row ds_read_b128 fragment reads hit
+// 16 distinct 4-bank groups). Accumulation is fp32 in the MFMA.
+//
+// Epilogues (all fp32): STORE, ACCUM (C += ..., used to add dX straight into
+// the concat-gradient buffer), STATS (STORE + per-column sum / sum of squares
+// of the block's rows: the train-mode BatchNorm statistics of conv5, so Z is
+// never re-read for them) and SLAB (split-K partial tile; slab_reduce_kernel
+// sums the slabs in a fixed order -> deterministic weight gradients).
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int GB_THREADS = 256;
+constexpr int GB_BM = 128;
+constexpr int GB_BK = 32;
+constexpr int GB_LDK = GB_BK + 8;  // bf16 per LDS row (80 B)
+
+enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3 };
+
+template <typename T> struct VecOf;
+template <> struct VecOf<float> { static constexpr int V = 4; typedef float4 type; };
+template <> struct VecOf<bf16> { static constexpr int V = 8; typedef uint4 type; };
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(bf16 v) { return (float)v; }
+
+// Blocks b and b+8 share an XCD (MI355X_MICROARCH.md); give each XCD a
+// contiguous range of logical tiles (bijective for any grid size) so the blocks
+// that share an A row panel share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+    const int q = n >> 3, r = n & 7, x = id & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+}
+
+// Stages a TILE x BK slab of op(i,k), i in [i0, i0+TILE) clipped to `rows`,
+// k in [k0, k0+BK) clipped to `kend`, into LDS [i][GB_LDK] as bf16. Global
+// loads go to registers first (load) and reach LDS after the current tile's
+// MFMAs (store), so their latency hides behind the compute.
+template <typename T, bool IC, int TILE>
+struct Stager {
+    static constexpr int V = VecOf<T>::V;
+    // KC: task = (row, V-wide k vector). IC: task = (V-wide i vector, 4 k rows).
+    static constexpr int TASKS = IC ? (TILE / V) * (GB_BK / 4) : TILE * (GB_BK / V);
+    static constexpr int NT = (TASKS + GB_THREADS - 1) / GB_THREADS;
+    static constexpr int PER = IC ? 4 * V : V;
+    float r[NT][PER];
+
+    __device__ __forceinline__ void load(const T* __restrict__ p, int64_t ld, int i0, int rows, int k0, int kend,
+                                         bool vec, int tid) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int task = tid + t * GB_THREADS;
+            if (task >= TASKS) break;
+            if (!IC) {
+                const int row = task / (GB_BK / V), kv = (task % (GB_BK / V)) * V;
+                const int i = i0 + row, k = k0 + kv;
+                if (vec && i < rows && k + V <= kend) {
+                    const typename VecOf<T>::type w =
+                        *reinterpret_cast<const typename VecOf<T>::type*>(p + (int64_t)i * ld + k);
+                    const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+                    for (int u = 0; u < V; ++u) r[t][u] = to_f(e[u]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < V; ++u)
+                        r[t][u] = (i < rows && k + u < kend) ? to_f(p[(int64_t)i * ld + k + u]) : 0.f;
+                }
+            } else {
+                const int ig = task % (TILE / V), kg = task / (TILE / V);
+                const int i = i0 + ig * V, k = k0 + kg * 4;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const bool krow = k + kk < kend;
+                    if (vec && krow && i + V <= rows) {
+                        const typename VecOf<T>::type w =
+                            *reinterpret_cast<const typename VecOf<T>::type*>(p + (int64_t)(k + kk) * ld + i);
+                        const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+                        for (int u = 0; u < V; ++u) r[t][kk * V + u] = to_f(e[u]);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < V; ++u)
+                            r[t][kk * V + u] = (krow && i + u < rows) ? to_f(p[(int64_t)(k + kk) * ld + i + u]) : 0.f;
+                    }
+                }
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store(bf16* __restrict__ lds, int tid) const {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int task = tid + t * GB_THREADS;
+            if (task >= TASKS) break;
+            if (!IC) {
+                const int row = task / (GB_BK / V), kv = (task % (GB_BK / V)) * V;
+                if constexpr (V == 4) {
+                    bf16x4 h = {(bf16)r[t][0], (bf16)r[t][1], (bf16)r[t][2], (bf16)r[t][3]};
+                    *reinterpret_cast<bf16x4*>(lds + row * GB_LDK + kv) = h;
+                } else {
+                    bf16x8 h;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) h[u] = (bf16)r[t][u];
+                    *reinterpret_cast<bf16x8*>(lds + row * GB_LDK + kv) = h;
+                }
+            } else {
+                const int ig = task % (TILE / V), kg = task / (TILE / V);
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    bf16x4 h = {(bf16)r[t][u], (bf16)r[t][V + u], (bf16)r[t][2 * V + u], (bf16)r[t][3 * V + u]};
+                    *reinterpret_cast<bf16x4*>(lds + (ig * V + u) * GB_LDK + kg * 4) = h;
+                }
+            }
+        }
+    }
+};
+
+// C[i][j] = sum_k opA(i,k) opB(j,k); i < M, j < N, k in this split's range.
+template <typename TA, bool AIC, typename TB, bool BIC, int BN, int EPI>
+__global__ __launch_bounds__(GB_THREADS, 2) void gemm_bf16_kernel(
+    const TA* __restrict__ A, int64_t lda, const TB* __restrict__ B, int64_t ldb, int M, int N, int K, int kchunk,
+    int vec_a, int vec_b, float* __restrict__ C, int64_t ldc, float* __restrict__ part) {
+    constexpr int BM = GB_BM;
+    constexpr int WN = BN >= 128 ? 2 : 1;
+    constexpr int WM = 4 / WN;
+    constexpr int TM = BM / WM / 16;
+    constexpr int TN = BN / WN / 16;
+    constexpr int STAGE = (BM + BN) * GB_LDK;
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nJ = (N + BN - 1) / BN;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ti = L / nJ, tj = L - ti * nJ;
+    const int i0 = ti * BM, j0 = tj * BN;
+    const int kbeg = blockIdx.y * kchunk;
+    const int kend = min(K, kbeg + kchunk);
+    const int nk = kend > kbeg ? (kend - kbeg + GB_BK - 1) / GB_BK : 0;
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    Stager<TA, AIC, BM> sa;
+    Stager<TB, BIC, BN> sb;
+    if (nk > 0) {
+        sa.load(A, lda, i0, M, kbeg, kend, vec_a, tid);
+        sb.load(B, ldb, j0, N, kbeg, kend, vec_b, tid);
+        sa.store(lds, tid);
+        sb.store(lds + BM * GB_LDK, tid);
+    }
+    __syncthreads();
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            const int kn = kbeg + (kt + 1) * GB_BK;
+            sa.load(A, lda, i0, M, kn, kend, vec_a, tid);
+            sb.load(B, ldb, j0, N, kn, kend, vec_b, tid);
+        }
+        const bf16* As = lds + cur * STAGE;
+        const bf16* Bs = As + BM * GB_LDK;
+        bf16x8 af[TM], bfv[TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+            af[a] = *reinterpret_cast<const bf16x8*>(As + (wm * TM * 16 + a * 16 + fr) * GB_LDK + fk);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+            bfv[b] = *reinterpret_cast<const bf16x8*>(Bs + (wn * TN * 16 + b * 16 + fr) * GB_LDK + fk);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfv[b], acc[a][b], 0, 0, 0);
+        if (more) {
+            bf16* nxt = lds + (cur ^ 1) * STAGE;
+            sa.store(nxt, tid);
+            sb.store(nxt + BM * GB_LDK, tid);
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile
+    float* out = C;
+    if (EPI == EPI_SLAB) out = C + (int64_t)blockIdx.y * M * N;
+    const int rb = i0 + wm * TM * 16 + (lane >> 4) * 4;
+    const int cb = j0 + wn * TN * 16 + fr;
+    float s1[TN], s2[TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = rb + a * 16 + r;
+            if (i >= M) continue;
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const int j = cb + b * 16;
+                if (j >= N) continue;
+                const float v = acc[a][b][r];
+                float* dst = out + (int64_t)i * ldc + j;
+                if (EPI == EPI_ACCUM) *dst += v;
+                else *dst = v;
+                if (EPI == EPI_STATS) { s1[b] += v; s2[b] = fmaf(v, v, s2[b]); }
+            }
+        }
+    }
+    if (EPI == EPI_STATS) {
+        // column partials of this block's rows: lanes l, l^16, l^32, l^48 share a column,
+        // then the WM waves of the column are summed through LDS (free after the loop)
+        float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            float a1 = s1[b], a2 = s2[b];
+            a1 += __shfl_xor(a1, 16);
+            a2 += __shfl_xor(a2, 16);
+            a1 += __shfl_xor(a1, 32);
+            a2 += __shfl_xor(a2, 32);
+            if (lane < 16) {
+                const int jl = wn * TN * 16 + b * 16 + lane;
+                red[(wm * BN + jl) * 2 + 0] = a1;
+                red[(wm * BN + jl) * 2 + 1] = a2;
+            }
+        }
+        __syncthreads();
+        for (int jl = tid; jl < BN; jl += GB_THREADS) {
+            const int j = j0 + jl;
+            if (j >= N) continue;
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) { t1 += red[(w * BN + jl) * 2]; t2 += red[(w * BN + jl) * 2 + 1]; }
+            part[(int64_t)ti * 2 * N + j] = t1;
+            part[(int64_t)ti * 2 * N + N + j] = t2;
+        }
+    }
+}
+
+// out[orow][ocol] = sum_s slab[s][r][c]; rows r >= split go to (r - split,
+// c + cols) — the [W1;W2] -> W = [W1 | W2] un-stacking of an EdgeConv weight.
+// Block = 64 output elements x 4 slab groups; group g sums slabs s = g mod 4 in
+// ascending s with 8 loads in flight, then the 4 group sums are added in a
+// fixed order: the result does not depend on timing (deterministic).
+constexpr int SR_E = 64, SR_G = 4, SR_U = 8;
+__global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_kernel(const float* __restrict__ slab, int S, int rows,
+                                                                  int cols, int split, float* __restrict__ out,
+                                                                  int64_t ldo) {
+    __shared__ float red[SR_G][SR_E];
+    const int64_t total = (int64_t)rows * cols;
+    const int el = threadIdx.x % SR_E, g = threadIdx.x / SR_E;
+    const int64_t e = (int64_t)blockIdx.x * SR_E + el;
+    float acc = 0.f;
+    if (e < total) {
+        int s = g;
+        for (; s + (SR_U - 1) * SR_G < S; s += SR_U * SR_G) {
+            float v[SR_U];
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) v[u] = slab[(int64_t)(s + u * SR_G) * total + e];
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) acc += v[u];
+        }
+        for (; s < S; s += SR_G) acc += slab[(int64_t)s * total + e];
+    }
+    red[g][el] = acc;
+    __syncthreads();
+    if (g == 0 && e < total) {
+        const float sum = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
+        const int r = (int)(e / cols), c = (int)(e - (int64_t)r * cols);
+        const int orow = r < split ? r : r - split;
+        const int ocol = r < split ? c : c + cols;
+        out[(int64_t)orow * ldo + ocol] = sum;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// bf16-operand GEMMs staged by LDS-DMA (global_load_lds_dwordx4).
+// Both operands bf16 in HBM, either both k-contiguous ("NT": C = A B^T, the
+// forward PQ / conv5 and the input gradients with pre-transposed weights) or
+// both i-contiguous ("TN": C = A^T B, the weight gradients, K = M rows split
+// over workgroups). 128 x BN x 64 tiles, 4 waves (2 x 2), two LDS stages: the
+// next stage's DMA is issued before the current stage's MFMAs and retired by
+// one vmcnt(0) + barrier per stage (cdna_hip_programming.md §5.5 T3+T4, 2-phase).
+// The LDS destination of a DMA is lane-linear, so the bank swizzles are
+// applied to each lane's SOURCE address:
+//   NT image [row][64 k] (128-B rows): 16-B chunk c of row r at c ^ (r & 7) —
+//      the 16-row ds_read_b128 fragment reads are conflict-free.
+//   TN image [k][TILE] (2*TILE-B rows): chunk c of k-row r at c ^ swz(r) —
+//      the ds_read_b64_tr_b16 transposed fragment reads (T10) of 8 consecutive
+//      k-rows per 32-lane half are conflict-free. TN fragments take k-rows
+//      {4g + q} and {16 + 4g + q} (g = lane / 16, q = 0..3) for MFMA k-slots
+//      8g + q and 8g + 4 + q: the same permutation on both operands, so the
+//      sum over k is unchanged.
+constexpr int G2_BM = 128, G2_BK = 64;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int tn_swz(int r, int tile) {
+    return tile >= 128 ? 2 * (r & 7) : 2 * ((r >> 1) & 3);
+}
+
+__device__ __forceinline__ void dma16(const bf16* g, bf16* lds_base) {
+    __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(lds_base), 16, 0, 0);
+}
+
+// NT operand tile: rows [r0, r0+TILE) (clamped to rows-1), k [k0, k0+64).
+template <int TILE>
+__device__ __forceinline__ void stage_nt(const bf16* __restrict__ p, int64_t ld, int r0, int rows, int k0,
+                                         bf16* img, int wave, int lane) {
+    constexpr int INST = TILE * 128 / 1024;  // 1 KB per wave-instruction
+#pragma unroll
+    for (int u = 0; u < INST / 4; ++u) {
+        const int inst = wave * (INST / 4) + u;
+        const int row = inst * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (row & 7);
+        const int gr = min(r0 + row, rows - 1);
+        dma16(p + (int64_t)gr * ld + k0 + 8 * c, img + inst * 512);
+    }
+}
+
+// TN operand tile: k-rows [k0, k0+64) (clamped to kend-1), columns [c0, c0+TILE)
+// (16-B chunks clamped to the last full chunk of the `cols` wide rows).
+template <int TILE>
+__device__ __forceinline__ void stage_tn(const bf16* __restrict__ p, int64_t ld, int c0, int cols, int k0,
+                                         int kend, bf16* img, int wave, int lane) {
+    constexpr int CPR = TILE / 8;            // chunks per row
+    constexpr int RPI = 64 / CPR;            // rows per wave-instruction
+    constexpr int INST = 64 / RPI;
+#pragma unroll
+    for (int u = 0; u < INST / 4; ++u) {
+        const int inst = wave * (INST / 4) + u;
+        const int row = inst * RPI + lane / CPR;
+        const int c = (lane % CPR) ^ tn_swz(row, TILE);
+        const int gk = min(k0 + row, kend - 1);
+        const int gc = min(c0 + 8 * c, cols - 8);
+        dma16(p + (int64_t)gk * ld + gc, img + inst * 512);
+    }
+}
+
+__device__ __forceinline__ bf16x8 frag_nt(const bf16* img, int row, int chunk) {
+    return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((chunk ^ (row & 7)) << 3));
+}
+
+template <int TILE>
+__device__ __forceinline__ bf16x8 frag_tn(const bf16* img, int s, int col0, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int chunk = (col0 >> 3) + (p >> 1);
+    const int r1 = 32 * s + 4 * g + q, r2 = r1 + 16;
+    const bf16* a1 = img + r1 * TILE + ((chunk ^ tn_swz(r1, TILE)) << 3) + 4 * (p & 1);
+    const bf16* a2 = img + r2 * TILE + ((chunk ^ tn_swz(r2, TILE)) << 3) + 4 * (p & 1);
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)const_cast<bf16*>(a1));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)const_cast<bf16*>(a2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+template <bool TN, int BN, int EPI>
+__global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
+    const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
+    int kchunk, float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend,
+    int64_t ldd) {
+    constexpr int BM = G2_BM;
+    constexpr int WN = BN >= 128 ? 2 : 1;
+    constexpr int WM = 4 / WN;
+    constexpr int TM = BM / WM / 16;
+    constexpr int TN_ = BN / WN / 16;
+    constexpr int STAGE = (BM + BN) * G2_BK;  // bf16 elements per stage
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nJ = (N + BN - 1) / BN;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ti = L / nJ, tj = L - ti * nJ;
+    const int i0 = ti * BM, j0 = tj * BN;
+    const int kbeg = blockIdx.y * kchunk;
+    const int kend = min(K, kbeg + kchunk);
+    const int nk = kend > kbeg ? (kend - kbeg + G2_BK - 1) / G2_BK : 0;
+
+    f32x4 acc[TM][TN_];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN_; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto stage = [&](int t, int buf) {
+        bf16* img = lds + buf * STAGE;
+        const int k0 = kbeg + t * G2_BK;
+        if (TN) {
+            stage_tn<BM>(A, lda, i0, M, k0, kend, img, wave, lane);
+            stage_tn<BN>(B, ldb, j0, N, k0, kend, img + BM * G2_BK, wave, lane);
+        } else {
+            stage_nt<BM>(A, lda, i0, M, k0, img, wave, lane);
+            stage_nt<BN>(B, ldb, j0, N, k0, img + BM * G2_BK, wave, lane);
+        }
+    };
+    if (nk > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < nk) stage(t + 1, cur ^ 1);
+        bf16* img = lds + cur * STAGE;
+        if (TN && kbeg + (t + 1) * G2_BK > kend) {
+            // partial last stage: k-rows past kend hold clamped copies -> zero them
+            // (uniform branch: every wave takes it or none)
+            const int valid = kend - kbeg - t * G2_BK;
+            for (int e = tid; e < (G2_BK - valid) * (BM + BN) / 8; e += GB_THREADS) {
+                const int per_a = (G2_BK - valid) * BM / 8;
+                bf16x8 z = {};
+                if (e < per_a) {
+                    *reinterpret_cast<bf16x8*>(img + valid * BM + e * 8) = z;
+                } else {
+                    *reinterpret_cast<bf16x8*>(img + BM * G2_BK + valid * BN + (e - per_a) * 8) = z;
+                }
+            }
+            __syncthreads();
+        }
+        const bf16* As = img;
+        const bf16* Bs = img + BM * G2_BK;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[TM], bfv[TN_];
+#pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                if (TN) af[a] = frag_tn<BM>(As, s, wm * TM * 16 + a * 16, lane);
+                else af[a] = frag_nt(As, wm * TM * 16 + a * 16 + (lane & 15), s * 4 + (lane >> 4));
+            }
+#pragma unroll
+            for (int b = 0; b < TN_; ++b) {
+                if (TN) bfv[b] = frag_tn<BN>(Bs, s, wn * TN_ * 16 + b * 16, lane);
+                else bfv[b] = frag_nt(Bs, wn * TN_ * 16 + b * 16 + (lane & 15), s * 4 + (lane >> 4));
+            }
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN_; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfv[b], acc[a][b], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    float* out = C;
+    if (EPI == EPI_SLAB) out = C + (int64_t)blockIdx.y * M * N;
+    const int rb = i0 + wm * TM * 16 + (lane >> 4) * 4;
+    const int cb = j0 + wn * TN_ * 16 + (lane & 15);
+    float s1[TN_], s2[TN_];
+#pragma unroll
+    for (int b = 0; b < TN_; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = rb + a * 16 + r;
+            if (i >= M) continue;
+#pragma unroll
+            for (int b = 0; b < TN_; ++b) {
+                const int j = cb + b * 16;
+                if (j >= N) continue;
+                const float v = acc[a][b][r];
+                float* dst = out + (int64_t)i * ldc + j;
+                if (EPI == EPI_ACCUM) *dst = (addend ? addend[(int64_t)i * ldd + j] : *dst) + v;
+                else *dst = v;
+                if (EPI == EPI_STATS) { s1[b] += v; s2[b] = fmaf(v, v, s2[b]); }
+            }
+        }
+    }
+    if (EPI == EPI_STATS) {
+        float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
+#pragma unroll
+        for (int b = 0; b < TN_; ++b) {
+            float a1 = s1[b], a2 = s2[b];
+            a1 += __shfl_xor(a1, 16);
+            a2 += __shfl_xor(a2, 16);
+            a1 += __shfl_xor(a1, 32);
+            a2 += __shfl_xor(a2, 32);
+            if (lane < 16) {
+                const int jl = wn * TN_ * 16 + b * 16 + lane;
+                red[(wm * BN + jl) * 2 + 0] = a1;
+                red[(wm * BN + jl) * 2 + 1] = a2;
+            }
+        }
+        __syncthreads();
+        for (int jl = tid; jl < BN; jl += GB_THREADS) {
+            const int j = j0 + jl;
+            if (j >= N) continue;
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) { t1 += red[(w * BN + jl) * 2]; t2 += red[(w * BN + jl) * 2 + 1]; }
+            part[(int64_t)ti * 2 * N + j] = t1;
+            part[(int64_t)ti * 2 * N + N + j] = t2;
+        }
+    }
+}
+
+template <bool TN, int BN, int EPI>
+int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int M, int N, int K, int splits,
+                    float* C, int64_t ldc, float* part, const float* addend, int64_t ldd, hipStream_t st) {
+    const int nI = (M + G2_BM - 1) / G2_BM, nJ = (N + BN - 1) / BN;
+    int kchunk = (K + splits - 1) / splits;
+    kchunk = (kchunk + G2_BK - 1) / G2_BK * G2_BK;
+    const int sp = (K + kchunk - 1) / kchunk;
+    dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
+    hipLaunchKernelGGL((gemm_lds_kernel<TN, BN, EPI>), grid, dim3(GB_THREADS), 0, st, A, lda, B, ldb, M, N, K,
+                       EPI == EPI_SLAB ? kchunk : K, C, ldc, part, addend, ldd);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+// Weight operands for the bf16 GEMMs, one launch per layer: `nt` = [rows][K]
+// (the GEMM's B for X W^T), `tn` = its transpose (the B for dY W). For an
+// EdgeConv weight W (Co, 2C) (reference conv weight, dgcnn.py:55) the rows are
+// the stacked halves [W1; W2] (2Co, C); for conv5 W (Co, K) as is.
+__global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ W, int Co, int C, int stacked,
+                                                          bf16* __restrict__ nt, bf16* __restrict__ tn) {
+    const int rows = stacked ? 2 * Co : Co;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= rows * C) return;
+    const int r = e / C, c = e - r * C;
+    const float v = stacked ? W[(r % Co) * 2 * C + (r / Co) * C + c] : W[r * C + c];
+    const bf16 h = (bf16)v;
+    nt[e] = h;
+    tn[c * rows + r] = h;
+}
+
+template <typename TA, bool AIC, typename TB, bool BIC, int BN, int EPI>
+int launch_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, int splits,
+                int vec_a, int vec_b, float* C, int64_t ldc, float* part, hipStream_t st) {
+    const int nI = (M + GB_BM - 1) / GB_BM, nJ = (N + BN - 1) / BN;
+    int kchunk = (K + splits - 1) / splits;
+    kchunk = (kchunk + GB_BK - 1) / GB_BK * GB_BK;
+    const int sp = (K + kchunk - 1) / kchunk;
+    dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
+    hipLaunchKernelGGL((gemm_bf16_kernel<TA, AIC, TB, BIC, BN, EPI>), grid, dim3(GB_THREADS), 0, st,
+                       static_cast<const TA*>(A), lda, static_cast<const TB*>(B), ldb, M, N, K,
+                       EPI == EPI_SLAB ? kchunk : K, vec_a, vec_b, C, ldc, part);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+bool aligned_to(const void* p, int bytes) { return (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int dgx_gemm_stats_rows(int M) { return (M + GB_BM - 1) / GB_BM; }
+
+int dgx_gemm_splits(int M, int N, int K) {
+    // split-K factor of a SLAB GEMM: about 2 workgroups per CU (256 CUs), each
+    // split at least 8 K-steps deep
+    const int BN = N > 64 ? 128 : 64;
+    const int tiles = ((M + GB_BM - 1) / GB_BM) * ((N + BN - 1) / BN);
+    int s = (512 + tiles - 1) / tiles;
+    const int maxs = (K + 8 * GB_BK - 1) / (8 * GB_BK);
+    if (s > maxs) s = maxs;
+    return s < 1 ? 1 : s;
+}
+
+int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda, const void* B, int b_bf16, int b_ic,
+                  int64_t ldb, int M, int N, int K, int epi, int splits, float* C, int64_t ldc, float* partials,
+                  void* stream) {
+    if (!A || !B || !C || M < 0 || N < 0 || K < 0 || lda < 1 || ldb < 1 || ldc < 1 || splits < 1)
+        return DGX_EINVAL;
+    if (epi == EPI_STATS && !partials) return DGX_EINVAL;
+    if (M == 0 || N == 0) return DGX_OK;
+    if (epi == EPI_SLAB) ldc = N;  // slabs are dense [splits][M][N]
+    hipStream_t st = dgx_stream(stream);
+    const int va = a_bf16 ? 8 : 4, vb = b_bf16 ? 8 : 4;
+    const int vec_a = (lda % va == 0) && aligned_to(A, 16);
+    const int vec_b = (ldb % vb == 0) && aligned_to(B, 16);
+    const bool wide = N > 64;
+#define DGX_GEMM(TA, AIC, TB, BIC, E)                                                                          \
+    return wide ? launch_gemm<TA, AIC, TB, BIC, 128, E>(A, lda, B, ldb, M, N, K, splits, vec_a, vec_b, C, ldc, \
+                                                        partials, st)                                          \
+                : launch_gemm<TA, AIC, TB, BIC, 64, E>(A, lda, B, ldb, M, N, K, splits, vec_a, vec_b, C, ldc,  \
+                                                       partials, st)
+    // the operand layouts the engine uses; others are rejected
+    if (!a_bf16 && !a_ic && !b_bf16 && !b_ic) {  // X W^T: forward PQ, conv5
+        if (epi == EPI_STORE) DGX_GEMM(float, false, float, false, EPI_STORE);
+        if (epi == EPI_STATS) DGX_GEMM(float, false, float, false, EPI_STATS);
+    }
+    if (!a_ic && !b_bf16 && b_ic) {  // dPQ Wcat / dZ W5: input gradients
+        if (!a_bf16 && epi == EPI_ACCUM) DGX_GEMM(float, false, float, true, EPI_ACCUM);
+        if (!a_bf16 && epi == EPI_STORE) DGX_GEMM(float, false, float, true, EPI_STORE);
+        if (a_bf16 && epi == EPI_ACCUM) DGX_GEMM(bf16, false, float, true, EPI_ACCUM);
+        if (a_bf16 && epi == EPI_STORE) DGX_GEMM(bf16, false, float, true, EPI_STORE);
+    }
+    if (a_ic && b_ic && !b_bf16 && epi == EPI_SLAB) {  // dPQ^T X / dZ^T X: weight gradients
+        if (a_bf16) DGX_GEMM(bf16, true, float, true, EPI_SLAB);
+        DGX_GEMM(float, true, float, true, EPI_SLAB);
+    }
+#undef DGX_GEMM
+    return DGX_EUNSUPPORTED;
+}
+
+int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int tn, int M, int N, int K,
+                      int epi, int splits, float* C, int64_t ldc, float* partials, const float* addend,
+                      int64_t ldd, void* stream) {
+    if (!A || !B || !C || M < 0 || N < 0 || K < 0 || splits < 1) return DGX_EINVAL;
+    if (epi == EPI_STATS && !partials) return DGX_EINVAL;
+    if (M == 0 || N == 0) return DGX_OK;
+    // DMA staging moves 16-B chunks: rows 16-B aligned, whole chunks per row
+    if (!aligned_to(A, 16) || !aligned_to(B, 16) || lda % 8 || ldb % 8) return DGX_EUNSUPPORTED;
+    if (tn ? (M < 8 || N < 8 || M % 8 || N % 8 || epi != EPI_SLAB) : (K % G2_BK || epi == EPI_SLAB))
+        return DGX_EUNSUPPORTED;
+    if (epi == EPI_SLAB) ldc = N;
+    hipStream_t st = dgx_stream(stream);
+    const bf16* a = static_cast<const bf16*>(A);
+    const bf16* b = static_cast<const bf16*>(B);
+    const bool wide = N > 64;
+    if (tn)
+        return wide ? launch_gemm_lds<true, 128, EPI_SLAB>(a, lda, b, ldb, M, N, K, splits, C, ldc, partials, nullptr,
+                                                           0, st)
+                    : launch_gemm_lds<true, 64, EPI_SLAB>(a, lda, b, ldb, M, N, K, splits, C, ldc, partials, nullptr, 0,
+                                                          st);
+#define DGX_G2(E)                                                                                              \
+    return wide ? launch_gemm_lds<false, 128, E>(a, lda, b, ldb, M, N, K, 1, C, ldc, partials, addend, ldd, st) \
+                : launch_gemm_lds<false, 64, E>(a, lda, b, ldb, M, N, K, 1, C, ldc, partials, addend, ldd, st)
+    if (epi == EPI_STORE) DGX_G2(EPI_STORE);
+    if (epi == EPI_ACCUM) DGX_G2(EPI_ACCUM);
+    if (epi == EPI_STATS) DGX_G2(EPI_STATS);
+#undef DGX_G2
+    return DGX_EUNSUPPORTED;
+}
+
+int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt, void* tn, void* stream) {
+    if (!W || !nt || !tn || Co < 1 || C < 1) return DGX_EINVAL;
+    const int total = (stacked ? 2 * Co : Co) * C;
+    hipLaunchKernelGGL(weight_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, dgx_stream(stream), W,
+                       Co, C, stacked, static_cast<bf16*>(nt), static_cast<bf16*>(tn));
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_slab_reduce_f32(const float* slab, int S, int rows, int cols, int split, float* out, int64_t ldo,
+                        void* stream) {
+    if (!slab || !out || S < 1 || rows < 0 || cols < 0 || split < 0 || split > rows) return DGX_EINVAL;
+    const int64_t total = (int64_t)rows * cols;
+    if (total == 0) return DGX_OK;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((total + SR_E - 1) / SR_E)), dim3(SR_E * SR_G), 0,
+                       dgx_stream(stream),
+                       slab, S, rows, cols, split, out, ldo);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+}  // extern "C"

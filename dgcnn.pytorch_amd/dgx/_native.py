@@ -38,11 +38,12 @@ _SIGS = {
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp],
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
-    "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
+    "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp],
     "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
-    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
+                                 _vp],
     "dgx_colstats_rows": [_i64],
     "dgx_colstats_f32": [_vp, _i32, _i64, _i32, _vp, _i32, _vp],
     "dgx_pointconv_apply_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],
@@ -50,6 +51,14 @@ _SIGS = {
     "dgx_pointconv_bwd_f32": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp],
     "dgx_pointconv_input_grad": [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_to_bf16": [_vp, _i64, _i64, _i32, _vp, _vp],
+    "dgx_gemm_stats_rows": [_i32],
+    "dgx_gemm_splits": [_i32, _i32, _i32],
+    "dgx_gemm_bf16": [_vp, _i32, _i32, _i64, _vp, _i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp,
+                      _vp],
+    "dgx_slab_reduce_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp],
+    "dgx_gemm_lds_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64,
+                          _vp],
+    "dgx_weight_prep_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
 }
 _RESTYPES = {
     "dgx_version": ctypes.c_char_p,

@@ -20,6 +20,7 @@ Backward per block (reverse order):
 import torch
 
 from . import _native as nat
+from . import gemm as G
 from . import precision as prec
 from .ops import knn_raw, reduction_order
 
@@ -65,11 +66,16 @@ class _EdgeConvStack(torch.autograd.Function):
         total = sum(widths)
         L = nat.lib()
         stream = nat.stream_of(x)
+        bf16 = prec.get() == "bf16"
         xcat = torch.empty((M, total), dtype=torch.float32, device=dev)
+        # bf16 twin of the concat buffer: the GEMM operand copy, written by the
+        # same kernel that writes xcat (precision "bf16" only)
+        xcat16 = torch.empty((M, total), dtype=torch.bfloat16, device=dev) if bf16 else None
         x_pm = x.permute(0, 2, 1).reshape(M, C0)  # point-major input rows (copy only if needed)
         saved = []
         off_in = None
         count = float(M * k)
+        have16 = False  # xcat16 holds the previous block's output
         for li, ly in enumerate(layers):
             w, gamma, beta = params[3 * li: 3 * li + 3]
             cin, co = ly.cin, ly.cout
@@ -82,8 +88,17 @@ class _EdgeConvStack(torch.autograd.Function):
                 # dim -1 of a contiguous tensor), hence the strided rounding order
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
                               strides=(N * total, 1, total), shape=(B, cin, N))
-            wcat = _split_weight(w, cin, co)
-            PQ = prec.mm(X, wcat.t())  # (M, 2Co) fp32 out
+            wprep = None
+            if bf16:
+                X16 = xcat16[:, off_in:off_in + cin] if li > 0 else None
+                if have16 and G.lds_ok_nt(X16, cin):
+                    # bf16 operands by LDS-DMA; the weight's bf16 [W1;W2] and transpose serve fwd and bwd
+                    wprep = G.prep_weight(w, co, cin, True)
+                    PQ = G.lds_xwt(X16, wprep[0])
+                else:
+                    PQ = G.mm_xwt(X, _split_weight(w, cin, co))  # fp32 operands rounded while staged
+            else:
+                PQ = prec.mm(X, _split_weight(w, cin, co).t())
             off = sum(widths[:li])
             out = xcat[:, off:off + co]
             bn = ly.bn
@@ -109,9 +124,12 @@ class _EdgeConvStack(torch.autograd.Function):
                         nat.ptr(bn.running_mean) if update else None,
                         nat.ptr(bn.running_var) if update else None, factor, float(bn.eps),
                         nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), stream), "bn finalize")
+                    out16 = xcat16[:, off:off + co] if bf16 else None
                     nat.check(L.dgx_bn_lrelu_apply_f32(nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift),
-                                                       float(ly.slope), nat.ptr(out), total, stream), "bn apply")
-                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd))
+                                                       float(ly.slope), nat.ptr(out), total, nat.ptr(out16), stream),
+                              "bn apply")
+                    have16 = bf16
+                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep))
                     if _debug is not None:
                         zpos = (scale * ysel + shift) > 0
                         _debug[("fwd", li)] = (idx.clone(), arg.clone(), zpos)
@@ -122,6 +140,7 @@ class _EdgeConvStack(torch.autograd.Function):
                     nat.check(L.dgx_edge_fwd_eval_f32(
                         nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(scale), nat.ptr(shift),
                         float(ly.slope), nat.ptr(out), total, stream), "edge eval")
+                    have16 = False
                     saved.append(None)
             off_in = off
         ctx.k = k
@@ -129,14 +148,18 @@ class _EdgeConvStack(torch.autograd.Function):
         ctx.shape = (B, C0, N)
         ctx.layer_state = saved
         ctx.x_needs_grad = x.requires_grad
-        ctx.save_for_backward(x_pm, xcat, *params)
-        return xcat
+        ctx.bf16 = bf16
+        ctx.save_for_backward(x_pm, xcat, xcat16, *params)
+        if xcat16 is None or not have16:
+            xcat16 = torch.empty(0, dtype=torch.bfloat16, device=dev)
+        ctx.mark_non_differentiable(xcat16)
+        return xcat, xcat16
 
     @staticmethod
-    def backward(ctx, dxcat):
+    def backward(ctx, dxcat, _unused):
         if any(s is None for s in ctx.layer_state):
             raise RuntimeError("dgx EdgeConv: backward through an eval-mode (running-stats) forward is not supported")
-        x_pm, xcat, *params = ctx.saved_tensors
+        x_pm, xcat, xcat16, *params = ctx.saved_tensors
         layers, k = ctx.layers, ctx.k
         B, C0, N = ctx.shape
         M = B * N
@@ -145,20 +168,33 @@ class _EdgeConvStack(torch.autograd.Function):
         stream = nat.stream_of(xcat)
         widths = [ly.cout for ly in layers]
         total = sum(widths)
-        dxcat = dxcat.contiguous().clone()
+        bf16 = ctx.bf16
         grads = [None] * len(params)
         dx_in = None
         count = float(M * k)
         rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
         edges = torch.empty(M * k, dtype=torch.int32, device=dev)
-        for li in reversed(range(len(layers))):
+        nl = len(layers)
+        if bf16:
+            # The incoming gradient stays read-only: block l's input gradient is written
+            # as addend (incoming slice) + dPQ Wcat into a fresh buffer, no clone pass.
+            dxcat = dxcat.contiguous()
+            lead = total - widths[-1]
+            dnew = torch.empty((M, max(lead, 1)), dtype=torch.float32, device=dev)
+        else:
+            dxcat = dxcat.contiguous().clone()
+        for li in reversed(range(nl)):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
             w = params[3 * li]
-            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd = ctx.layer_state[li]
+            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep = ctx.layer_state[li]
             off = sum(widths[:li])
-            X = x_pm if li == 0 else xcat[:, off - widths[li - 1]: off - widths[li - 1] + cin]
-            dY = dxcat[:, off:off + co]
+            prev = off - widths[li - 1] if li > 0 else None
+            X = x_pm if li == 0 else xcat[:, prev: prev + cin]
+            if bf16 and li < nl - 1:
+                dY, ldy = dnew[:, off:off + co], dnew.stride(0)
+            else:
+                dY, ldy = dxcat[:, off:off + co], dxcat.stride(0)
             nblk = max(1, min(1024, (M + 63) // 64))
             dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dz with packed slot
             partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
@@ -166,10 +202,11 @@ class _EdgeConvStack(torch.autograd.Function):
             dbeta = torch.empty(co, dtype=torch.float32, device=dev)
             c0 = torch.empty(co, dtype=torch.float32, device=dev)
             c1 = torch.empty(co, dtype=torch.float32, device=dev)
-            dPQ = torch.empty((M, 2 * co), dtype=torch.float32, device=dev)
+            # dPQ only feeds the GEMMs: bf16 (what the GEMM would round it to) in bf16 mode
+            dPQ = torch.empty((M, 2 * co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
             with torch.cuda.device(dev):
                 nat.check(L.dgx_edge_bwd_dz_f32(
-                    nat.ptr(dY), total, nat.ptr(ysel), nat.ptr(arg), M, co, nat.ptr(scale), nat.ptr(shift),
+                    nat.ptr(dY), ldy, nat.ptr(ysel), nat.ptr(arg), M, co, nat.ptr(scale), nat.ptr(shift),
                     nat.ptr(mean), nat.ptr(invstd), float(ly.slope), nat.ptr(dz), nat.ptr(partials), nblk, stream),
                     "edge bwd dz")
                 nat.check(L.dgx_bn_bwd_finalize_f32(
@@ -179,31 +216,48 @@ class _EdgeConvStack(torch.autograd.Function):
                           "reverse graph")
                 nat.check(L.dgx_edge_bwd_scatter_f32(
                     nat.ptr(PQ), 2 * co, nat.ptr(rowptr), nat.ptr(edges), nat.ptr(dz), nat.ptr(sumP), B, N, k, co,
-                    nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), stream), "edge bwd scatter")
+                    nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), int(bf16), stream), "edge bwd scatter")
             if _debug is not None:
                 _debug[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
-                              "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.clone(), "partials": partials.clone(),
+                              "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.float(), "partials": partials.clone(),
                               "ysel": ysel.clone(), "scale": scale.clone(), "shift": shift.clone(),
                               "arg": arg.clone(), "idx": idx.clone(), "PQ": PQ.clone(), "sumP": sumP.clone(),
                               "mean": mean.clone(), "invstd": invstd.clone(), "X": X.clone(),
                               "rowptr": rowptr.clone(), "edges": edges.clone()}
-            wcat = _split_weight(w, cin, co)
-            dwcat = prec.mm(dPQ.t(), X)  # (2Co, C)
-            grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)
             grads[3 * li + 1] = dgamma
             grads[3 * li + 2] = dbeta
-            if li > 0:
-                prev = off - widths[li - 1]
-                dxcat[:, prev:prev + cin] += prec.mm(dPQ, wcat)
-            elif ctx.x_needs_grad:
-                dx_in = prec.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
+            if bf16:
+                # dW = dPQ^T X, un-stacked to the reference layout [W1 | W2]
+                gw = torch.empty((co, 2 * cin), dtype=torch.float32, device=dev)
+                if wprep is not None:
+                    G.lds_atb(dPQ, xcat16[:, prev:prev + cin], gw, split_rows=co)
+                else:
+                    G.mm_atb(dPQ, X, gw, split_rows=co)
+                grads[3 * li] = gw.view(w.shape)
+                if li > 0:
+                    dst = dnew[:, prev:prev + cin]
+                    add = dxcat[:, prev:prev + cin]
+                    if wprep is not None:
+                        G.lds_xwt(dPQ, wprep[1], out=dst, addend=add)
+                    else:
+                        dst.copy_(add)
+                        G.mm_xw(dPQ, _split_weight(w, cin, co), out=dst, accumulate=True)
+                elif ctx.x_needs_grad:
+                    dx_in = G.mm_xw(dPQ, _split_weight(w, cin, co)).view(B, N, C0).permute(0, 2, 1)
+            else:
+                wcat = _split_weight(w, cin, co)
+                dwcat = prec.mm(dPQ.t(), X)  # (2Co, C)
+                grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)
+                if li > 0:
+                    dxcat[:, prev:prev + cin] += prec.mm(dPQ, wcat)
+                elif ctx.x_needs_grad:
+                    dx_in = prec.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
         return (dx_in, None, None, None, *grads)
 
 
-def edgeconv_stack(x, k, convs, training):
-    """Run the block chain. ``convs``: list of nn.Sequential(Conv2d(2C,Co,1,bias=False),
-    BatchNorm2d(Co), LeakyReLU) exactly as the reference builds them (dgcnn.py:54-73).
-    Returns the point-major concat buffer (B*N, sum Co)."""
+def edgeconv_stack_pair(x, k, convs, training):
+    """As edgeconv_stack, also returning the bf16 twin of the concat buffer
+    (empty unless precision "bf16" produced it): conv5's GEMM operand."""
     nat.require_device(x)
     if x.dtype != torch.float32:
         x = x.float()
@@ -216,3 +270,10 @@ def edgeconv_stack(x, k, convs, training):
         layers.append(_Layer(c2 // 2, co, bn, act.negative_slope))
         params += [conv.weight, bn.weight, bn.bias]
     return _EdgeConvStack.apply(x, k, layers, training, *params)
+
+
+def edgeconv_stack(x, k, convs, training):
+    """Run the block chain. ``convs``: list of nn.Sequential(Conv2d(2C,Co,1,bias=False),
+    BatchNorm2d(Co), LeakyReLU) exactly as the reference builds them (dgcnn.py:54-73).
+    Returns the point-major concat buffer (B*N, sum Co)."""
+    return edgeconv_stack_pair(x, k, convs, training)[0]

@@ -1,0 +1,150 @@
+"""Host side of the engine's bf16 MFMA GEMMs (csrc/gemm.hip, C ABI dgx_gemm_bf16).
+
+Every GEMM of the chain is ``C[i][j] = sum_k opA(i,k) opB(j,k)`` with each
+operand either k-contiguous ("kc": row i at A[i*ld:]) or i-contiguous ("ic":
+column i of a row-major (K, ld) buffer). Operands are fp32 or bf16 views of
+existing buffers (column slices of the concat buffer included): nothing is
+copied or converted on the host side.
+"""
+import torch
+
+from . import _native as nat
+
+EPI_STORE, EPI_ACCUM, EPI_STATS, EPI_SLAB = 0, 1, 2, 3
+
+
+def _operand(t, ic):
+    """(pointer, is_bf16, ld) of a 2-D view whose inner dim is unit-stride."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise RuntimeError(f"dgx gemm: operand must be a 2-D row-major view, got strides {t.stride()}")
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError(f"dgx gemm: operand dtype {t.dtype} (fp32/bf16 only)")
+    ld = t.stride(0) if t.shape[0] > 1 else max(1, t.shape[1])
+    return nat.ptr(t), int(t.dtype == torch.bfloat16), int(ic), ld
+
+
+def gemm(a, a_ic, b, b_ic, M, N, K, epi, out, partials=None, splits=1):
+    """Raw launch. ``a``: (M,K) view if not a_ic else (K,M); same for ``b`` with N."""
+    ap, abf, aic, lda = _operand(a, a_ic)
+    bp, bbf, bic, ldb = _operand(b, b_ic)
+    if epi == EPI_SLAB:
+        ldc = N
+    else:
+        if out.dim() != 2 or out.stride(1) != 1 or out.dtype != torch.float32:
+            raise RuntimeError("dgx gemm: output must be a row-major fp32 2-D view")
+        ldc = out.stride(0)
+    with torch.cuda.device(out.device):
+        nat.check(nat.lib().dgx_gemm_bf16(ap, abf, aic, lda, bp, bbf, bic, ldb, M, N, K, epi, splits,
+                                          nat.ptr(out), ldc, nat.ptr(partials), nat.stream_of(out)), "gemm bf16")
+    return out
+
+
+def mm_xwt(x, w, out=None, stats=False):
+    """out (M,N) = x (M,K) @ w (N,K)^T; with ``stats`` also returns the column
+    partials (rows, 2, N) of the train-mode BatchNorm statistics."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    part = None
+    if stats:
+        part = torch.empty((nat.lib().dgx_gemm_stats_rows(M), 2, N), dtype=torch.float32, device=x.device)
+    gemm(x, False, w, False, M, N, K, EPI_STATS if stats else EPI_STORE, out, part)
+    return (out, part) if stats else out
+
+
+def mm_xw(x, w, out=None, accumulate=False):
+    """out (M,N) (+)= x (M,K) @ w (K,N)."""
+    M, K = x.shape
+    N = w.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    gemm(x, False, w, True, M, N, K, EPI_ACCUM if accumulate else EPI_STORE, out)
+    return out
+
+
+def mm_atb(a, b, out, split_rows=None):
+    """out = a^T @ b for a (R, M), b (R, N) (reduction over the R rows, split-K
+    over workgroups, deterministic slab sum). ``split_rows`` = Co un-stacks a
+    [W1;W2] result into out = [W1 | W2] (out is (M - Co, 2N))."""
+    R, M = a.shape
+    N = b.shape[1]
+    L = nat.lib()
+    S = L.dgx_gemm_splits(M, N, R)
+    slab = torch.empty((S, M, N), dtype=torch.float32, device=a.device)
+    gemm(a, True, b, True, M, N, R, EPI_SLAB, slab, splits=S)
+    # the launch may use fewer splits than asked when R is short; count them the same way
+    chunk = -(-R // S)
+    chunk = -(-chunk // 32) * 32
+    used = -(-R // chunk)
+    split = M if split_rows is None else split_rows
+    with torch.cuda.device(out.device):
+        nat.check(L.dgx_slab_reduce_f32(nat.ptr(slab), used, M, N, split, nat.ptr(out), out.stride(0),
+                                        nat.stream_of(out)), "slab reduce")
+    return out
+
+
+# ---- bf16-operand path (LDS-DMA staging, dgx_gemm_lds_bf16) ------------------
+
+def _bf16_2d(t):
+    if t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1:
+        raise RuntimeError("dgx gemm (bf16 path): operands must be row-major bf16 2-D views")
+    return t.stride(0) if t.shape[0] > 1 else max(8, t.shape[1])
+
+
+def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None):
+    """out (M,N) = x16 (M,K) @ w16 (N,K)^T (bf16 operands, K % 64 == 0).
+    ``stats``: also returns the BatchNorm column partials (rows, 2, N).
+    ``accumulate``: out += ...; with ``addend``: out = addend + ... ."""
+    M, K = x16.shape
+    N = w16.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x16.device)
+    part = None
+    if stats:
+        part = torch.empty((nat.lib().dgx_gemm_stats_rows(M), 2, N), dtype=torch.float32, device=x16.device)
+    epi = EPI_STATS if stats else (EPI_ACCUM if (accumulate or addend is not None) else EPI_STORE)
+    with torch.cuda.device(out.device):
+        nat.check(nat.lib().dgx_gemm_lds_bf16(
+            nat.ptr(x16), _bf16_2d(x16), nat.ptr(w16), _bf16_2d(w16), 0, M, N, K, epi, 1, nat.ptr(out),
+            out.stride(0), nat.ptr(part), nat.ptr(addend), addend.stride(0) if addend is not None else 0,
+            nat.stream_of(out)), "gemm lds nt")
+    return (out, part) if stats else out
+
+
+def lds_atb(a16, b16, out, split_rows=None):
+    """out = a16^T @ b16 for a16 (R, M), b16 (R, N) bf16 (reduction over R rows,
+    split-K slabs summed deterministically); ``split_rows`` as in mm_atb."""
+    R, M = a16.shape
+    N = b16.shape[1]
+    L = nat.lib()
+    S = L.dgx_gemm_splits(M, N, R)
+    chunk = -(-R // S)
+    chunk = -(-chunk // 64) * 64
+    used = -(-R // chunk)
+    slab = torch.empty((used, M, N), dtype=torch.float32, device=a16.device)
+    with torch.cuda.device(out.device):
+        st = nat.stream_of(out)
+        nat.check(L.dgx_gemm_lds_bf16(nat.ptr(a16), _bf16_2d(a16), nat.ptr(b16), _bf16_2d(b16), 1, M, N, R,
+                                      EPI_SLAB, S, nat.ptr(slab), N, None, None, 0, st), "gemm lds tn")
+        split = M if split_rows is None else split_rows
+        nat.check(L.dgx_slab_reduce_f32(nat.ptr(slab), used, M, N, split, nat.ptr(out), out.stride(0), st),
+                  "slab reduce")
+    return out
+
+
+def prep_weight(w, rows, cols, stacked):
+    """bf16 operand copies of a conv weight: (nt (R, cols), tn (cols, R)) with
+    R = 2*rows for a stacked EdgeConv weight (rows = Co, cols = C)."""
+    R = 2 * rows if stacked else rows
+    nt = torch.empty((R, cols), dtype=torch.bfloat16, device=w.device)
+    tn = torch.empty((cols, R), dtype=torch.bfloat16, device=w.device)
+    with torch.cuda.device(w.device):
+        nat.check(nat.lib().dgx_weight_prep_bf16(nat.ptr(w), rows, cols, int(stacked), nat.ptr(nt), nat.ptr(tn),
+                                                 nat.stream_of(w)), "weight prep")
+    return nt, tn
+
+
+def lds_ok_nt(x, K):
+    """Whether the DMA path takes this k-contiguous operand (else the register-staged kernel)."""
+    return x.dtype == torch.bfloat16 and K % 64 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0

@@ -12,32 +12,50 @@ cumulative average).
 import torch
 
 from . import _native as nat
+from . import gemm as G
 from . import precision as prec
 from .edgeconv import _bn_factor
 
 
 class _PointConvBNLReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, X, B, N, bn, slope, training, weight, gamma, beta):
+    def forward(ctx, X, X16, B, N, bn, slope, training, weight, gamma, beta):
         L = nat.lib()
         dev = X.device
         stream = nat.stream_of(X)
         M, K = X.shape
         Co = weight.shape[0]
         W = weight.reshape(Co, K)
-        Xop = prec.operand(X)
-        Z = prec.mm(Xop, prec.operand(W).t())  # (M, Co) fp32
+        use_batch = training or bn.running_mean is None
+        bf16 = prec.get() == "bf16"
+        gemm_part = None
+        wprep = None
+        Xop = X
+        if bf16:  # bf16 MFMA GEMM (gemm.hip) with the BN column statistics fused in its epilogue
+            if X16 is not None and X16.numel() and G.lds_ok_nt(X16, K):
+                # bf16 twin of the concat buffer + bf16 W / W^T: LDS-DMA staged operands
+                Xop = X16
+                wprep = G.prep_weight(weight, Co, K, False)
+                res = G.lds_xwt(X16, wprep[0], stats=use_batch)
+            else:
+                res = G.mm_xwt(X, W, stats=use_batch)
+            Z, gemm_part = res if use_batch else (res, None)
+        else:
+            Z = prec.mm(X, W.t())  # (M, Co) fp32
         scale = torch.empty(Co, dtype=torch.float32, device=dev)
         shift = torch.empty_like(scale)
         mean = torch.empty_like(scale)
         invstd = torch.empty_like(scale)
         out = torch.empty((B, Co, N), dtype=torch.float32, device=dev)
-        use_batch = training or bn.running_mean is None
         with torch.cuda.device(dev):
             if use_batch:
-                rows = L.dgx_colstats_rows(M)
-                partials = torch.empty((rows, 2, Co), dtype=torch.float32, device=dev)
-                nat.check(L.dgx_colstats_f32(nat.ptr(Z), Co, M, Co, nat.ptr(partials), rows, stream), "colstats")
+                if gemm_part is not None:
+                    partials, rows = gemm_part, gemm_part.shape[0]
+                else:
+                    rows = L.dgx_colstats_rows(M)
+                    partials = torch.empty((rows, 2, Co), dtype=torch.float32, device=dev)
+                    nat.check(L.dgx_colstats_f32(nat.ptr(Z), Co, M, Co, nat.ptr(partials), rows, stream),
+                              "colstats")
                 update = training and bn.running_mean is not None
                 factor = _bn_factor(bn) if update else 0.0
                 nat.check(L.dgx_bn_finalize_f32(
@@ -51,14 +69,15 @@ class _PointConvBNLReLU(torch.autograd.Function):
                     float(bn.eps), nat.ptr(scale), nat.ptr(shift), stream), "bn eval affine")
             nat.check(L.dgx_pointconv_apply_f32(nat.ptr(Z), Co, B, N, Co, nat.ptr(scale), nat.ptr(shift),
                                                   float(slope), nat.ptr(out), stream), "pointconv apply")
-        ctx.meta = (B, N, float(slope), use_batch)
+        ctx.meta = (B, N, float(slope), use_batch, bf16)
+        ctx.wprep = wprep
         ctx.save_for_backward(Xop, W, Z, scale, shift, mean, invstd)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         Xop, W, Z, scale, shift, mean, invstd = ctx.saved_tensors
-        B, N, slope, use_batch = ctx.meta
+        B, N, slope, use_batch, bf16 = ctx.meta
         L = nat.lib()
         dev = Z.device
         stream = nat.stream_of(Z)
@@ -71,7 +90,6 @@ class _PointConvBNLReLU(torch.autograd.Function):
         dbeta = torch.empty_like(dgamma)
         c0 = torch.zeros_like(dgamma)
         c1 = torch.zeros_like(dgamma)
-        bf16 = prec.get() == "bf16"
         dZ = torch.empty((M, Co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
         with torch.cuda.device(dev):
             nat.check(L.dgx_pointconv_bwd_f32(nat.ptr(dout), nat.ptr(Z), Co, B, N, Co, nat.ptr(scale),
@@ -87,22 +105,27 @@ class _PointConvBNLReLU(torch.autograd.Function):
                 dgamma.copy_(sums[1])
             nat.check(L.dgx_pointconv_input_grad(nat.ptr(dz), nat.ptr(Z), Co, M, Co, nat.ptr(scale), nat.ptr(c0),
                                              nat.ptr(c1), nat.ptr(dZ), int(bf16), stream), "pointconv dZ")
-        Wop = prec.operand(W)
-        if bf16:
-            dW = torch.mm(dZ.t(), Xop, out_dtype=torch.float32)
-            dX = torch.mm(dZ, Wop, out_dtype=torch.float32)
+        if bf16:  # bf16 MFMA: dW = dZ^T X (split-K, deterministic), dX = dZ W
+            dW = torch.empty((Co, Xop.shape[1]), dtype=torch.float32, device=dev)
+            if ctx.wprep is not None:
+                G.lds_atb(dZ, Xop, dW)
+                dX = G.lds_xwt(dZ, ctx.wprep[1])
+            else:
+                G.mm_atb(dZ, Xop, dW)
+                dX = G.mm_xw(dZ, W)
         else:
             dW = torch.mm(dZ.t(), Xop)
-            dX = torch.mm(dZ, Wop)
-        return dX, None, None, None, None, None, dW.view(Co, -1, 1, 1), dgamma, dbeta
+            dX = torch.mm(dZ, W)
+        return dX, None, None, None, None, None, None, dW.view(Co, -1, 1, 1), dgamma, dbeta
 
 
-def pointconv_bn_lrelu(X, B, N, seq, training):
+def pointconv_bn_lrelu(X, B, N, seq, training, X16=None):
     """X (B*N, K) point-major -> (B, Co, N) = LeakyReLU(BN(Conv1x1(X))) with the
     modules of ``seq`` = nn.Sequential(Conv2d(K,Co,1,bias=False), BatchNorm2d,
-    LeakyReLU) (reference dgcnn.py:74-78)."""
+    LeakyReLU) (reference dgcnn.py:74-78). ``X16``: optional bf16 twin of X
+    (precision "bf16"), the GEMM operand."""
     nat.require_device(X)
     conv, bn, act = seq[0], seq[1], seq[2]
     if conv.bias is not None or bn.weight is None:
         raise NotImplementedError("dgx pointconv expects Conv(bias=False) + affine BatchNorm")
-    return _PointConvBNLReLU.apply(X, B, N, bn, act.negative_slope, training, conv.weight, bn.weight, bn.bias)
+    return _PointConvBNLReLU.apply(X, X16, B, N, bn, act.negative_slope, training, conv.weight, bn.weight, bn.bias)

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from dgx import ops as _ops
-from dgx.edgeconv import edgeconv_stack
+from dgx.edgeconv import edgeconv_stack_pair
 from dgx.pointconv import pointconv_bn_lrelu
 
 
@@ -63,6 +63,6 @@ class DGCNN(nn.Module):
     def forward(self, x):
         batch_size, _, num_points = x.size()
         # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)
-        feats = edgeconv_stack(x, self.k, self.edge_blocks(), self.training)   # (B*N, 512)
+        feats, feats16 = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training)   # (B*N, 512)
         # conv5 -> BN -> LeakyReLU (dgcnn.py:100-102), written as (B, emb, N)
-        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training)
+        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training, X16=feats16)

@@ -110,7 +110,7 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         void* stream);
 int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
                            const float* shift, float slope, float* out, int ldo,
-                           void* stream);
+                           void* out_bf16, void* stream);
 /* Eval-mode forward in one launch: out = LeakyReLU(a*sel + b), a,b from
  * running stats (dgx_bn_eval_affine_f32). */
 int dgx_bn_eval_affine_f32(int Co, const float* gamma, const float* beta,
@@ -147,7 +147,8 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
                              const int32_t* edges, const float* dzp,
                              const float* sumP, int B, int N, int k, int Co,
                              const float* scale, const float* c0,
-                             const float* c1, float* dPQ, void* stream);
+                             const float* c1, void* dPQ, int out_bf16,
+                             void* stream);
 
 /* ---- a4: pointwise Conv1x1 + BatchNorm + LeakyReLU, replaces conv5 of
  * models/dgcnn.py:74-78, 100-102 (cat(x1..x4) -> Conv2d(512,emb,1) -> BN ->
@@ -178,6 +179,48 @@ int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M
                          const float* c1, void* dZ, int bf16, void* stream);
 int dgx_to_bf16(const float* src, int64_t ld, int64_t rows, int cols, void* dst,
                 void* stream);
+
+/* ---- a3/a4/a8: the Conv2d(1x1) GEMMs of the chain, bf16 MFMA ----------------
+ * Replace the reference's per-edge conv GEMMs (models/dgcnn.py:55-73, K11) and
+ * conv5 (dgcnn.py:74-78, 100-102, K15) plus their autograd dgrad/wgrad, in the
+ * decomposed per-point form:
+ *   C[i][j] = sum_k opA(i,k) * opB(j,k),  i < M, j < N, k < K
+ *   opA(i,k) = A[i*lda + k] (a_ic = 0) or A[k*lda + i] (a_ic = 1), same for B.
+ * A/B are fp32 (x_bf16 = 0) or bf16 (1); operands are rounded to bf16 (RNE)
+ * when staged, products accumulate in fp32, C is fp32 with row stride ldc.
+ * epi: 0 store, 1 accumulate (C += ...), 2 store + column statistics
+ * (partials[dgx_gemm_stats_rows(M)][2][N] = per 128-row block sum, sum of
+ * squares; feeds dgx_bn_finalize_f32), 3 split-K slabs: C is a dense
+ * [splits][M][N] workspace (ldc ignored), summed by dgx_slab_reduce_f32.
+ * Supported layouts: (fp32 KC, fp32 KC) epi 0/2; (fp32|bf16 KC, fp32 IC)
+ * epi 0/1; (fp32|bf16 IC, fp32 IC) epi 3. Others: DGX_EUNSUPPORTED. */
+int dgx_gemm_stats_rows(int M);
+int dgx_gemm_splits(int M, int N, int K);
+int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda,
+                  const void* B, int b_bf16, int b_ic, int64_t ldb,
+                  int M, int N, int K, int epi, int splits,
+                  float* C, int64_t ldc, float* partials, void* stream);
+/* out[orow][ocol] = sum_s slab[s][r][c] (fixed order: deterministic); rows
+ * r >= split land at (r - split, c + cols): the [W1;W2] -> [W1 | W2] weight
+ * un-stacking (reference conv weight layout (Co, 2C, 1, 1)). */
+int dgx_slab_reduce_f32(const float* slab, int S, int rows, int cols, int split,
+                        float* out, int64_t ldo, void* stream);
+/* The same GEMMs with bf16 operands in HBM, staged by LDS-DMA
+ * (global_load_lds) into swizzled LDS images. tn = 0: C = A B^T with A (M,K)
+ * and B (N,K) k-contiguous, K % 64 == 0, epi 0/1/2. tn = 1: C = A^T B with A
+ * (K,M), B (K,N) row-major (the weight gradients), M, N multiples of 8, epi 3
+ * (split-K slabs). lda, ldb multiples of 8, 16-byte aligned bases; anything
+ * else returns DGX_EUNSUPPORTED (callers then use dgx_gemm_bf16). With epi 1
+ * and addend != NULL: C = addend (row stride ldd) + A B^T (C need not hold data). */
+int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int tn,
+                      int M, int N, int K, int epi, int splits, float* C,
+                      int64_t ldc, float* partials, const float* addend,
+                      int64_t ldd, void* stream);
+/* bf16 weight operands per step: nt = [rows][C], tn = its transpose. stacked
+ * != 0: W is an EdgeConv weight (Co, 2C) (dgcnn.py:55) and rows = 2Co are
+ * [W1; W2]; else W is (Co, C) (conv5, dgcnn.py:74). */
+int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt,
+                         void* tn, void* stream);
 
 #ifdef __cplusplus
 }

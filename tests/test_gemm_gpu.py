@@ -1,0 +1,189 @@
+"""bf16 MFMA GEMMs (csrc/gemm.hip) against a plain fp32/fp64 PyTorch reference of
+the same op on the bf16-rounded operands (the kernel rounds operands to bf16
+RNE and accumulates in fp32, so only the summation order differs: 1e-5 rel).
+Covers every layout/epilogue the engine launches, ragged M/N/K, the K=3 first
+layer, column slices of the concat buffer, the fused BatchNorm statistics,
+split-K slabs with the [W1;W2] -> [W1|W2] un-stacking, and determinism."""
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).double()
+
+
+def _ref(a, b):  # a (M,K), b (N,K) in fp64 of bf16-rounded values
+    return (_bf(a) @ _bf(b).t()).cpu()
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 1024, 512), (1000, 200, 64), (777, 128, 3), (130, 64, 45),
+                                   (4096, 512, 128), (1, 1, 1)])
+def test_xwt_store_and_stats(cuda, M, N, K):
+    from dgx import gemm as G
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=cuda)
+    w = torch.randn(N, K, device=cuda) * 0.1
+    ref = _ref(x, w)
+    z = G.mm_xwt(x, w)
+    assert rel_err(z.cpu().numpy(), ref.numpy()) < TOL
+    z2, part = G.mm_xwt(x, w, stats=True)
+    assert torch.equal(z, z2)
+    ps = part.double().sum(0).cpu()
+    zd = z.double().cpu()
+    assert rel_err(ps[0].numpy(), zd.sum(0).numpy()) < 1e-4
+    assert rel_err(ps[1].numpy(), (zd * zd).sum(0).numpy()) < 1e-5
+
+
+def test_xwt_strided_slice_of_concat_buffer(cuda):
+    from dgx import gemm as G
+    torch.manual_seed(1)
+    xcat = torch.randn(3000, 512, device=cuda)
+    X = xcat[:, 128:256]           # a block's input columns
+    w = torch.randn(512, 128, device=cuda)
+    assert rel_err(G.mm_xwt(X, w).cpu().numpy(), _ref(X, w).numpy()) < TOL
+    xpm = torch.randn(2, 517, 3, device=cuda).reshape(-1, 3)  # first layer, K = 3, ld = 3
+    w3 = torch.randn(128, 3, device=cuda)
+    assert rel_err(G.mm_xwt(xpm, w3).cpu().numpy(), _ref(xpm, w3).numpy()) < TOL
+
+
+@pytest.mark.parametrize("a_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(32768, 512, 1024), (1000, 64, 128), (333, 128, 512), (70, 3, 128)])
+def test_xw_store_and_accumulate(cuda, a_dtype, M, N, K):
+    from dgx import gemm as G
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device=cuda).to(a_dtype)
+    w = torch.randn(K, N, device=cuda) * 0.05
+    ref = (_bf(x.float()) @ _bf(w)).cpu()
+    y = G.mm_xw(x, w)
+    assert rel_err(y.cpu().numpy(), ref.numpy()) < TOL
+    base = torch.randn(M, N + 5, device=cuda)
+    dst = base.clone()
+    G.mm_xw(x, w, out=dst[:, 2:2 + N], accumulate=True)
+    exp = base.double().cpu()
+    exp[:, 2:2 + N] += ref
+    assert rel_err(dst.cpu().numpy(), exp.numpy()) < TOL
+
+
+@pytest.mark.parametrize("a_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("R,M,N", [(32768, 1024, 512), (32768, 512, 128), (5000, 128, 64), (999, 128, 3),
+                                   (64, 40, 20)])
+def test_atb_split_k(cuda, a_dtype, R, M, N):
+    from dgx import gemm as G
+    torch.manual_seed(R + M)
+    a = torch.randn(R, M, device=cuda).to(a_dtype)
+    b = torch.randn(R, N, device=cuda)
+    ref = (_bf(a.float()).t() @ _bf(b)).cpu()
+    out = torch.empty(M, N, device=cuda)
+    G.mm_atb(a, b, out)
+    assert rel_err(out.cpu().numpy(), ref.numpy()) < TOL
+    out2 = torch.empty(M, N, device=cuda)
+    G.mm_atb(a, b, out2)
+    assert torch.equal(out, out2), "split-K slab sum must be deterministic"
+
+
+def test_atb_unstacks_edge_weight(cuda):
+    """dW of an EdgeConv block: rows [0,Co) are the x_j half, rows [Co,2Co) the
+    x_i half; the reference weight is (Co, 2C) = [W1 | W2] (dgcnn.py:55)."""
+    from dgx import gemm as G
+    torch.manual_seed(3)
+    co, c, R = 64, 64, 4096
+    dpq = torch.randn(R, 2 * co, device=cuda)
+    X = torch.randn(R, 512, device=cuda)[:, 64:64 + c]
+    full = (_bf(dpq).t() @ _bf(X)).cpu()
+    gw = torch.empty(co, 2 * c, device=cuda)
+    G.mm_atb(dpq, X, gw, split_rows=co)
+    exp = torch.cat([full[:co], full[co:]], dim=1)
+    assert rel_err(gw.cpu().numpy(), exp.numpy()) < TOL
+
+
+def test_gemm_rejects_unsupported(cuda):
+    from dgx import _native as nat
+    x = torch.randn(16, 16, device=cuda)
+    L = nat.lib()
+    # (bf16 KC, fp32 KC) with accumulate is not a layout the engine launches
+    rc = L.dgx_gemm_bf16(nat.ptr(x), 1, 0, 16, nat.ptr(x), 0, 0, 16, 16, 16, 16, 1, 1, nat.ptr(x), 16, None,
+                         nat.stream_of(x))
+    assert rc == -2
+    assert L.dgx_gemm_bf16(None, 0, 0, 16, nat.ptr(x), 0, 0, 16, 16, 16, 16, 0, 1, nat.ptr(x), 16, None,
+                           nat.stream_of(x)) == -1
+
+
+# ---- bf16-operand path: LDS-DMA staging (global_load_lds), transposed reads ----
+
+@pytest.mark.parametrize("M,N,K", [(32768, 1024, 512), (1000, 128, 64), (777, 64, 128), (3000, 512, 1024),
+                                   (129, 200, 192)])
+def test_lds_xwt_store_stats_addend(cuda, M, N, K):
+    from dgx import gemm as G
+    torch.manual_seed(M + 3 * N + K)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.1).to(torch.bfloat16)
+    ref = (x.double() @ w.double().t()).cpu()
+    z = G.lds_xwt(x, w)
+    assert rel_err(z.cpu().numpy(), ref.numpy()) < TOL
+    z2, part = G.lds_xwt(x, w, stats=True)
+    assert torch.equal(z, z2)
+    ps = part.double().sum(0).cpu()
+    zd = z.double().cpu()
+    assert rel_err(ps[0].numpy(), zd.sum(0).numpy()) < 1e-4
+    assert rel_err(ps[1].numpy(), (zd * zd).sum(0).numpy()) < 1e-5
+    add = torch.randn(M, N + 8, device=cuda)[:, 3:3 + N]
+    dst = torch.full((M, N + 16), 7.0, device=cuda)[:, 8:8 + N]
+    G.lds_xwt(x, w, out=dst, addend=add)
+    assert rel_err(dst.cpu().numpy(), (add.double().cpu() + ref).numpy()) < TOL
+
+
+def test_lds_xwt_concat_slice_operand(cuda):
+    from dgx import gemm as G
+    torch.manual_seed(5)
+    xcat = torch.randn(2048, 512, device=cuda).to(torch.bfloat16)
+    X = xcat[:, 128:256]
+    w = torch.randn(512, 128, device=cuda).to(torch.bfloat16)
+    ref = (X.double() @ w.double().t()).cpu()
+    assert rel_err(G.lds_xwt(X, w).cpu().numpy(), ref.numpy()) < TOL
+
+
+@pytest.mark.parametrize("R,M,N", [(32768, 1024, 512), (32768, 512, 128), (5000, 128, 64), (1000, 256, 64),
+                                   (100, 64, 64), (4099, 128, 128)])
+def test_lds_atb_split_k(cuda, R, M, N):
+    from dgx import gemm as G
+    torch.manual_seed(R + M + N)
+    a = torch.randn(R, M, device=cuda).to(torch.bfloat16)
+    b = torch.randn(R, N, device=cuda).to(torch.bfloat16)
+    ref = (a.double().t() @ b.double()).cpu()
+    out = torch.empty(M, N, device=cuda)
+    G.lds_atb(a, b, out)
+    assert rel_err(out.cpu().numpy(), ref.numpy()) < TOL
+    out2 = torch.empty(M, N, device=cuda)
+    G.lds_atb(a, b, out2)
+    assert torch.equal(out, out2)
+
+
+def test_lds_atb_strided_concat_operand_and_unstack(cuda):
+    from dgx import gemm as G
+    torch.manual_seed(9)
+    co, c, R = 128, 64, 6000
+    dpq = torch.randn(R, 2 * co, device=cuda).to(torch.bfloat16)
+    X = torch.randn(R, 512, device=cuda).to(torch.bfloat16)[:, 64:64 + c]
+    full = (dpq.double().t() @ X.double()).cpu()
+    gw = torch.empty(co, 2 * c, device=cuda)
+    G.lds_atb(dpq, X, gw, split_rows=co)
+    exp = torch.cat([full[:co], full[co:]], dim=1)
+    assert rel_err(gw.cpu().numpy(), exp.numpy()) < TOL
+
+
+@pytest.mark.parametrize("co,c,stacked", [(64, 64, True), (256, 128, True), (1024, 512, False)])
+def test_weight_prep(cuda, co, c, stacked):
+    from dgx import gemm as G
+    torch.manual_seed(co)
+    w = torch.randn(co, 2 * c if stacked else c, 1, 1, device=cuda)
+    nt, tn = G.prep_weight(w, co, c, stacked)
+    w2 = w.reshape(co, -1)
+    exp = torch.cat([w2[:, :c], w2[:, c:]], dim=0) if stacked else w2
+    assert torch.equal(nt, exp.to(torch.bfloat16))
+    assert torch.equal(tn, exp.t().contiguous().to(torch.bfloat16))

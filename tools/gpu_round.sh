@@ -17,7 +17,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-    step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf --timeout 600
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 900 python bench.py --steps 20 --warmup 5
