@@ -36,7 +36,7 @@ constexpr int GB_BM = 128;
 constexpr int GB_BK = 32;
 constexpr int GB_LDK = GB_BK + 8;  // bf16 per LDS row (80 B)
 
-enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3 };
+enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4 };
 
 template <typename T> struct VecOf;
 template <> struct VecOf<float> { static constexpr int V = 4; typedef float4 type; };
@@ -488,12 +488,13 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
                 const float v = acc[a][b][r];
                 float* dst = out + (int64_t)i * ldc + j;
                 if (EPI == EPI_ACCUM) *dst = (addend ? addend[(int64_t)i * ldd + j] : *dst) + v;
+                else if (EPI == EPI_STATS16) reinterpret_cast<bf16*>(out)[(int64_t)i * ldc + j] = (bf16)v;
                 else *dst = v;
-                if (EPI == EPI_STATS) { s1[b] += v; s2[b] = fmaf(v, v, s2[b]); }
+                if (EPI == EPI_STATS || EPI == EPI_STATS16) { s1[b] += v; s2[b] = fmaf(v, v, s2[b]); }
             }
         }
     }
-    if (EPI == EPI_STATS) {
+    if (EPI == EPI_STATS || EPI == EPI_STATS16) {
         float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
 #pragma unroll
         for (int b = 0; b < TN_; ++b) {
@@ -624,7 +625,7 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
                       int epi, int splits, float* C, int64_t ldc, float* partials, const float* addend,
                       int64_t ldd, void* stream) {
     if (!A || !B || !C || M < 0 || N < 0 || K < 0 || splits < 1) return DGX_EINVAL;
-    if (epi == EPI_STATS && !partials) return DGX_EINVAL;
+    if ((epi == EPI_STATS || epi == EPI_STATS16) && !partials) return DGX_EINVAL;
     if (M == 0 || N == 0) return DGX_OK;
     // DMA staging moves 16-B chunks: rows 16-B aligned, whole chunks per row
     if (!aligned_to(A, 16) || !aligned_to(B, 16) || lda % 8 || ldb % 8) return DGX_EUNSUPPORTED;
@@ -646,6 +647,7 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
     if (epi == EPI_STORE) DGX_G2(EPI_STORE);
     if (epi == EPI_ACCUM) DGX_G2(EPI_ACCUM);
     if (epi == EPI_STATS) DGX_G2(EPI_STATS);
+    if (epi == EPI_STATS16) DGX_G2(EPI_STATS16);
 #undef DGX_G2
     return DGX_EUNSUPPORTED;
 }

@@ -14,6 +14,7 @@
 // the MFMA A operand read (lane l -> c = 4t + l/16, j = l%16) is a contiguous,
 // conflict-free 256 B per wave.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -509,6 +510,8 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
         hipLaunchKernelGGL((knn_kernel<NSTEP, KB, false>), grid, block, 0, st, x, sB, sC, sN, xx, B, C, N, k,
                            nqb, idx64, idx32, vals);
     if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH;
+    static const bool nofix = getenv("DGX_KNN_NOFIX") != nullptr;  // diagnostics: leave flagged rows marked
+    if (nofix) return DGX_OK;
     const int64_t rows = (int64_t)B * N;
     hipLaunchKernelGGL(knn_fix_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, x, sB, sC, sN, xx,
                        B, C, N, k, idx64, idx32, vals);

@@ -141,6 +141,165 @@ __global__ void to_bf16_kernel(const float* __restrict__ src, int64_t lds_, int6
     }
 }
 
+// ---- bf16 Z (precision "bf16": the conv5 GEMM stores Z as bf16, as autocast
+// stores a conv output; statistics come from the fp32 accumulators) ----------
+// Register transposes, no LDS: a lane owns a 4-point x 8-channel micro-tile.
+// Z / dZ (point-major bf16) move as one 16-B access per point, dout / out
+// ((B,C,N) fp32) as one 16-B access per channel; lane = (channel group
+// cg = lane & 7, point group pg = lane >> 3), so every wave-instruction covers
+// 8 segments of 128 contiguous bytes on both sides. Block = 4 waves = 64
+// channels x 128 points; grid (B * ceil(N/128), ceil(C/64)).
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int RT_P = 128;  // points per block
+
+struct RtTile {
+    int b, n, o;  // cloud, first point, first channel of this lane's micro-tile
+    __device__ __forceinline__ RtTile(int N) {
+        const int nt = (N + RT_P - 1) / RT_P;
+        b = blockIdx.x / nt;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        n = (blockIdx.x - b * nt) * RT_P + w * 32 + (lane >> 3) * 4;
+        o = blockIdx.y * 64 + (lane & 7) * 8;
+    }
+};
+
+__device__ __forceinline__ void load_z8(const bf16* __restrict__ Z, int64_t row, int C, int o, bool ok, float (&z)[8]) {
+    if (ok && o + 8 <= C && (C % 8) == 0) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Z + row * C + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[j] = (float)v[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[j] = (ok && o + j < C) ? (float)Z[row * C + o + j] : 0.f;
+    }
+}
+
+// 4 consecutive points of channel row `oo` of a (B,C,N) fp32 tensor
+__device__ __forceinline__ float4 load_row4(const float* __restrict__ p, int64_t rowbase, int n, int N, bool ok) {
+    if (!ok || n >= N) return make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((N % 4) == 0) return *reinterpret_cast<const float4*>(p + rowbase + n);
+    float v[4];
+    for (int i = 0; i < 4; ++i) v[i] = n + i < N ? p[rowbase + n + i] : 0.f;
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void store_row4(float* __restrict__ p, int64_t rowbase, int n, int N, const float (&v)[4]) {
+    if (n >= N) return;
+    if ((N % 4) == 0) {
+        *reinterpret_cast<float4*>(p + rowbase + n) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int i = 0; i < 4 && n + i < N; ++i) p[rowbase + n + i] = v[i];
+    }
+}
+
+// out(b, o, n) = LeakyReLU(a_o z + b_o)
+__global__ __launch_bounds__(256) void apply16_T_kernel(const bf16* __restrict__ Z, int N, int C,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, float slope,
+                                                        float* __restrict__ out) {
+    const RtTile T(N);
+    float z[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load_z8(Z, (int64_t)T.b * N + T.n + i, C, T.o, T.n + i < N, z[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int oo = T.o + j;
+        if (oo >= C) break;
+        const float a = scale[oo], sh = shift[oo];
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(a, z[i][j], sh), slope);
+        store_row4(out, ((int64_t)T.b * C + oo) * N, T.n, N, v);
+    }
+}
+
+// PASS 0: per-block partial (sum d, sum d*zhat) with d = dout * LeakyReLU'(a z + b)
+//         (the train-mode BatchNorm backward reductions); nothing else is written.
+// PASS 1: dZ = a d + c0 + c1 z (BN train-mode input gradient, bf16 point-major):
+//         the operand of the two weight/input-gradient GEMMs.
+template <int PASS>
+__global__ __launch_bounds__(256) void bwd16_kernel(const float* __restrict__ dout, const bf16* __restrict__ Z, int N,
+                                                    int C, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, const float* __restrict__ mean,
+                                                    const float* __restrict__ invstd, float slope,
+                                                    const float* __restrict__ c0, const float* __restrict__ c1,
+                                                    float* __restrict__ partials, bf16* __restrict__ dZ) {
+    __shared__ float red[2][4][64];
+    const RtTile T(N);
+    float z[4][8], g[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float4 v = load_row4(dout, ((int64_t)T.b * C + T.o + j) * N, T.n, N, T.o + j < C);
+        g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load_z8(Z, (int64_t)T.b * N + T.n + i, C, T.o, T.n + i < N, z[i]);
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const bool ok = T.o + j < C;
+        const int oj = ok ? T.o + j : 0;
+        const float a = scale[oj], sh = shift[oj];
+        if (PASS == 0) {
+            const float mu = mean[oj], is = invstd[oj];
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float d = g[j][i] * (fmaf(a, z[i][j], sh) > 0.f ? 1.f : slope);
+                t1 += d;
+                t2 = fmaf(d, (z[i][j] - mu) * is, t2);
+            }
+            s1[j] = t1;
+            s2[j] = t2;
+        } else {
+            const float k0 = c0[oj], k1 = c1[oj];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float d = g[j][i] * (fmaf(a, z[i][j], sh) > 0.f ? 1.f : slope);
+                z[i][j] = fmaf(a, d, fmaf(k1, z[i][j], k0));  // dZ, reusing the registers
+            }
+        }
+    }
+    if (PASS == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = T.n + i;
+            if (n >= N) break;
+            const int64_t row = (int64_t)T.b * N + n;
+            if (T.o + 8 <= C && (C % 8) == 0) {
+                bf16x8 w;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) w[j] = (bf16)z[i][j];
+                *reinterpret_cast<bf16x8*>(dZ + row * C + T.o) = w;
+            } else {
+                for (int j = 0; j < 8 && T.o + j < C; ++j) dZ[row * C + T.o + j] = (bf16)z[i][j];
+            }
+        }
+        return;
+    }
+    // lanes of one channel group: l, l^8, l^16, l^32 in the wave, then the 4 waves
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int m = 8; m < 64; m <<= 1) {
+            s1[j] += __shfl_xor(s1[j], m);
+            s2[j] += __shfl_xor(s2[j], m);
+        }
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { red[0][w][lane * 8 + j] = s1[j]; red[1][w][lane * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+    const int t = threadIdx.x, o0 = blockIdx.y * 64;
+    if (t < 64 && o0 + t < C) {
+        partials[(int64_t)blockIdx.x * 2 * C + o0 + t] = ((red[0][0][t] + red[0][1][t]) + red[0][2][t]) + red[0][3][t];
+        partials[(int64_t)blockIdx.x * 2 * C + C + o0 + t] = ((red[1][0][t] + red[1][1][t]) + red[1][2][t]) + red[1][3][t];
+    }
+}
+
 inline int grid_for(int64_t total, int block) {
     int64_t g = (total + block - 1) / block;
     return (int)(g < 16384 ? (g < 1 ? 1 : g) : 16384);
@@ -196,6 +355,36 @@ int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M
     else
         hipLaunchKernelGGL(bwd_dZ_kernel<false>, dim3(g), dim3(256), 0, dgx_stream(stream), dz, Z, ldz, M, C, scale,
                            c0, c1, dZ);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_pointconv_bf16_rows(int B, int N) {
+    if (B < 1 || N < 1) return DGX_EINVAL;
+    return B * ((N + RT_P - 1) / RT_P);
+}
+
+int dgx_pointconv_apply_bf16(const void* Z, int B, int N, int C, const float* scale, const float* shift, float slope,
+                             float* out, void* stream) {
+    if (!Z || !scale || !shift || !out || B < 1 || N < 1 || C < 1) return DGX_EINVAL;
+    dim3 grid(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64);
+    hipLaunchKernelGGL(apply16_T_kernel, grid, dim3(256), 0, dgx_stream(stream), static_cast<const bf16*>(Z), N, C,
+                       scale, shift, slope, out);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_pointconv_bwd_bf16(const float* dout, const void* Z, int B, int N, int C, const float* scale,
+                           const float* shift, const float* mean, const float* invstd, float slope, const float* c0,
+                           const float* c1, float* partials, void* dZ, int pass, void* stream) {
+    if (!dout || !Z || !scale || !shift || B < 1 || N < 1 || C < 1) return DGX_EINVAL;
+    if (pass == 0 ? (!mean || !invstd || !partials) : (!c0 || !c1 || !dZ)) return DGX_EINVAL;
+    dim3 grid(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64);
+    const bf16* z = static_cast<const bf16*>(Z);
+    if (pass == 0)
+        hipLaunchKernelGGL(bwd16_kernel<0>, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean,
+                           invstd, slope, c0, c1, partials, static_cast<bf16*>(dZ));
+    else
+        hipLaunchKernelGGL(bwd16_kernel<1>, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean,
+                           invstd, slope, c0, c1, partials, static_cast<bf16*>(dZ));
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -10,7 +10,7 @@ import torch
 
 from . import _native as nat
 
-EPI_STORE, EPI_ACCUM, EPI_STATS, EPI_SLAB = 0, 1, 2, 3
+EPI_STORE, EPI_ACCUM, EPI_STATS, EPI_SLAB, EPI_STATS16 = 0, 1, 2, 3, 4
 
 
 def _operand(t, ic):
@@ -92,18 +92,22 @@ def _bf16_2d(t):
     return t.stride(0) if t.shape[0] > 1 else max(8, t.shape[1])
 
 
-def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None):
+def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None, out_bf16=False):
     """out (M,N) = x16 (M,K) @ w16 (N,K)^T (bf16 operands, K % 64 == 0).
-    ``stats``: also returns the BatchNorm column partials (rows, 2, N).
+    ``stats``: also returns the BatchNorm column partials (rows, 2, N);
+    with ``out_bf16`` the product is stored bf16 (stats from the fp32 sums).
     ``accumulate``: out += ...; with ``addend``: out = addend + ... ."""
     M, K = x16.shape
     N = w16.shape[0]
     if out is None:
-        out = torch.empty((M, N), dtype=torch.float32, device=x16.device)
+        out = torch.empty((M, N), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x16.device)
     part = None
     if stats:
         part = torch.empty((nat.lib().dgx_gemm_stats_rows(M), 2, N), dtype=torch.float32, device=x16.device)
-    epi = EPI_STATS if stats else (EPI_ACCUM if (accumulate or addend is not None) else EPI_STORE)
+    if out_bf16 and not stats:
+        raise RuntimeError("dgx gemm: a bf16 product is only stored together with its statistics")
+    epi = (EPI_STATS16 if out_bf16 else EPI_STATS) if stats else (
+        EPI_ACCUM if (accumulate or addend is not None) else EPI_STORE)
     with torch.cuda.device(out.device):
         nat.check(nat.lib().dgx_gemm_lds_bf16(
             nat.ptr(x16), _bf16_2d(x16), nat.ptr(w16), _bf16_2d(w16), 0, M, N, K, epi, 1, nat.ptr(out),

@@ -31,15 +31,18 @@ class _PointConvBNLReLU(torch.autograd.Function):
         gemm_part = None
         wprep = None
         Xop = X
+        z16 = False
         if bf16:  # bf16 MFMA GEMM (gemm.hip) with the BN column statistics fused in its epilogue
             if X16 is not None and X16.numel() and G.lds_ok_nt(X16, K):
-                # bf16 twin of the concat buffer + bf16 W / W^T: LDS-DMA staged operands
+                # bf16 twin of the concat buffer + bf16 W / W^T: LDS-DMA staged operands;
+                # Z is stored bf16 (as autocast stores a conv output), stats from fp32 sums
                 Xop = X16
                 wprep = G.prep_weight(weight, Co, K, False)
-                res = G.lds_xwt(X16, wprep[0], stats=use_batch)
+                Z, gemm_part = G.lds_xwt(X16, wprep[0], stats=True, out_bf16=True)
+                z16 = True
             else:
                 res = G.mm_xwt(X, W, stats=use_batch)
-            Z, gemm_part = res if use_batch else (res, None)
+                Z, gemm_part = res if use_batch else (res, None)
         else:
             Z = prec.mm(X, W.t())  # (M, Co) fp32
         scale = torch.empty(Co, dtype=torch.float32, device=dev)
@@ -67,8 +70,15 @@ class _PointConvBNLReLU(torch.autograd.Function):
                 nat.check(L.dgx_bn_eval_affine_f32(
                     Co, nat.ptr(gamma), nat.ptr(beta), nat.ptr(bn.running_mean), nat.ptr(bn.running_var),
                     float(bn.eps), nat.ptr(scale), nat.ptr(shift), stream), "bn eval affine")
-            nat.check(L.dgx_pointconv_apply_f32(nat.ptr(Z), Co, B, N, Co, nat.ptr(scale), nat.ptr(shift),
-                                                  float(slope), nat.ptr(out), stream), "pointconv apply")
+                # z-hat of the running statistics, for dgamma if eval-mode output is differentiated
+                mean.copy_(bn.running_mean)
+                invstd.copy_(torch.rsqrt(bn.running_var + bn.eps))
+            if z16:
+                nat.check(L.dgx_pointconv_apply_bf16(nat.ptr(Z), B, N, Co, nat.ptr(scale), nat.ptr(shift),
+                                                     float(slope), nat.ptr(out), stream), "pointconv apply bf16")
+            else:
+                nat.check(L.dgx_pointconv_apply_f32(nat.ptr(Z), Co, B, N, Co, nat.ptr(scale), nat.ptr(shift),
+                                                    float(slope), nat.ptr(out), stream), "pointconv apply")
         ctx.meta = (B, N, float(slope), use_batch, bf16)
         ctx.wprep = wprep
         ctx.save_for_backward(Xop, W, Z, scale, shift, mean, invstd)
@@ -83,8 +93,8 @@ class _PointConvBNLReLU(torch.autograd.Function):
         stream = nat.stream_of(Z)
         M, Co = Z.shape
         dout = dout.contiguous()
-        dz = torch.empty((M, Co), dtype=torch.float32, device=dev)
-        rows = L.dgx_pointconv_bwd_rows(B, N)
+        z16 = Z.dtype == torch.bfloat16
+        rows = L.dgx_pointconv_bf16_rows(B, N) if z16 else L.dgx_pointconv_bwd_rows(B, N)
         partials = torch.empty((rows, 2, Co), dtype=torch.float32, device=dev)
         dgamma = torch.empty(Co, dtype=torch.float32, device=dev)
         dbeta = torch.empty_like(dgamma)
@@ -92,19 +102,31 @@ class _PointConvBNLReLU(torch.autograd.Function):
         c1 = torch.zeros_like(dgamma)
         dZ = torch.empty((M, Co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
         with torch.cuda.device(dev):
-            nat.check(L.dgx_pointconv_bwd_f32(nat.ptr(dout), nat.ptr(Z), Co, B, N, Co, nat.ptr(scale),
-                                                nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), slope, nat.ptr(dz),
-                                                nat.ptr(partials), stream), "pointconv bwd")
+            if z16:  # two passes over (dout, Z): BN-backward reductions, then dZ directly
+                nat.check(L.dgx_pointconv_bwd_bf16(nat.ptr(dout), nat.ptr(Z), B, N, Co, nat.ptr(scale),
+                                                   nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), slope, None, None,
+                                                   nat.ptr(partials), None, 0, stream), "pointconv bwd stats")
+            else:
+                dz = torch.empty((M, Co), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_pointconv_bwd_f32(nat.ptr(dout), nat.ptr(Z), Co, B, N, Co, nat.ptr(scale),
+                                                  nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), slope, nat.ptr(dz),
+                                                  nat.ptr(partials), stream), "pointconv bwd")
             if use_batch:
                 nat.check(L.dgx_bn_bwd_finalize_f32(nat.ptr(partials), rows, Co, float(M), nat.ptr(scale),
                                                     nat.ptr(mean), nat.ptr(invstd), nat.ptr(dgamma), nat.ptr(dbeta),
                                                     nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
-            else:  # running-stats BN: affine only; dgamma needs z-hat of the running stats
+            else:  # running-stats BN: affine only
                 sums = partials.sum(0)
                 dbeta.copy_(sums[0])
                 dgamma.copy_(sums[1])
-            nat.check(L.dgx_pointconv_input_grad(nat.ptr(dz), nat.ptr(Z), Co, M, Co, nat.ptr(scale), nat.ptr(c0),
-                                             nat.ptr(c1), nat.ptr(dZ), int(bf16), stream), "pointconv dZ")
+            if z16:
+                nat.check(L.dgx_pointconv_bwd_bf16(nat.ptr(dout), nat.ptr(Z), B, N, Co, nat.ptr(scale),
+                                                   nat.ptr(shift), None, None, slope, nat.ptr(c0), nat.ptr(c1), None,
+                                                   nat.ptr(dZ), 1, stream), "pointconv bwd dZ")
+            else:
+                nat.check(L.dgx_pointconv_input_grad(nat.ptr(dz), nat.ptr(Z), Co, M, Co, nat.ptr(scale),
+                                                     nat.ptr(c0), nat.ptr(c1), nat.ptr(dZ), int(bf16), stream),
+                          "pointconv dZ")
         if bf16:  # bf16 MFMA: dW = dZ^T X (split-K, deterministic), dX = dZ W
             dW = torch.empty((Co, Xop.shape[1]), dtype=torch.float32, device=dev)
             if ctx.wprep is not None:

@@ -179,6 +179,24 @@ int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M
                          const float* c1, void* dZ, int bf16, void* stream);
 int dgx_to_bf16(const float* src, int64_t ld, int64_t rows, int cols, void* dst,
                 void* stream);
+/* conv5 with a bf16 Z (precision "bf16": dgx_gemm_lds_bf16 epi 4 stores Z as
+ * bf16 (M x C, row stride C) with the BN statistics taken from the fp32
+ * accumulators — what autocast stores for a conv output).
+ *   dgx_pointconv_apply_bf16: out (B,C,N) = LeakyReLU(scale*z + shift).
+ *   dgx_pointconv_bwd_bf16 pass 0: partials[dgx_pointconv_bf16_rows(B,N)][2][C]
+ *     = per 128-point tile (sum d, sum d*zhat), d = dout * LeakyReLU'(scale*z + shift), zhat =
+ *     (z - mean) * invstd; -> dgx_bn_bwd_finalize_f32 -> c0, c1.
+ *   pass 1: dZ (bf16, M x C) = scale*d + c0 + c1*z — the GEMM operand of
+ *     dW5 = dZ^T X and dX = dZ W5. Replace the reference's autograd of
+ *     conv5 + BatchNorm2d + LeakyReLU (dgcnn.py:74-78, 102). */
+int dgx_pointconv_bf16_rows(int B, int N);
+int dgx_pointconv_apply_bf16(const void* Z, int B, int N, int C, const float* scale,
+                             const float* shift, float slope, float* out, void* stream);
+int dgx_pointconv_bwd_bf16(const float* dout, const void* Z, int B, int N, int C,
+                           const float* scale, const float* shift, const float* mean,
+                           const float* invstd, float slope, const float* c0,
+                           const float* c1, float* partials, void* dZ, int pass,
+                           void* stream);
 
 /* ---- a3/a4/a8: the Conv2d(1x1) GEMMs of the chain, bf16 MFMA ----------------
  * Replace the reference's per-edge conv GEMMs (models/dgcnn.py:55-73, K11) and
@@ -189,6 +207,7 @@ int dgx_to_bf16(const float* src, int64_t ld, int64_t rows, int cols, void* dst,
  * A/B are fp32 (x_bf16 = 0) or bf16 (1); operands are rounded to bf16 (RNE)
  * when staged, products accumulate in fp32, C is fp32 with row stride ldc.
  * epi: 0 store, 1 accumulate (C += ...), 2 store + column statistics
+ * (4, dgx_gemm_lds_bf16 only: as 2 but C is stored bf16)
  * (partials[dgx_gemm_stats_rows(M)][2][N] = per 128-row block sum, sum of
  * squares; feeds dgx_bn_finalize_f32), 3 split-K slabs: C is a dense
  * [splits][M][N] workspace (ldc ignored), summed by dgx_slab_reduce_f32.
