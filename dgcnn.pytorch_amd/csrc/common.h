@@ -26,3 +26,17 @@ __device__ __forceinline__ bool dgx_xcd_cloud_map(int block, int B, int tiles, i
     return b < B;
 }
 static inline int dgx_xcd_cloud_grid(int B, int tiles) { return 8 * ((B + 7) / 8) * tiles; }
+
+// (cloud, point part, channel slice) work items of the EdgeConv gather/scatter
+// kernels: every block of one cloud gets the same residue mod 8 (one XCD) and
+// consecutive dispatch slots, so the slices that read different 32-64 B pieces
+// of the same rows run together and the rows come from HBM once (that XCD's
+// L2 serves the rest). Slices vary fastest. Returns false for padding blocks.
+__device__ __forceinline__ bool dgx_xcd_slice_map(int block, int B, int parts, int slices, int& b, int& part,
+                                                  int& slice) {
+    int tile;
+    if (!dgx_xcd_cloud_map(block, B, parts * slices, b, tile)) return false;
+    part = tile / slices;
+    slice = tile - part * slices;
+    return true;
+}

@@ -25,6 +25,8 @@
 // compulsory M*Co*(bytes) instead of M*k*Co*(bytes).
 #include <math.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "common.h"
@@ -179,14 +181,16 @@ __device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float
 
 template <int CS, bool EVAL>
 __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
-    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int N, int k, int Co, int nparts,
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int B, int N, int k, int Co, int nparts,
     const float* __restrict__ sel_sign, const float* __restrict__ shift, float slope, float* __restrict__ ysel,
     uint8_t* __restrict__ arg, float* __restrict__ sumP, float* __restrict__ partials, float* __restrict__ out,
     int ldo) {
     constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V;
     extern __shared__ float lds[];  // [N][CS] slice of P | idx rows of a pass; then the stat reduction
-    const int b = blockIdx.x / nparts, part = blockIdx.x - b * nparts;
-    const int o0 = blockIdx.y * CS;
+    int b, part, slice;
+    if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
+    const int o0 = slice * CS;
+    const int prow = b * nparts + part;  // partial-stat row
     const int t = threadIdx.x;
     const int64_t base = (int64_t)b * N;
     const int per = (N + nparts - 1) / nparts;
@@ -340,8 +344,8 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
             r1 += red[(2 * uc) * EC_THREADS + w];
             r2 += red[(2 * uc + 1) * EC_THREADS + w];
         }
-        partials[(int64_t)blockIdx.x * 2 * Co + o0 + t] = r1;
-        partials[(int64_t)blockIdx.x * 2 * Co + Co + o0 + t] = r2;
+        partials[(int64_t)prow * 2 * Co + o0 + t] = r1;
+        partials[(int64_t)prow * 2 * Co + Co + o0 + t] = r2;
     }
 }
 
@@ -623,7 +627,7 @@ __global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(const int32_t
 template <int CS, bool OUT16>
 __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
-    const float* __restrict__ dzp, const float* __restrict__ sumP, int N, int k, int Co, int nparts,
+    const float* __restrict__ dzp, const float* __restrict__ sumP, int B, int N, int k, int Co, int nparts,
     const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
     void* __restrict__ dPQv) {
     // dPQ fp32, or bf16 when it only feeds the bf16 GEMMs (dX, dW)
@@ -635,8 +639,9 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
     float* ds = lds + N * CS;
     int* ebuf = reinterpret_cast<int*>(ds + N * CS);
     int* rps = ebuf + GB_ECAP;
-    const int b = blockIdx.x / nparts, part = blockIdx.x - b * nparts;
-    const int o0 = blockIdx.y * CS;
+    int b, part, slice;
+    if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
+    const int o0 = slice * CS;
     const int t = threadIdx.x;
     const int64_t base = (int64_t)b * N;
     const int per = (N + nparts - 1) / nparts;
@@ -779,6 +784,114 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
     }
 }
 
+// Wide form of the dP/dQ scatter (the slice holds CS <= 8 channels): one
+// point per thread, all CS channels of the slice per thread, so the per-edge
+// work (edge-id decode, addresses, 16-B LDS reads of Q_i and dz_i) is shared
+// by CS channels. In-edge lists and row pointers are read from HBM/L2 directly
+// (contiguous per point, consecutive points -> consecutive ranges).
+template <int CS, bool OUT16>
+__global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
+    const float* __restrict__ dzp, const float* __restrict__ sumP, int B, int N, int k, int Co, int nparts,
+    const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
+    void* __restrict__ dPQv) {
+    float* __restrict__ dPQ = static_cast<float*>(dPQv);
+    __bf16* __restrict__ dPQh = static_cast<__bf16*>(dPQv);
+    extern __shared__ float lds[];  // [N][CS] Q slice | [N][CS] packed dz slice
+    float* qs = lds;
+    float* ds = lds + N * CS;
+    int b, part, slice;
+    if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
+    const int o0 = slice * CS;
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)b * N;
+    const int per = (N + nparts - 1) / nparts;
+    const int n_beg = part * per, n_end = min(N, n_beg + per);
+    stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
+    stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+    float a[CS], k0[CS], k1[CS];
+#pragma unroll
+    for (int u = 0; u < CS; ++u) {
+        const int o = min(o0 + u, Co - 1);
+        a[u] = scale[o];
+        k0[u] = c0[o];
+        k1[u] = c1[o];
+    }
+    const bool full = o0 + CS <= Co;
+    const bool vec = full && (CS % 4) == 0 && (Co % 4) == 0 && (ldpq % 4) == 0;
+    const float kf = (float)k;
+    const int32_t ibase = (int32_t)base;
+    __syncthreads();
+    for (int n = n_beg + t; n < n_end; n += EC_THREADS) {
+        const int64_t j = base + n;
+        const int32_t beg = rowptr[j], end = rowptr[j + 1];
+        float pjv[CS], spv[CS];  // HBM reads issued before the edge loop hides their latency
+        if (vec) {
+            gld_vec<CS>(PQ + j * ldpq + o0, pjv);
+            gld_vec<CS>(sumP + j * Co + o0, spv);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CS; ++u) {
+                pjv[u] = o0 + u < Co ? PQ[j * ldpq + o0 + u] : 0.f;
+                spv[u] = o0 + u < Co ? sumP[j * Co + o0 + u] : 0.f;
+            }
+        }
+        float sq[CS], sd[CS];
+#pragma unroll
+        for (int u = 0; u < CS; ++u) { sq[u] = 0.f; sd[u] = 0.f; }
+        auto edge = [&](int32_t e) {
+            const int il = (e >> 6) - ibase;
+            const uint32_t slot = (uint32_t)(e & 63);
+            float q[CS], d[CS];
+            lds_vec<CS>(qs + il * CS, q);
+            lds_vec<CS>(ds + il * CS, d);
+#pragma unroll
+            for (int u = 0; u < CS; ++u) {
+                sq[u] += q[u];
+                sd[u] += (__float_as_uint(d[u]) & 63u) == slot ? unpack_dz(d[u]) : 0.f;
+            }
+        };
+        int32_t u0 = beg;
+        for (; u0 + 4 <= end; u0 += 4) {
+            const int4 e4 = make_int4(edges[u0], edges[u0 + 1], edges[u0 + 2], edges[u0 + 3]);
+            edge(e4.x);
+            edge(e4.y);
+            edge(e4.z);
+            edge(e4.w);
+        }
+        for (; u0 < end; ++u0) edge(edges[u0]);
+        const float deg = (float)(end - beg);
+        float qn[CS], dn[CS];
+        lds_vec<CS>(qs + n * CS, qn);
+        lds_vec<CS>(ds + n * CS, dn);
+        float dp[CS], dq[CS];
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
+            dq[u] = fmaf(a[u], unpack_dz(dn[u]), fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
+        }
+        if (OUT16 && vec) {
+            gst_bf16<CS>(dPQh + j * 2 * Co + o0, dp);
+            gst_bf16<CS>(dPQh + j * 2 * Co + Co + o0, dq);
+        } else if (vec) {
+            gst_vec<CS>(dPQ + j * 2 * Co + o0, dp);
+            gst_vec<CS>(dPQ + j * 2 * Co + Co + o0, dq);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CS; ++u) {
+                if (o0 + u >= Co) continue;
+                if (OUT16) {
+                    dPQh[j * 2 * Co + o0 + u] = (__bf16)dp[u];
+                    dPQh[j * 2 * Co + Co + o0 + u] = (__bf16)dq[u];
+                } else {
+                    dPQ[j * 2 * Co + o0 + u] = dp[u];
+                    dPQ[j * 2 * Co + Co + o0 + u] = dq[u];
+                }
+            }
+        }
+    }
+}
+
 inline int grid_for(int64_t total, int block) {
     int64_t g = (total + block - 1) / block;
     return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
@@ -801,13 +914,14 @@ inline int point_parts(int B, int slices, int N) {
 }
 
 template <bool EVAL>
-int launch_gather(int cs, dim3 grid, size_t lds, hipStream_t st, const float* PQ, int ldpq, const int32_t* idx, int N,
+int launch_gather(int cs, dim3 grid, size_t lds, hipStream_t st, const float* PQ, int ldpq, const int32_t* idx, int B,
+                  int N,
                   int k, int Co, int nparts, const float* sel, const float* shift, float slope, float* ysel,
                   uint8_t* arg, float* sumP, float* partials, float* out, int ldo) {
 #define DGX_GATHER_CASE(CSV)                                                                                      \
     case CSV:                                                                                                    \
-        hipLaunchKernelGGL((edge_gather_lds_kernel<CSV, EVAL>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, idx, N, \
-                           k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo);                \
+        hipLaunchKernelGGL((edge_gather_lds_kernel<CSV, EVAL>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, idx, B, \
+                           N, k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo);             \
         break;
     switch (cs) {
         DGX_GATHER_CASE(32)
@@ -856,7 +970,8 @@ int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx, int B
     const GatherGeom g = gather_geom(B, N, Co);
     if (nrows != B * g.parts) return DGX_EINVAL;
     if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
-    return launch_gather<false>(g.cs, dim3(B * g.parts, g.slices), g.lds, dgx_stream(stream), PQ, ldpq, idx, N, k, Co,
+    return launch_gather<false>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
+                                ldpq, idx, B, N, k, Co,
                                 g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials, nullptr, 0);
 }
 
@@ -866,7 +981,8 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, 
     if (B < 1 || N < 1 || k < 1 || Co < 1 || ldpq < 2 * Co || ldo < Co) return DGX_EINVAL;
     if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
     const GatherGeom g = gather_geom(B, N, Co);
-    return launch_gather<true>(g.cs, dim3(B * g.parts, g.slices), g.lds, dgx_stream(stream), PQ, ldpq, idx, N, k, Co,
+    return launch_gather<true>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
+                               ldpq, idx, B, N, k, Co,
                                g.parts, scale, shift, slope, nullptr, nullptr, nullptr, nullptr, out, ldo);
 }
 
@@ -943,18 +1059,40 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, c
     if ((size_t)2 * N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
     const int slices = (Co + cs - 1) / cs;
     const int parts = point_parts(B, slices, N);
-    const dim3 grid(B * parts, slices);
+    const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
     const size_t lds = (size_t)2 * N * cs * sizeof(float) + (GB_ECAP + EC_THREADS + 1) * sizeof(int);
     hipStream_t st = dgx_stream(stream);
 #define DGX_BWD_CASE(CSV)                                                                                    \
     case CSV:                                                                                               \
         if (out_bf16)                                                                                       \
             hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, true>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                               edges, dzp, sumP, N, k, Co, parts, scale, c0, c1, dPQ);                       \
+                               edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                    \
         else                                                                                                \
             hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, false>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                               edges, dzp, sumP, N, k, Co, parts, scale, c0, c1, dPQ);                       \
+                               edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                    \
         break;
+    static const bool narrow = getenv("DGX_EDGE_BWD_NARROW") != nullptr;  // A/B switch for profiling
+    if (cs <= 8 && !narrow) {
+        const size_t wl = (size_t)2 * N * cs * sizeof(float);
+#define DGX_WIDE_CASE(CSV)                                                                                    \
+    case CSV:                                                                                                \
+        if (out_bf16)                                                                                        \
+            hipLaunchKernelGGL((edge_bwd_wide_kernel<CSV, true>), grid, dim3(EC_THREADS), wl, st, PQ, ldpq, rowptr, \
+                               edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                     \
+        else                                                                                                 \
+            hipLaunchKernelGGL((edge_bwd_wide_kernel<CSV, false>), grid, dim3(EC_THREADS), wl, st, PQ, ldpq,      \
+                               rowptr, edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);             \
+        break;
+        switch (cs) {
+            DGX_WIDE_CASE(8)
+            DGX_WIDE_CASE(4)
+            DGX_WIDE_CASE(2)
+            DGX_WIDE_CASE(1)
+            default: return DGX_EUNSUPPORTED;
+        }
+#undef DGX_WIDE_CASE
+        return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+    }
     switch (cs) {
         DGX_BWD_CASE(32)
         DGX_BWD_CASE(16)
