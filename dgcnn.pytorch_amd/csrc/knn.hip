@@ -10,9 +10,9 @@
 //     in registers, 4 lanes per query, merged through LDS at the end.
 //
 // Workgroup = 4 waves x 16 queries = 64 queries of one cloud. Candidates stream
-// through a double-buffered LDS chunk of 64 points laid out [j/16][c][j%16] so
-// the MFMA A operand read (lane l -> c = 4t + l/16, j = l%16) is a contiguous,
-// conflict-free 256 B per wave.
+// through an LDS chunk laid out [j/16][c][j%16] (padded, see knn_tile_stride)
+// so the MFMA A operand read (lane l -> c = 4t + l/16, j = l%16) and the chunk
+// stores are bank-conflict-free.
 #include <math.h>
 #include <stdlib.h>
 
@@ -148,11 +148,22 @@ struct KnnList {
     static constexpr int RPL = (KB + 3) / 4;   // output ranks per lane
 };
 
+// Candidate tile image: 16 candidates x CP channels per tile, channel rows of
+// 17 floats (16 + 1 pad) and tiles KT_SKEW floats apart beyond CP*17: the
+// channel-fastest stores of a point-major chunk and the candidate-fastest
+// stores of a channel-major one both hit 64 distinct banks, and the MFMA
+// A-operand read (lane -> channel 4t + lane/16, candidate lane%16) is
+// conflict-free (odd row stride).
+constexpr int KT_ROW = 17;
+constexpr int KT_SKEW = 16;
+template <int CP>
+constexpr int knn_tile_stride() { return CP * KT_ROW + KT_SKEW; }
+
 template <int NSTEP>
 constexpr int knn_smem_floats() {
     constexpr int CP = NSTEP * 4;
     constexpr int JC = KnnGeom<CP>::JC;
-    return JC * CP + JC + KQ_WAVES * 2 * KQ_QCAP * 64;  // tile | xx | per-wave FIFOs
+    return (JC / 16) * knn_tile_stride<CP>() + JC + KQ_WAVES * 2 * KQ_QCAP * 64;  // tile | xx | per-wave FIFOs
 }
 
 // Canonical order: value descending, then index ascending.
@@ -175,7 +186,8 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
     constexpr int RPL = KnnList<KB>::RPL;
     __shared__ __attribute__((aligned(16))) float smem[knn_smem_floats<NSTEP>()];
     float* tile = smem;                 // [JC/16][CP][16]
-    float* xxs = smem + JC * CP;        // [JC]
+    constexpr int TS = knn_tile_stride<CP>();
+    float* xxs = smem + (JC / 16) * TS;  // [JC]
     float* qbase = xxs + JC;            // per wave: [KQ_QCAP][64] float2 (value, index)
 
     int b, qb;
@@ -225,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
             int jj, c;
             if (CMAJOR) { jj = e % JC; c = e / JC; }
             else { c = e % CP; jj = e / CP; }
-            tile[(jj >> 4) * (CP * 16) + c * 16 + (jj & 15)] = pf[u];
+            tile[(jj >> 4) * TS + c * KT_ROW + (jj & 15)] = pf[u];
         }
 #pragma unroll
         for (int u = 0; u < XPF; ++u) {
@@ -289,11 +301,11 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
 #pragma unroll 1
         for (int s = 0; s < (jend + 15) / 16; s += 2) {
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-            const float* __restrict__ ts = tile + s * (CP * 16);
+            const float* __restrict__ ts = tile + s * TS + (lane >> 4) * KT_ROW + (lane & 15);
 #pragma unroll
             for (int t = 0; t < NSTEP; ++t) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ts[t * 64 + lane], bq[t], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ts[CP * 16 + t * 64 + lane], bq[t], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ts[t * 4 * KT_ROW], bq[t], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ts[TS + t * 4 * KT_ROW], bq[t], acc1, 0, 0, 0);
             }
             // lane holds candidates j = jb + r (r = 0..3) and jb + 16 + r of query q
             const int jl = s * 16 + 4 * g;

@@ -14,7 +14,10 @@ dev = torch.device("cuda:0")
 x3 = torch.from_numpy(synth.cube_clouds(32, 1024, 0)).to(dev).permute(0, 2, 1)
 f64 = torch.from_numpy(synth.relu_normal(3, (32, 64, 1024))).to(dev)
 f128 = torch.from_numpy(synth.relu_normal(4, (32, 128, 1024))).to(dev)
-for name, x in (("C3", x3), ("C64", f64), ("C128", f128)):
+# point-major (B,N,C) memory, as the engine's concat buffer feeds layers 2-4
+p64 = f64.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+p128 = f128.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+for name, x in (("C3", x3), ("C64", f64), ("C128", f128), ("C64pm", p64), ("C128pm", p128)):
     for _ in range(3):
         knn_raw(x, 20, out_dtype=torch.int32)
     torch.cuda.synchronize()
