@@ -30,6 +30,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "dgcnn.pytorch_amd"))
 
+from dgx import gemm as dgx_gemm  # noqa: E402
 from dgx import ops as dgx_ops  # noqa: E402
 from dgx import precision as dgx_prec  # noqa: E402
 from dgx import synth  # noqa: E402
@@ -38,6 +39,7 @@ from models.dgcnn import DGCNN  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 vector = f32 MFMA peak
 PEAK_HBM_GBS = 8000.0
+PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 METRIC = "point-clouds/sec + EdgeConv fwd+bwd ms at B=32 N=1024 k=20, 1/2/4/8 MI355X"
 
@@ -58,7 +60,18 @@ def parse():
                    help="GEMM operand precision (BASELINE cfg2 is bf16; fp32 is the parity mode)")
     p.add_argument("--no-fp32-leg", action="store_true", help="skip the extra fp32-mode timing")
     p.add_argument("--no-edgeconv-leg", action="store_true", help="skip the EdgeConv-only fwd+bwd timing")
+    p.add_argument("--sync-bn", action="store_true",
+                   help="N>1: SyncBatchNorm (global-batch BN statistics, main_partseg_dist.py:189) instead of "
+                        "per-replica BN (main_cls.py:62 DataParallel semantics)")
     return p.parse_args()
+
+
+def reduce_elapsed(elapsed, world, dev):
+    """The job's time for the timed region: the slowest rank's (max over ranks)."""
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def sync_all(world):
@@ -203,8 +216,13 @@ def main():
     model = DGCNN(types.SimpleNamespace(emb_dim=args.emb, k=args.k)).to(dev).train()
     net = model
     if world > 1:
+        if args.sync_bn:
+            model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
-    opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    try:  # one fused kernel for the whole parameter list (same math as the foreach form)
+        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
+    except (RuntimeError, TypeError, ValueError):
+        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     pts = torch.from_numpy(synth.cube_clouds(args.batch, args.points, seed=rank)).to(dev)
     x = pts.permute(0, 2, 1)  # (B,3,N) view, as main_cls.py:91 feeds the model
 
@@ -216,14 +234,19 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timing = []
-    dgx_ops.set_knn_timing(timing)
+    # headline: the timed region runs uninstrumented
     elapsed = timed_region(step, args.steps, world)
+    # roofline / MFMA: the same K steps again with HIP events around every kNN
+    # selection and GEMM launch (on their launch stream); events perturb the
+    # step slightly, so this region is reported separately
+    timing, gtiming = [], []
+    dgx_ops.set_knn_timing(timing)
+    dgx_gemm.set_timing(gtiming)
+    elapsed_inst = timed_region(step, args.steps, world)
     dgx_ops.set_knn_timing(None)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    dgx_gemm.set_timing(None)
+    elapsed = reduce_elapsed(elapsed, world, dev)
+    elapsed_inst = reduce_elapsed(elapsed_inst, world, dev)
 
     knn_ms = [e0.elapsed_time(e1) for (e0, e1, _, _) in timing]
     knn_flops = [f for (_, _, f, _) in timing]
@@ -236,6 +259,17 @@ def main():
         per_layer.setdefault(f"C{shape[1]}", []).append(ms)
     per_layer = {c: round(sum(v) / len(v), 4) for c, v in per_layer.items()}
 
+    g_ms = sum(e0.elapsed_time(e1) for (e0, e1, _, _) in gtiming)
+    g_flops = sum(f for (_, _, f, _) in gtiming)
+    by_tag = {}
+    for (e0, e1, f, tg) in gtiming:
+        if tg is not None:
+            ms, fl, n = by_tag.get(tg, (0.0, 0.0, 0))
+            by_tag[tg] = (ms + e0.elapsed_time(e1), fl + f, n + 1)
+    peak_g = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_FP32_TFLOPS
+    conv5 = {tg: {"avg_launch_ms": round(ms / n, 4), "flops_per_launch": fl / n,
+                  "achieved": round(fl / (ms * 1e-3) / 1e12, 1), "frac": round(fl / (ms * 1e-3) / 1e12 / peak_g, 4)}
+             for tg, (ms, fl, n) in by_tag.items() if ms > 0}
     result = {
         "metric": METRIC,
         "value": round(args.batch * world * args.steps / elapsed, 2),
@@ -252,24 +286,32 @@ def main():
         "config": {"workload": "DGCNN(emb=1024,k=20) train step fwd+bwd+SGD, cfg2",
                    "model": "DGCNN", "global_batch": args.batch * world, "points": args.points,
                    "seq_len": args.points, "k": args.k, "emb_dim": args.emb,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}" + ("+syncbn" if (args.sync_bn and world > 1) else "")},
         "roofline": {"kernel": "knn_kernel (fused fp32 Gram on MFMA + top-k)", "bound": "mfma",
                      "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                      "traffic": latest_pmc_traffic(),
                      "avg_launch_ms": round(avg_ms, 4), "algorithmic_flops_per_launch": avg_flops,
-                     "launches_timed": len(knn_ms), "knn_ms_by_layer": per_layer},
+                     "launches_timed": len(knn_ms), "knn_ms_by_layer": per_layer,
+                     "timed_region": "second K-step region with HIP events (ms_per_step %.3f)"
+                                     % (elapsed_inst / args.steps * 1e3)},
+        # the Conv(1x1) GEMMs of the chain and conv5 (fwd + dX + dW) on the bf16 MFMA.
+        # Every GEMM launch is bracketed by HIP events (~20 us of marker overhead each
+        # on this stack), so the all-GEMM sum is an upper bound of their time; the
+        # three conv5 GEMMs (34 GFLOP each) are the per-kernel MFMA utilisation.
+        "mfma_gemm": {"kernels": "gemm_lds_kernel / gemm_bf16_kernel (csrc/gemm.hip)",
+                      "flops_per_step": g_flops / max(1, args.steps),
+                      "event_bracketed_ms_per_step": round(g_ms / max(1, args.steps), 4),
+                      "peak": peak_g, "unit": "TFLOP/s", "conv5": conv5},
     }
     if args.precision != "fp32" and not args.no_fp32_leg:
         dgx_prec.set("fp32")  # same model, parity-mode GEMMs
         for _ in range(2):
             step()
         el32 = timed_region(step, args.steps, world)
-        t32 = torch.tensor([el32], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(t32, op=dist.ReduceOp.MAX)
-        result["fp32_mode"] = {"ms_per_step": round(float(t32.item()) / args.steps * 1e3, 3),
-                               "value": round(args.batch * world * args.steps / float(t32.item()), 2)}
+        el32 = reduce_elapsed(el32, world, dev)
+        result["fp32_mode"] = {"ms_per_step": round(el32 / args.steps * 1e3, 3),
+                               "value": round(args.batch * world * args.steps / el32, 2)}
         dgx_prec.set(args.precision)
     if rank == 0 and world == 1:
         if not args.no_edgeconv_leg:

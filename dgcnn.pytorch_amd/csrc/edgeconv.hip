@@ -356,9 +356,11 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ rvar, double momentum, double eps,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float* __restrict__ mean_out,
-                                                          float* __restrict__ invstd_out) {
+                                                          float* __restrict__ invstd_out,
+                                                          int64_t* __restrict__ nbt) {
     __shared__ double r1[256], r2[256];
     const int o = blockIdx.x, t = threadIdx.x;
+    if (nbt && o == 0 && t == 0) *nbt += 1;  // BatchNorm.num_batches_tracked, no extra launch
     double s1 = 0.0, s2 = 0.0;
     for (int i = t; i < nrows; i += 256) {
         s1 += (double)partials[(int64_t)i * 2 * Co + o];
@@ -988,10 +990,12 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, 
 
 int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, double momentum, double eps,
-                        float* scale, float* shift, float* mean, float* invstd, void* stream) {
+                        float* scale, float* shift, float* mean, float* invstd, int64_t* num_batches_tracked,
+                        void* stream) {
     if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co, count,
-                       gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd);
+                       gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
+                       num_batches_tracked);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

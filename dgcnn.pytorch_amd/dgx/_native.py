@@ -36,7 +36,7 @@ _SIGS = {
     "dgx_edge_partials_rows": [_i32, _i32, _i32],
     "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
-    "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp],
+    "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
     "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp],
     "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],

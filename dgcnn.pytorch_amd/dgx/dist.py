@@ -1,0 +1,40 @@
+"""Cross-rank BatchNorm statistics for the engine's fused BN (SyncBatchNorm).
+
+Reference: main_partseg_dist.py:189 wraps the model with
+``nn.SyncBatchNorm.convert_sync_batchnorm`` before DDP, so every BN layer of
+the EdgeConv chain and conv5 normalises with the statistics of the GLOBAL batch
+(torch/nn/modules/_functions.py: forward all-gathers per-rank mean/invstd/count,
+backward all-reduces sum(dy) and sum(dy * xmu)).
+
+The engine keeps those exact semantics with one collective per BN layer and
+direction: the kernels already produce per-block partial sums, the host sums
+them to one (2, C) vector, and ``allreduce_sums`` adds the vectors of all ranks
+(plus the element count) in a single all-reduce over RCCL (or gloo). Parameter
+gradients stay rank-local (DDP averages them), exactly as SyncBatchNorm does.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+
+def sync_group(bn, training):
+    """(True, group) when ``bn`` is a SyncBatchNorm that must synchronise now."""
+    if not (training and isinstance(bn, nn.SyncBatchNorm)):
+        return False, None
+    if not (dist.is_available() and dist.is_initialized()):
+        return False, None
+    group = bn.process_group if bn.process_group is not None else dist.group.WORLD
+    if dist.get_world_size(group) < 2:
+        return False, None
+    return True, group
+
+
+def allreduce_sums(sums, count, group):
+    """sums: (2, C) fp32 local column sums; count: local element count.
+    Returns (global sums (2, C), global count) with ONE all-reduce."""
+    C = sums.shape[-1]
+    buf = torch.empty(2 * C + 1, dtype=torch.float64, device=sums.device)
+    buf[:2 * C] = sums.reshape(-1).double()
+    buf[2 * C] = float(count)
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return buf[:2 * C].view(2, C).float(), float(buf[2 * C].item())

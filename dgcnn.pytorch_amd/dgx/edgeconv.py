@@ -20,6 +20,7 @@ Backward per block (reverse order):
 import torch
 
 from . import _native as nat
+from . import dist as dist_
 from . import gemm as G
 from . import precision as prec
 from .ops import knn_raw, reduction_order
@@ -32,15 +33,16 @@ _debug = None
 
 
 def _bn_factor(bn):
-    """Exponential-average factor nn.BatchNorm uses this step (and bump the counter)."""
+    """(exponential-average factor nn.BatchNorm uses this step, num_batches_tracked
+    tensor for the finalize kernel to increment or None). With a momentum the
+    counter is bumped on device by dgx_bn_finalize_f32 (no extra launch); the
+    cumulative-average form (momentum None) needs the count on the host."""
     if bn.momentum is None:
         if bn.num_batches_tracked is not None:
             bn.num_batches_tracked.add_(1)
-            return 1.0 / float(bn.num_batches_tracked.item())
-        return 0.0
-    if bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
-    return float(bn.momentum)
+            return 1.0 / float(bn.num_batches_tracked.item()), None
+        return 0.0, None
+    return float(bn.momentum), bn.num_batches_tracked
 
 
 class _Layer:
@@ -118,18 +120,24 @@ class _EdgeConvStack(torch.autograd.Function):
                         nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(gamma), nat.ptr(ysel),
                         nat.ptr(arg), nat.ptr(sumP), nat.ptr(partials), prow, stream), "edge gather")
                     update = training and bn.running_mean is not None
-                    factor = _bn_factor(bn) if update else 0.0
+                    factor, nbt = _bn_factor(bn) if update else (0.0, None)
+                    fin, frows, fcount = partials, prow, count
+                    sync, group = dist_.sync_group(bn, training)
+                    if sync:  # SyncBatchNorm: statistics of the global batch, one all-reduce
+                        tot, fcount = dist_.allreduce_sums(partials.sum(0), count, group)
+                        fin, frows = tot.unsqueeze(0).contiguous(), 1
                     nat.check(L.dgx_bn_finalize_f32(
-                        nat.ptr(partials), prow, co, count, nat.ptr(gamma), nat.ptr(beta),
+                        nat.ptr(fin), frows, co, fcount, nat.ptr(gamma), nat.ptr(beta),
                         nat.ptr(bn.running_mean) if update else None,
                         nat.ptr(bn.running_var) if update else None, factor, float(bn.eps),
-                        nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), stream), "bn finalize")
+                        nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), nat.ptr(nbt), stream),
+                        "bn finalize")
                     out16 = xcat16[:, off:off + co] if bf16 else None
                     nat.check(L.dgx_bn_lrelu_apply_f32(nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift),
                                                        float(ly.slope), nat.ptr(out), total, nat.ptr(out16), stream),
                               "bn apply")
                     have16 = bf16
-                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep))
+                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group if sync else None))
                     if _debug is not None:
                         zpos = (scale * ysel + shift) > 0
                         _debug[("fwd", li)] = (idx.clone(), arg.clone(), zpos)
@@ -187,7 +195,7 @@ class _EdgeConvStack(torch.autograd.Function):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
             w = params[3 * li]
-            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep = ctx.layer_state[li]
+            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group = ctx.layer_state[li]
             off = sum(widths[:li])
             prev = off - widths[li - 1] if li > 0 else None
             X = x_pm if li == 0 else xcat[:, prev: prev + cin]
@@ -209,9 +217,19 @@ class _EdgeConvStack(torch.autograd.Function):
                     nat.ptr(dY), ldy, nat.ptr(ysel), nat.ptr(arg), M, co, nat.ptr(scale), nat.ptr(shift),
                     nat.ptr(mean), nat.ptr(invstd), float(ly.slope), nat.ptr(dz), nat.ptr(partials), nblk, stream),
                     "edge bwd dz")
-                nat.check(L.dgx_bn_bwd_finalize_f32(
-                    nat.ptr(partials), nblk, co, count, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
-                    nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
+                if group is None:
+                    nat.check(L.dgx_bn_bwd_finalize_f32(
+                        nat.ptr(partials), nblk, co, count, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
+                        nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
+                else:  # SyncBatchNorm: input gradient from global sums, gamma/beta grads rank-local
+                    loc = partials.sum(0)
+                    tot, gcount = dist_.allreduce_sums(loc, count, group)
+                    tot = tot.unsqueeze(0).contiguous()
+                    nat.check(L.dgx_bn_bwd_finalize_f32(
+                        nat.ptr(tot), 1, co, gcount, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
+                        None, None, nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
+                    dbeta.copy_(loc[0])
+                    dgamma.copy_(loc[1])
                 nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges), stream),
                           "reverse graph")
                 nat.check(L.dgx_edge_bwd_scatter_f32(

@@ -12,6 +12,52 @@ from . import _native as nat
 
 EPI_STORE, EPI_ACCUM, EPI_STATS, EPI_SLAB, EPI_STATS16 = 0, 1, 2, 3, 4
 
+# Optional instrumentation (bench.py): when a list, every GEMM launch appends
+# (start_event, end_event, flops) recorded on the launch stream.
+_timing = None
+
+
+def set_timing(lst):
+    global _timing
+    _timing = lst
+
+
+class _Timed:
+    def __init__(self, flops):
+        self.flops = flops
+
+    def __enter__(self):
+        if _timing is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _timing is not None:
+            self.e1.record()
+            _timing.append((self.e0, self.e1, self.flops, _tag))
+        return False
+
+
+_tag = None
+
+
+class tag:
+    """Label the GEMM launches issued inside (bench.py's per-class MFMA report)."""
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        global _tag
+        self.prev, _tag = _tag, self.name
+        return self
+
+    def __exit__(self, *exc):
+        global _tag
+        _tag = self.prev
+        return False
+
 
 def _operand(t, ic):
     """(pointer, is_bf16, ld) of a 2-D view whose inner dim is unit-stride."""
@@ -33,7 +79,7 @@ def gemm(a, a_ic, b, b_ic, M, N, K, epi, out, partials=None, splits=1):
         if out.dim() != 2 or out.stride(1) != 1 or out.dtype != torch.float32:
             raise RuntimeError("dgx gemm: output must be a row-major fp32 2-D view")
         ldc = out.stride(0)
-    with torch.cuda.device(out.device):
+    with torch.cuda.device(out.device), _Timed(2.0 * M * N * K):
         nat.check(nat.lib().dgx_gemm_bf16(ap, abf, aic, lda, bp, bbf, bic, ldb, M, N, K, epi, splits,
                                           nat.ptr(out), ldc, nat.ptr(partials), nat.stream_of(out)), "gemm bf16")
     return out
@@ -108,7 +154,7 @@ def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None, out_
         raise RuntimeError("dgx gemm: a bf16 product is only stored together with its statistics")
     epi = (EPI_STATS16 if out_bf16 else EPI_STATS) if stats else (
         EPI_ACCUM if (accumulate or addend is not None) else EPI_STORE)
-    with torch.cuda.device(out.device):
+    with torch.cuda.device(out.device), _Timed(2.0 * M * N * K):
         nat.check(nat.lib().dgx_gemm_lds_bf16(
             nat.ptr(x16), _bf16_2d(x16), nat.ptr(w16), _bf16_2d(w16), 0, M, N, K, epi, 1, nat.ptr(out),
             out.stride(0), nat.ptr(part), nat.ptr(addend), addend.stride(0) if addend is not None else 0,
@@ -129,8 +175,9 @@ def lds_atb(a16, b16, out, split_rows=None):
     slab = torch.empty((used, M, N), dtype=torch.float32, device=a16.device)
     with torch.cuda.device(out.device):
         st = nat.stream_of(out)
-        nat.check(L.dgx_gemm_lds_bf16(nat.ptr(a16), _bf16_2d(a16), nat.ptr(b16), _bf16_2d(b16), 1, M, N, R,
-                                      EPI_SLAB, S, nat.ptr(slab), N, None, None, 0, st), "gemm lds tn")
+        with _Timed(2.0 * M * N * R):
+            nat.check(L.dgx_gemm_lds_bf16(nat.ptr(a16), _bf16_2d(a16), nat.ptr(b16), _bf16_2d(b16), 1, M, N, R,
+                                          EPI_SLAB, S, nat.ptr(slab), N, None, None, 0, st), "gemm lds tn")
         split = M if split_rows is None else split_rows
         nat.check(L.dgx_slab_reduce_f32(nat.ptr(slab), used, M, N, split, nat.ptr(out), out.stride(0), st),
                   "slab reduce")

@@ -12,6 +12,7 @@ cumulative average).
 import torch
 
 from . import _native as nat
+from . import dist as dist_
 from . import gemm as G
 from . import precision as prec
 from .edgeconv import _bn_factor
@@ -38,7 +39,8 @@ class _PointConvBNLReLU(torch.autograd.Function):
                 # Z is stored bf16 (as autocast stores a conv output), stats from fp32 sums
                 Xop = X16
                 wprep = G.prep_weight(weight, Co, K, False)
-                Z, gemm_part = G.lds_xwt(X16, wprep[0], stats=True, out_bf16=True)
+                with G.tag("conv5_fwd"):
+                    Z, gemm_part = G.lds_xwt(X16, wprep[0], stats=True, out_bf16=True)
                 z16 = True
             else:
                 res = G.mm_xwt(X, W, stats=use_batch)
@@ -50,6 +52,7 @@ class _PointConvBNLReLU(torch.autograd.Function):
         mean = torch.empty_like(scale)
         invstd = torch.empty_like(scale)
         out = torch.empty((B, Co, N), dtype=torch.float32, device=dev)
+        sync, group = False, None
         with torch.cuda.device(dev):
             if use_batch:
                 if gemm_part is not None:
@@ -60,12 +63,17 @@ class _PointConvBNLReLU(torch.autograd.Function):
                     nat.check(L.dgx_colstats_f32(nat.ptr(Z), Co, M, Co, nat.ptr(partials), rows, stream),
                               "colstats")
                 update = training and bn.running_mean is not None
-                factor = _bn_factor(bn) if update else 0.0
+                factor, nbt = _bn_factor(bn) if update else (0.0, None)
+                fcount = float(M)
+                sync, group = dist_.sync_group(bn, training)
+                if sync:  # SyncBatchNorm: statistics of the global batch, one all-reduce
+                    tot, fcount = dist_.allreduce_sums(partials.sum(0), fcount, group)
+                    partials, rows = tot.unsqueeze(0).contiguous(), 1
                 nat.check(L.dgx_bn_finalize_f32(
-                    nat.ptr(partials), rows, Co, float(M), nat.ptr(gamma), nat.ptr(beta),
+                    nat.ptr(partials), rows, Co, fcount, nat.ptr(gamma), nat.ptr(beta),
                     nat.ptr(bn.running_mean) if update else None, nat.ptr(bn.running_var) if update else None,
-                    factor, float(bn.eps), nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), stream),
-                    "bn finalize")
+                    factor, float(bn.eps), nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd),
+                    nat.ptr(nbt), stream), "bn finalize")
             else:
                 nat.check(L.dgx_bn_eval_affine_f32(
                     Co, nat.ptr(gamma), nat.ptr(beta), nat.ptr(bn.running_mean), nat.ptr(bn.running_var),
@@ -80,6 +88,7 @@ class _PointConvBNLReLU(torch.autograd.Function):
                 nat.check(L.dgx_pointconv_apply_f32(nat.ptr(Z), Co, B, N, Co, nat.ptr(scale), nat.ptr(shift),
                                                     float(slope), nat.ptr(out), stream), "pointconv apply")
         ctx.meta = (B, N, float(slope), use_batch, bf16)
+        ctx.group = group if (use_batch and sync) else None
         ctx.wprep = wprep
         ctx.save_for_backward(Xop, W, Z, scale, shift, mean, invstd)
         return out
@@ -111,7 +120,16 @@ class _PointConvBNLReLU(torch.autograd.Function):
                 nat.check(L.dgx_pointconv_bwd_f32(nat.ptr(dout), nat.ptr(Z), Co, B, N, Co, nat.ptr(scale),
                                                   nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), slope, nat.ptr(dz),
                                                   nat.ptr(partials), stream), "pointconv bwd")
-            if use_batch:
+            if use_batch and ctx.group is not None:  # SyncBatchNorm (see dgx.dist)
+                loc = partials.sum(0)
+                tot, gcount = dist_.allreduce_sums(loc, float(M), ctx.group)
+                tot = tot.unsqueeze(0).contiguous()
+                nat.check(L.dgx_bn_bwd_finalize_f32(nat.ptr(tot), 1, Co, gcount, nat.ptr(scale), nat.ptr(mean),
+                                                    nat.ptr(invstd), None, None, nat.ptr(c0), nat.ptr(c1), 0,
+                                                    stream), "bn bwd finalize")
+                dbeta.copy_(loc[0])
+                dgamma.copy_(loc[1])
+            elif use_batch:
                 nat.check(L.dgx_bn_bwd_finalize_f32(nat.ptr(partials), rows, Co, float(M), nat.ptr(scale),
                                                     nat.ptr(mean), nat.ptr(invstd), nat.ptr(dgamma), nat.ptr(dbeta),
                                                     nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
@@ -130,8 +148,10 @@ class _PointConvBNLReLU(torch.autograd.Function):
         if bf16:  # bf16 MFMA: dW = dZ^T X (split-K, deterministic), dX = dZ W
             dW = torch.empty((Co, Xop.shape[1]), dtype=torch.float32, device=dev)
             if ctx.wprep is not None:
-                G.lds_atb(dZ, Xop, dW)
-                dX = G.lds_xwt(dZ, ctx.wprep[1])
+                with G.tag("conv5_dW"):
+                    G.lds_atb(dZ, Xop, dW)
+                with G.tag("conv5_dX"):
+                    dX = G.lds_xwt(dZ, ctx.wprep[1])
             else:
                 G.mm_atb(dZ, Xop, dW)
                 dX = G.mm_xw(dZ, W)

@@ -107,7 +107,7 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         float* running_mean, float* running_var,
                         double momentum, double eps,
                         float* scale, float* shift, float* mean, float* invstd,
-                        void* stream);
+                        int64_t* num_batches_tracked, void* stream);
 int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
                            const float* shift, float slope, float* out, int ldo,
                            void* out_bf16, void* stream);

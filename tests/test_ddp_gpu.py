@@ -1,0 +1,82 @@
+"""Multi-rank path on one GPU: two DDP ranks (gloo, both on
+cuda:0) run the engine's DGCNN on their halves of a batch.
+
+* syncbn: the model is converted with nn.SyncBatchNorm.convert_sync_batchnorm
+  (reference main_partseg_dist.py:189). The engine then normalises with the
+  statistics of the global batch, so each rank's output must equal the
+  corresponding half of a single-process full-batch run, the running stats must
+  match, and the DDP-averaged gradients x world = the full-batch gradients.
+* plain: per-replica BN (nn.DataParallel semantics, main_cls.py:62): each rank
+  equals a single-process run on its own shard; DDP grads = mean of the shards'.
+"""
+import os
+import subprocess
+import sys
+import types
+
+import pytest
+import torch
+
+from conftest import REPO, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_ranks(tmp_path, mode, precision="fp32"):
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000))
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "_ddp_worker.py"), str(tmp_path),
+                                       mode, precision], env=e))
+    for p in procs:
+        assert p.wait(timeout=180) == 0
+    return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+
+
+def _single(cuda, shards, precision="fp32"):
+    from dgx import precision as prec
+    from dgx import synth
+    from models.dgcnn import DGCNN
+    torch.manual_seed(0)
+    model = DGCNN(types.SimpleNamespace(emb_dim=64, k=10)).to(cuda).train()
+    pts = synth.cube_clouds(4, 256, 5)
+    g = torch.from_numpy(synth.uniform(6, (4, 64, 256)) - 0.5)
+    outs = []
+    prec.set(precision)
+    try:
+        for sl in shards:
+            model.zero_grad(set_to_none=True)
+            x = torch.from_numpy(pts[sl]).to(cuda).permute(0, 2, 1)
+            y = model(x)
+            (y * g[sl].to(cuda)).sum().backward()
+            outs.append({"y": y.detach().cpu(),
+                         "grads": {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()},
+                         "running": {n: b.detach().cpu().clone() for n, b in model.named_buffers()}})
+    finally:
+        prec.set("fp32")
+    return outs
+
+
+def test_ddp_syncbn_matches_full_batch(cuda, tmp_path):
+    ranks = _run_ranks(tmp_path, "syncbn")
+    full = _single(cuda, [slice(0, 4)])[0]
+    for r in range(2):
+        assert rel_err(ranks[r]["y"], full["y"][2 * r:2 * r + 2]) < 1e-4
+    for n, gfull in full["grads"].items():
+        # DDP averages the two ranks' gradients; the full-batch loss is their sum
+        assert rel_err(ranks[0]["grads"][n] * 2, gfull) < 1e-3, n
+        assert torch.equal(ranks[0]["grads"][n], ranks[1]["grads"][n]), n
+    for n, b in full["running"].items():
+        if b.is_floating_point():
+            assert rel_err(ranks[0]["running"][n], b) < 1e-4, n
+
+
+def test_ddp_plain_bn_is_per_replica(cuda, tmp_path):
+    ranks = _run_ranks(tmp_path, "plain")
+    shards = _single(cuda, [slice(0, 2), slice(2, 4)])
+    for r in range(2):
+        assert rel_err(ranks[r]["y"], shards[r]["y"]) < 1e-5
+    for n in shards[0]["grads"]:
+        mean = (shards[0]["grads"][n] + shards[1]["grads"][n]) / 2
+        assert rel_err(ranks[0]["grads"][n], mean) < 1e-4, n
