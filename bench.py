@@ -49,9 +49,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=32, help="clouds per GPU")
-    p.add_argument("--points", type=int, default=1024)
-    p.add_argument("--k", type=int, default=20)
+    p.add_argument("--config", choices=["cfg2", "cfg3", "cfg5"], default="cfg2",
+                   help="BASELINE.json configs: cfg2 N1024 k20 B32 (headline), cfg3 N2048 k40 B32, "
+                        "cfg5 N4096 k20 B24 (S3DIS block size; DGCNN on xyz)")
+    p.add_argument("--batch", type=int, default=None, help="clouds per GPU (default: the config's)")
+    p.add_argument("--points", type=int, default=None)
+    p.add_argument("--k", type=int, default=None)
     p.add_argument("--emb", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-eager-baseline", action="store_true")
@@ -63,7 +66,28 @@ def parse():
     p.add_argument("--sync-bn", action="store_true",
                    help="N>1: SyncBatchNorm (global-batch BN statistics, main_partseg_dist.py:189) instead of "
                         "per-replica BN (main_cls.py:62 DataParallel semantics)")
-    return p.parse_args()
+    a = p.parse_args()
+    preset = {"cfg2": (32, 1024, 20), "cfg3": (32, 2048, 40), "cfg5": (24, 4096, 20)}[a.config]
+    a.batch = a.batch or preset[0]
+    a.points = a.points or preset[1]
+    a.k = a.k or preset[2]
+    return a
+
+
+_GRADS = {}
+
+
+def upstream_grad(shape, dev):
+    """The loss head's gradient w.r.t. DGCNN's (B, emb, N) output: a fixed
+    random tensor, made once outside every timed region. The reference DGCNN
+    is an embedding net with no loss of its own (models/dgcnn.py:80-103); all
+    three legs (engine, eager PyTorch, CPU) back-propagate the same kind of
+    dense upstream gradient."""
+    key = (tuple(shape), str(dev))
+    if key not in _GRADS:
+        g = torch.Generator().manual_seed(1234)
+        _GRADS[key] = (torch.rand(tuple(shape), generator=g) - 0.5).to(dev)
+    return _GRADS[key]
 
 
 def reduce_elapsed(elapsed, world, dev):
@@ -145,7 +169,7 @@ def eager_reference_step_ms(x, k, emb, reps=5):
             h = m(gf(h)).max(dim=-1, keepdim=False)[0]
             feats.append(h)
         y = c5(torch.cat(feats, dim=1).unsqueeze(-1)).view(x.shape[0], -1, x.shape[2])
-        y.sum().backward()
+        y.backward(upstream_grad(y.shape, dev))
     step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -174,7 +198,7 @@ def cpu_baseline(args):
 
     def step():
         y, _ = R.dgcnn(x, args.k, params, training=True)
-        y.sum().backward()
+        y.backward(upstream_grad(y.shape, torch.device("cpu")))
     step()
     times = []
     for _ in range(3):
@@ -226,10 +250,12 @@ def main():
     pts = torch.from_numpy(synth.cube_clouds(args.batch, args.points, seed=rank)).to(dev)
     x = pts.permute(0, 2, 1)  # (B,3,N) view, as main_cls.py:91 feeds the model
 
+    gy = upstream_grad((args.batch, args.emb, args.points), dev)
+
     def step():
         opt.zero_grad(set_to_none=True)
         y = net(x)
-        y.sum().backward()
+        y.backward(gy)
         opt.step()
 
     for _ in range(args.warmup):
@@ -282,8 +308,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic (splitmix64 uniform-cube clouds, random-init weights)",
-        "config": {"workload": "DGCNN(emb=1024,k=20) train step fwd+bwd+SGD, cfg2",
+        "data": "synthetic (splitmix64 uniform-cube clouds, random-init weights, fixed random upstream gradient)",
+        "config": {"workload": f"DGCNN(emb={args.emb},k={args.k}) train step fwd+bwd+SGD, {args.config}",
                    "model": "DGCNN", "global_batch": args.batch * world, "points": args.points,
                    "seq_len": args.points, "k": args.k, "emb_dim": args.emb,
                    "parallelism": f"dp{world}" + ("+syncbn" if (args.sync_bn and world > 1) else "")},

@@ -139,7 +139,9 @@ class _EdgeConvStack(torch.autograd.Function):
                     have16 = bf16
                     saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group if sync else None))
                     if _debug is not None:
-                        zpos = (scale * ysel + shift) > 0
+                        # sign of fmaf(scale, ysel, shift) as the kernels evaluate it: the fp64
+                        # product of two fp32 values is exact, so this sign is fma's sign
+                        zpos = (scale.double() * ysel.double() + shift.double()) > 0
                         _debug[("fwd", li)] = (idx.clone(), arg.clone(), zpos)
                 else:
                     nat.check(L.dgx_bn_eval_affine_f32(
@@ -161,10 +163,13 @@ class _EdgeConvStack(torch.autograd.Function):
         if xcat16 is None or not have16:
             xcat16 = torch.empty(0, dtype=torch.bfloat16, device=dev)
         ctx.mark_non_differentiable(xcat16)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the bf16 twin
         return xcat, xcat16
 
     @staticmethod
     def backward(ctx, dxcat, _unused):
+        if dxcat is None:
+            return (None,) * (4 + len(ctx.saved_tensors) - 3)
         if any(s is None for s in ctx.layer_state):
             raise RuntimeError("dgx EdgeConv: backward through an eval-mode (running-stats) forward is not supported")
         x_pm, xcat, xcat16, *params = ctx.saved_tensors
