@@ -2,37 +2,40 @@
 //
 // One fused pass per cloud, no N x N matrix in HBM:
 //   * |x|^2 per point in the reference's exact fp32 summation order (sqnorm).
-//   * Gram tiles on the f32 MFMA (v_mfma_f32_16x16x4_f32). Its result is
+//   * Gram tiles on the f32 MFMA (v_mfma_f32_16x16x4f32). Its result is
 //     bit-for-bit the k-ordered fmaf chain (cdna_hip_programming.md §3), which
 //     is exactly what MKL's sgemm does for the reference, so the
 //     distances match the reference bit for bit.
 //   * pd = fl(fl(2*dot - xx_j) - xx_i) (dgcnn.py:7-9) and a per-row top-k kept
-//     in registers, 4 lanes per query, merged through LDS at the end.
+//     in registers: 8 lanes per query (4 lanes x 2 candidate halves), merged
+//     at the end.
 //
-// Workgroup = 4 waves x 16 queries = 64 queries of one cloud. Candidates stream
-// through an LDS chunk laid out [j/16][c][j%16] (padded, see knn_tile_stride)
-// so the MFMA A operand read (lane l -> c = 4t + l/16, j = l%16) and the chunk
-// stores are bank-conflict-free.
+// Workgroup = 8 waves = 4 query groups x 2 candidate halves: 64 queries of one
+// cloud. The two waves of a query group share the query operand and split each
+// candidate chunk's 16-candidate tiles (even / odd), so a cloud's 32768 query
+// rows keep 4 waves per SIMD busy. Candidates stream through an LDS chunk laid
+// out [j/16][c][row(j%16)] (padded, see knn_tile_stride) so the MFMA A operand
+// read (lane l -> c = 4t + l/16, row l%16) and the chunk stores are
+// bank-conflict-free.
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 
 #include "common.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifdef DGX_KNN_DEBUG
-__device__ float* dgx_knn_dbg;
-extern "C" int dgx_knn_set_debug(float* p) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(dgx_knn_dbg), &p, sizeof(p)) == hipSuccess ? 0 : -3;
-}
-#endif
-
 namespace {
 
-constexpr int KQ_WAVES = 4;
-constexpr int KQ_QPW = 16;                    // queries per wave
-constexpr int KQ_QPB = KQ_WAVES * KQ_QPW;     // queries per block
-constexpr int KQ_QCAP = 16;                   // per-lane pending-candidate FIFO
+constexpr int KQ_GROUPS = 2;                    // query groups of 16 per block
+constexpr int KQ_HALVES = 2;                    // candidate halves: waves per query group
+constexpr int KQ_WAVES = KQ_GROUPS * KQ_HALVES;
+constexpr int KQ_THREADS = 64 * KQ_WAVES;
+constexpr int KQ_QPW = 16;                      // queries per wave
+constexpr int KQ_QPB = KQ_GROUPS * KQ_QPW;      // queries per block
+constexpr int KQ_QCAP = 16;                     // per-lane pending-candidate FIFO
+constexpr int KQ_LISTS = 4 * KQ_HALVES;         // top-k lists (lanes) per query
+static_assert(KQ_HALVES == 2, "the threshold exchange and the final merge pair two halves");
 
 // ---------------------------------------------------------------- sqnorm ----
 // |x_i|^2 with the rounding sequence of torch 2.10's CPU sum kernel, which the
@@ -125,45 +128,80 @@ __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[
     id[0] = gt_cur ? nj : id[0];
 }
 
-// Candidate chunk per LDS fill: JC candidates x CP channels, <= 16 KB, a
-// multiple of 32 candidates (tiles are processed in pairs), and JC*CP a
-// multiple of the 256 threads so each thread prefetches exactly PF floats of
-// the next chunk into registers.
-template <int CP>
-struct KnnGeom {
-    static constexpr int JC = CP <= 4 ? 1024 : (CP <= 12 ? 320 : (CP <= 32 ? 128 : (CP <= 64 ? 64 : 32)));
-    static constexpr int PF = JC * CP / 256;
-    static constexpr int XPF = (JC + 255) / 256;
-};
-
-// Per-lane list length for k <= KB: a quarter of k plus a margin. Each lane
-// sees a quarter of the candidates; the true top-k splits ~Binomial(k, 1/4)
-// over the 4 lanes, so a lane needing more than KL slots is rare. When it
-// happens the row is flagged and recomputed exactly (knn_fix_kernel).
+// Per-lane list length for k <= KB. A query's candidates are dealt over
+// KQ_LISTS = 8 lanes (interleaved by index, see knn_row), so the true top-k
+// splits ~Binomial(k, 1/8) over its lists; KL is where that distribution's
+// upper tail drops to ~2e-6 per lane. A lane needing more than KL slots flags
+// its row, which is recomputed exactly (knn_fix_kernel).
 template <int KB>
 struct KnnList {
-    // KL ~ k/4 + 5 standard deviations of Binomial(k, 1/4): a flagged row
-    // (~1e-6 per row for random point order at k = 20) costs one fix-up.
-    static constexpr int KL = KB <= 16 ? 13 : (KB <= 20 ? 16 : (KB <= 32 ? 20 : (KB <= 40 ? 24 : 34)));
-    static constexpr int RPL = (KB + 3) / 4;   // output ranks per lane
+    static constexpr int KL = KB <= 16 ? 10 : (KB <= 20 ? 12 : (KB <= 32 ? 15 : (KB <= 40 ? 17 : 23)));
+    static constexpr int RPL = (KB + 3) / 4;   // ranks per lane of a wave's 4-list merge
 };
 
-// Candidate tile image: 16 candidates x CP channels per tile, channel rows of
-// 17 floats (16 + 1 pad) and tiles KT_SKEW floats apart beyond CP*17: the
-// channel-fastest stores of a point-major chunk and the candidate-fastest
-// stores of a channel-major one both hit 64 distinct banks, and the MFMA
-// A-operand read (lane -> channel 4t + lane/16, candidate lane%16) is
-// conflict-free (odd row stride).
-constexpr int KT_ROW = 17;
-constexpr int KT_SKEW = 16;
-template <int CP>
-constexpr int knn_tile_stride() { return CP * KT_ROW + KT_SKEW; }
+// Tile row of candidate c (0..15): c = 4r + g goes to row 4g + r, so MFMA
+// output lane group g holds candidates g, g+4, g+8, g+12 of the tile. Index
+// classes are interleaved over a query's lists, so neighbours that sit close
+// together in a cloud's index order still spread over its 8 lists.
+__device__ __forceinline__ int knn_row(int c) { return ((c & 3) << 2) | (c >> 2); }
+__device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (row >> 2); }  // inverse (an involution)
 
+// ------------------------------------------------------------ operand image --
+// The MFMA A operand of every 16-candidate tile, in lane order: for tile s of
+// cloud b, lane l = 16*kk + i holds channels 4t + kk (t = 0..NSTEP-1) of
+// candidate 16 s + knn_cand(i), NSTEP consecutive floats:
+//     img[((b*ntile + s)*64 + l)*NSTEP + t]
+// so one wave fetches a whole tile as NSTEP*256 contiguous bytes with 16-byte
+// loads straight from L2, without staging through LDS or synchronising with
+// other waves. Zero rows pad N to a multiple of 16 and zero channels pad C to
+// 4*NSTEP (they add exact zeros to the fmaf chain). xximg holds |x_j|^2 in the
+// same row order: xximg[(b*ntile + s)*16 + i]. A query's own operand (the B
+// side) is read from the same image.
+constexpr int KI_TILES = 4;  // tiles per image-builder block
 template <int NSTEP>
-constexpr int knn_smem_floats() {
+__global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
+                                                        int64_t sN, const float* __restrict__ xx, int B, int C,
+                                                        int N, int ntile, int tgroups, float* __restrict__ img,
+                                                        float* __restrict__ xximg) {
     constexpr int CP = NSTEP * 4;
-    constexpr int JC = KnnGeom<CP>::JC;
-    return (JC / 16) * knn_tile_stride<CP>() + JC + KQ_WAVES * 2 * KQ_QCAP * 64;  // tile | xx | per-wave FIFOs
+    constexpr int P = 16 * KI_TILES;
+    __shared__ float rows[P][CP + 1];
+    const int b = blockIdx.x / tgroups;
+    const int s0 = (blockIdx.x - b * tgroups) * KI_TILES;
+    const int t = threadIdx.x;
+    const float* __restrict__ xb = x + b * sB;
+    for (int e = t; e < P * CP; e += 256) {
+        int p, c;
+        if (sN == 1) { c = e / P; p = e - c * P; }   // candidate-fastest: unit stride along n
+        else { p = e / CP; c = e - p * CP; }          // channel-fastest
+        const int n = s0 * 16 + p;
+        rows[p][c] = (n < N && c < C) ? xb[c * sC + n * sN] : 0.f;
+    }
+    if (t < P && s0 + t / 16 < ntile) {
+        const int n = (s0 + t / 16) * 16 + knn_cand(t & 15);
+        xximg[((int64_t)b * ntile + s0) * 16 + t] = n < N ? xx[(int64_t)b * N + n] : 0.f;
+    }
+    __syncthreads();
+    const int ntl = min(KI_TILES, ntile - s0);
+    float* __restrict__ dst = img + ((int64_t)b * ntile + s0) * 64 * NSTEP;
+    for (int e = t; e < ntl * 64 * NSTEP; e += 256) {
+        const int tl = e / (64 * NSTEP);
+        const int r = e - tl * 64 * NSTEP;
+        const int l = r / NSTEP, st = r - l * NSTEP;
+        dst[e] = rows[tl * 16 + knn_cand(l & 15)][4 * st + (l >> 4)];
+    }
+}
+
+inline int knn_nstep(int C) { return C <= 4 ? 1 : (C <= 12 ? 3 : (C <= 32 ? 8 : (C <= 64 ? 16 : 32))); }
+inline int knn_ntile(int N) { return (N + 15) / 16; }
+
+template <int KB>
+constexpr int knn_smem_floats() {
+    constexpr int stream = KQ_HALVES * KQ_QPB                     // published admission bounds
+                           + KQ_WAVES * KQ_QCAP * 64              // FIFO values
+                           + KQ_WAVES * KQ_QCAP * 32;             // FIFO indices (u16)
+    constexpr int merge = KQ_HALVES * KQ_QPB * KB * 2 + 2 * KQ_QPB;  // half lists | k-th | flags
+    return stream > merge ? stream : merge;
 }
 
 // Canonical order: value descending, then index ascending.
@@ -171,24 +209,41 @@ __device__ __forceinline__ bool canon_better(float av, int aj, float bv, int bj)
     return av > bv || (av == bv && aj < bj);
 }
 
+template <int V>
+__device__ __forceinline__ void ld_vec(const float* __restrict__ p, float (&r)[V]) {
+    if constexpr (V % 4 == 0) {
+#pragma unroll
+        for (int u = 0; u < V; u += 4) {
+            const float4 q = *reinterpret_cast<const float4*>(p + u);
+            r[u] = q.x;
+            r[u + 1] = q.y;
+            r[u + 2] = q.z;
+            r[u + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; ++u) r[u] = p[u];
+    }
+}
+
 // ------------------------------------------------------------ knn kernel ----
-template <int NSTEP, int KB, bool CMAJOR>
-__global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
-                                                    int64_t sN, const float* __restrict__ xx, int B, int C,
-                                                    int N, int k, int nqb, int64_t* __restrict__ idx64,
-                                                    int32_t* __restrict__ idx32, float* __restrict__ vals) {
+// Block = KQ_GROUPS query groups x 2 candidate halves, one wave each. A wave
+// streams the tiles s = h, h+2, h+4, ... of its cloud's image with its loads
+// two units ahead (see the operand stream below). The only block-wide
+// synchronisation is the final merge.
+template <int NSTEP, int KB>
+__global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const float* __restrict__ img,
+                                                         const float* __restrict__ xximg,
+                                                         const float* __restrict__ xx, int B, int N, int k,
+                                                         int nqb, int64_t* __restrict__ idx64,
+                                                         int32_t* __restrict__ idx32, float* __restrict__ vals) {
 #pragma clang fp contract(off)
-    constexpr int CP = NSTEP * 4;
-    constexpr int JC = KnnGeom<CP>::JC;
-    constexpr int PF = KnnGeom<CP>::PF;
-    constexpr int XPF = KnnGeom<CP>::XPF;
     constexpr int KL = KnnList<KB>::KL;
     constexpr int RPL = KnnList<KB>::RPL;
-    __shared__ __attribute__((aligned(16))) float smem[knn_smem_floats<NSTEP>()];
-    float* tile = smem;                 // [JC/16][CP][16]
-    constexpr int TS = knn_tile_stride<CP>();
-    float* xxs = smem + (JC / 16) * TS;  // [JC]
-    float* qbase = xxs + JC;            // per wave: [KQ_QCAP][64] float2 (value, index)
+    __shared__ __attribute__((aligned(16))) float smem[knn_smem_floats<KB>()];
+    float* pub = smem;                            // [KQ_HALVES][KQ_QPB] admission bounds
+    float* fval = smem + KQ_HALVES * KQ_QPB;      // per wave [KQ_QCAP][64] pending values
+    uint16_t* fidx = reinterpret_cast<uint16_t*>(fval + KQ_WAVES * KQ_QCAP * 64);  // ... and indices
 
     int b, qb;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
@@ -196,62 +251,34 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int g = lane >> 4;     // which quarter of the candidates this lane sees
+    const int grp = wave % KQ_GROUPS;  // query group
+    const int h = wave / KQ_GROUPS;    // candidate half: tiles h, h + 2, h + 4, ...
+    const int g = lane >> 4;           // MFMA output rows 4g..4g+3 of a tile
     const int ql = lane & 15;
-    const int q = qb * KQ_QPB + wave * KQ_QPW + ql;
-    const float* __restrict__ xb = x + b * sB;
-    const float* __restrict__ xxb = xx + (int64_t)b * N;
+    const int qq = grp * KQ_QPW + ql;  // query within the block
+    const int q = qb * KQ_QPB + qq;
+    const int ntile = (N + 15) >> 4;
+    const float* __restrict__ ib = img + (int64_t)b * ntile * 64 * NSTEP;
+    const float* __restrict__ xib = xximg + (int64_t)b * ntile * 16;
 
-    // B operand (queries) stays in registers: lane holds x[q][4t + g].
+    // B operand (queries) in registers: lane holds x[q][4t + g], read from the
+    // query's own image row (zero channels beyond C; q >= N reads a zero row).
     float bq[NSTEP];
-#pragma unroll
-    for (int t = 0; t < NSTEP; ++t) {
-        int c = 4 * t + g;
-        bq[t] = (q < N && c < C) ? xb[c * sC + q * sN] : 0.f;
+    {
+        const int qs = min(q, N - 1);
+        ld_vec<NSTEP>(ib + ((int64_t)(qs >> 4) * 64 + g * 16 + knn_row(qs & 15)) * NSTEP, bq);
     }
-    const float xxq = q < N ? xxb[q] : 0.f;
-
-    // Next-chunk prefetch in registers: issued before the current chunk's
-    // compute, written to LDS after it (load latency hidden by the MFMAs).
-    float pf[PF], pfx[XPF];
-    auto load_regs = [&](int j0) {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            const int e = tid + u * 256;
-            int jj, c;
-            if (CMAJOR) { jj = e % JC; c = e / JC; }
-            else { c = e % CP; jj = e / CP; }
-            const int j = j0 + jj;
-            pf[u] = (c < C && j < N) ? xb[c * sC + j * sN] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < XPF; ++u) {
-            const int jj = tid + u * 256;
-            pfx[u] = (jj < JC && j0 + jj < N) ? xxb[j0 + jj] : 0.f;
-        }
-    };
-    auto store_regs = [&]() {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            const int e = tid + u * 256;
-            int jj, c;
-            if (CMAJOR) { jj = e % JC; c = e / JC; }
-            else { c = e % CP; jj = e / CP; }
-            tile[(jj >> 4) * TS + c * KT_ROW + (jj & 15)] = pf[u];
-        }
-#pragma unroll
-        for (int u = 0; u < XPF; ++u) {
-            const int jj = tid + u * 256;
-            if (jj < JC) xxs[jj] = pfx[u];
-        }
-    };
+    const float xxq = q < N ? xx[(int64_t)b * N + q] : 0.f;
 
     // Each lane keeps the KL best of ITS candidates (sorted, registers, static
     // indexing). Admission filter thr = max(own KL-th, T) where T = min over
-    // the query's 4 lanes of their m-th value, m = ceil(k/4): 4 lanes x m
-    // candidates >= T exist, so T never exceeds the row's final k-th value.
+    // the query's 8 lists of their m-th value, m = ceil(k/8): 8 lists x m
+    // candidates >= T exist, so T never exceeds the row's final k-th value. The
+    // other half's 4 lists contribute through `pub` — a value published at its
+    // last flush; lists only improve, so a stale value is still a lower bound.
     // '>=' keeps equal values; their order is settled canonically at the merge.
-    const int m = (k + 3) >> 2;
+    const int m = (k + KQ_LISTS - 1) / KQ_LISTS;
+    const int m4 = (k + 3) / 4;
     float lv[KL];
     int li[KL];
 #pragma unroll
@@ -260,94 +287,121 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
     // Candidates that pass the filter wait in a per-lane FIFO in LDS and are
     // inserted in batches, so an insertion round (5*KL VALU ops for the whole
     // wave) is paid once per admitted candidate of the busiest lane.
-    float2* fifo = reinterpret_cast<float2*>(qbase) + wave * (KQ_QCAP * 64);
+    float* fv = fval + wave * (KQ_QCAP * 64);
+    uint16_t* fj = fidx + wave * (KQ_QCAP * 64);
     int cnt = 0;
     float thr = -INFINITY;
+    if (tid < KQ_HALVES * KQ_QPB) pub[tid] = -INFINITY;
+    static_assert(KnnList<KB>::KL >= (KB + 3) / 4, "lists must hold the m4-th value");
+    __syncthreads();
     auto flush = [&]() {
-        float2 cur = cnt > 0 ? fifo[lane] : make_float2(-INFINITY, __int_as_float(0x7fffffff));
-#pragma unroll 1
-        for (int t = 0; __any(t < cnt); ++t) {
-            const float2 nxt = (t + 1 < cnt) ? fifo[(t + 1) * 64 + lane]
-                                             : make_float2(-INFINITY, __int_as_float(0x7fffffff));
-            list_insert_ordered<KL>(lv, li, cur.x >= thr ? cur.x : -INFINITY, __float_as_int(cur.y));
-            cur = nxt;
+        // branch-free rounds: slots past a lane's count read stale entries and
+        // are replaced by -inf, so every round is the same straight-line code
+        float cv = fv[lane];
+        int cj = fj[lane];
+        cv = cnt > 0 ? cv : -INFINITY;
+        // fully unrolled with an early exit: no loop-carried copies of the list
+#pragma unroll
+        for (int t = 0; t < KQ_QCAP; ++t) {
+            if (!__any(t < cnt)) break;
+            const int nx = min(t + 1, KQ_QCAP - 1);
+            float nv = fv[nx * 64 + lane];
+            const int nj = fj[nx * 64 + lane];
+            nv = t + 1 < cnt ? nv : -INFINITY;
+            list_insert_ordered<KL>(lv, li, cv >= thr ? cv : -INFINITY, cj);
+            cv = nv;
+            cj = nj;
         }
         cnt = 0;
-        float tm = lv[0];
+        // admission bound: max of (own 4 lists' min m4-th value: 4*m4 >= k
+        // candidates reach it) and (all 8 lists' min m-th value: 8*m >= k)
+        float tm = lv[0], t4 = lv[0];
 #pragma unroll
-        for (int t = 1; t < KL; ++t) tm = (t == m - 1) ? lv[t] : tm;
+        for (int t = 1; t < KL; ++t) {
+            tm = (t == m - 1) ? lv[t] : tm;
+            t4 = (t == m4 - 1) ? lv[t] : t4;
+        }
         tm = fminf(tm, __shfl_xor(tm, 16));
         tm = fminf(tm, __shfl_xor(tm, 32));
-        thr = fmaxf(tm, lv[KL - 1]);
+        t4 = fminf(t4, __shfl_xor(t4, 16));
+        t4 = fminf(t4, __shfl_xor(t4, 32));
+        if (g == 0) __hip_atomic_store(pub + h * KQ_QPB + qq, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const float tp = __hip_atomic_load(pub + (1 - h) * KQ_QPB + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        thr = fmaxf(fmaxf(t4, fminf(tm, tp)), lv[KL - 1]);
     };
 
-    auto consider = [&](float dot, float xc, int j, bool valid) {
-        float two_dot = 2.0f * dot;
-        float tq = two_dot - xc;
-        float v = tq - xxq;
-        const bool pass = valid && v >= thr;
-        if (pass) fifo[cnt * 64 + lane] = make_float2(v, __int_as_float(j));
+    auto consider = [&](float dot, float xc, int j) {
+        const float two_dot = 2.0f * dot;
+        const float tq = two_dot - xc;
+        const float v = tq - xxq;
+        const bool pass = j < N && v >= thr;
+        // unconditional store: a rejected candidate's slot is reused by the
+        // next one (a tile adds at most 4 entries to a FIFO holding <= QCAP-4)
+        fv[cnt * 64 + lane] = v;
+        fj[cnt * 64 + lane] = (uint16_t)j;
         cnt += pass ? 1 : 0;
     };
 
-    const int nch = (N + JC - 1) / JC;
-    load_regs(0);
-    store_regs();
-    __syncthreads();
-    for (int ch = 0; ch < nch; ++ch) {
-        if (ch + 1 < nch) load_regs((ch + 1) * JC);
-        const int jend = min(JC, N - ch * JC);
-        // tiles in pairs: two independent MFMA chains in flight
+    // Operand stream: units of SW MFMA k-steps (a whole tile when NSTEP <= 16,
+    // a quarter tile at NSTEP = 32) through a two-slot register ring; the load
+    // of unit u+2 is issued as soon as unit u's MFMAs have read their slot, so
+    // a unit's L2 latency hides behind two units of MFMA + selection work.
+    constexpr int SW = NSTEP <= 8 ? NSTEP : 8;
+    constexpr int SPT = NSTEP / SW;          // units per tile
+    constexpr int UB = SPT < 2 ? 2 : SPT;    // units per loop trip (static ring slots)
+    static_assert(NSTEP % SW == 0 && UB % SPT == 0, "unit split");
+    const int ntl = (ntile - h + KQ_HALVES - 1) / KQ_HALVES;  // this half's tiles: h + 2*tl
+    const int nunits = ntl * SPT;
+    float a[2][SW];
+    float4 xq[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    auto load = [&](int slot, int u) {
+        if (u >= nunits) return;
+        const int s = h + KQ_HALVES * (u / SPT), sl = u % SPT;
+        ld_vec<SW>(ib + ((int64_t)s * 64 + lane) * NSTEP + sl * SW, a[slot]);
+        if (sl == 0) xq[slot] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
+    };
+    load(0, 0);
+    load(1, 1);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float4 xc = xq[0];
 #pragma unroll 1
-        for (int s = 0; s < (jend + 15) / 16; s += 2) {
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-            const float* __restrict__ ts = tile + s * TS + (lane >> 4) * KT_ROW + (lane & 15);
+    for (int u = 0; u < nunits; u += UB) {
 #pragma unroll
-            for (int t = 0; t < NSTEP; ++t) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ts[t * 4 * KT_ROW], bq[t], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ts[TS + t * 4 * KT_ROW], bq[t], acc1, 0, 0, 0);
+        for (int ub = 0; ub < UB; ++ub) {
+            const int slot = ub & 1, sl = ub % SPT;
+            if (SPT > 1 || u + ub < nunits) {
+                if (sl == 0) {
+                    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                    xc = xq[slot];
+                }
+#pragma unroll
+                for (int t = 0; t < SW; ++t)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][t], bq[sl * SW + t], acc, 0, 0, 0);
+                load(slot, u + ub + 2);
+                if (sl == SPT - 1) {
+                    // lane holds rows 4g..4g+3 = candidates g, g+4, g+8, g+12 of the tile
+                    const int j0 = (h + KQ_HALVES * ((u + ub) / SPT)) * 16 + g;
+                    consider(acc[0], xc.x, j0);
+                    consider(acc[1], xc.y, j0 + 4);
+                    consider(acc[2], xc.z, j0 + 8);
+                    consider(acc[3], xc.w, j0 + 12);
+                    if (__any(cnt > KQ_QCAP - 4)) flush();
+                }
             }
-            // lane holds candidates j = jb + r (r = 0..3) and jb + 16 + r of query q
-            const int jl = s * 16 + 4 * g;
-            const int jb = ch * JC + jl;
-            const float4 xc0 = *reinterpret_cast<const float4*>(xxs + jl);
-            const float4 xc1 = *reinterpret_cast<const float4*>(xxs + jl + 16);
-            const int lim = N - jb;
-            consider(acc0[0], xc0.x, jb + 0, 0 < lim);
-            consider(acc0[1], xc0.y, jb + 1, 1 < lim);
-            consider(acc0[2], xc0.z, jb + 2, 2 < lim);
-            consider(acc0[3], xc0.w, jb + 3, 3 < lim);
-            consider(acc1[0], xc1.x, jb + 16, 16 < lim);
-            consider(acc1[1], xc1.y, jb + 17, 17 < lim);
-            consider(acc1[2], xc1.z, jb + 18, 18 < lim);
-            consider(acc1[3], xc1.w, jb + 19, 19 < lim);
-            if (__any(cnt > KQ_QCAP - 8)) flush();
-        }
-        __syncthreads();
-        if (ch + 1 < nch) {
-            store_regs();
-            __syncthreads();
         }
     }
     flush();
 
-#ifdef DGX_KNN_DEBUG
-    if (q < N && dgx_knn_dbg) {
-        float* d = dgx_knn_dbg + (((int64_t)b * N + q) * 4 + g) * KL * 2;
-        for (int t = 0; t < KL; ++t) { d[t] = lv[t]; d[KL + t] = (float)li[t]; }
-    }
-#endif
-    // Merge the query's 4 lists (lanes ql, ql+16, ql+32, ql+48) by k rounds of
-    // a canonical arg-max over the 4 list heads; the winning lane pops its
-    // head. Rank r ends up in lane r % 4.
+    // Merge the wave's 4 lists of each query (lanes ql, ql+16, ql+32, ql+48)
+    // by k rounds of a canonical arg-max over the 4 list heads; the winning
+    // lane pops its head. Rank r ends up in lane r % 4.
     const float last = lv[KL - 1];
     float ov[RPL];
     int oj[RPL];
-    float hv = -INFINITY;
 #pragma unroll
     for (int r = 0; r < KB; ++r) {
         if (r < k) {
-            hv = lv[0];
+            float hv = lv[0];
             int hj = li[0];
             float pv = __shfl_xor(hv, 16);
             int pj = __shfl_xor(hj, 16);
@@ -366,21 +420,60 @@ __global__ __launch_bounds__(256, 2) void knn_kernel(const float* __restrict__ x
             if ((r & 3) == g) { ov[r >> 2] = hv; oj[r >> 2] = hj; }
         }
     }
-    // hv is now the merged k-th value. A lane whose list was full and whose
-    // last kept value reaches it may have dropped a member of the true top-k:
-    // mark the row for the exact fix-up pass.
-    int flag = (last != -INFINITY && last >= hv) ? 1 : 0;
-    flag |= __shfl_xor(flag, 16);
-    flag |= __shfl_xor(flag, 32);
+
+    // Merge the two halves: each half's sorted top-k goes to LDS; an element's
+    // final rank is its rank in its own list plus the number of elements of the
+    // other list that are canonically better (binary search). The halves hold
+    // disjoint candidates, so the ranks 0..k-1 are taken exactly once.
+    __syncthreads();  // every wave is done with its FIFO
+    float2* lists = reinterpret_cast<float2*>(smem);         // [KQ_HALVES][KQ_QPB][KB]
+    float* kth = smem + KQ_HALVES * KQ_QPB * KB * 2;         // [KQ_QPB] merged k-th value
+    int* flg = reinterpret_cast<int*>(kth + KQ_QPB);         // [KQ_QPB] row needs the fix-up
+#pragma unroll
+    for (int t = 0; t < RPL; ++t) {
+        const int r = 4 * t + g;
+        if (r < k) lists[(h * KQ_QPB + qq) * KB + r] = make_float2(ov[t], __int_as_float(oj[t]));
+    }
+    if (tid < KQ_QPB) {
+        kth[tid] = -INFINITY;
+        flg[tid] = 0;
+    }
+    __syncthreads();
+    const float2* other = lists + ((1 - h) * KQ_QPB + qq) * KB;
+    int rk[RPL];
+#pragma unroll
+    for (int t = 0; t < RPL; ++t) {
+        const int r = 4 * t + g;
+        rk[t] = k;
+        if (r < k) {
+            int lo = 0, hi = k;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const float2 o = other[mid];
+                if (canon_better(o.x, __float_as_int(o.y), ov[t], oj[t])) lo = mid + 1;
+                else hi = mid;
+            }
+            rk[t] = r + lo;
+            if (rk[t] == k - 1) kth[qq] = ov[t];
+        }
+    }
+    __syncthreads();
+    // A lane whose list was full and whose last kept value reaches the merged
+    // k-th may have dropped a member of the true top-k: mark the row for the
+    // exact fix-up pass.
+    const float kv = kth[qq];
+    if (last != -INFINITY && last >= kv) flg[qq] = 1;
+    __syncthreads();
     if (q < N) {
+        const bool flag = flg[qq] != 0;
         const int64_t row = ((int64_t)b * N + q) * k;
 #pragma unroll
         for (int t = 0; t < RPL; ++t) {
-            const int r = 4 * t + g;
+            const int r = rk[t];
             if (r < k) {
                 // flagged: rank 0 = -1 marker, rank 1 = bits of the merged k-th
                 // value (a lower bound of the true k-th) for the fix-up pass
-                const int j = !flag ? oj[t] : (r == 0 ? -1 : (r == 1 ? __float_as_int(hv) : oj[t]));
+                const int j = !flag ? oj[t] : (r == 0 ? -1 : (r == 1 ? __float_as_int(kv) : oj[t]));
                 if (idx64) idx64[row + r] = j;
                 if (idx32) idx32[row + r] = j;
                 if (vals) vals[row + r] = ov[t];
@@ -510,17 +603,24 @@ __global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ 
     }
 }
 
+template <int NSTEP>
+int launch_image(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
+                 float* img, float* xximg, hipStream_t st) {
+    const int ntile = knn_ntile(N);
+    const int tgroups = (ntile + KI_TILES - 1) / KI_TILES;
+    hipLaunchKernelGGL(knn_image_kernel<NSTEP>, dim3((unsigned)(B * tgroups)), dim3(256), 0, st, x, sB, sC, sN, xx,
+                       B, C, N, ntile, tgroups, img, xximg);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
 template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-               int k, int64_t* idx64, int32_t* idx32, float* vals, hipStream_t st) {
+               int k, int64_t* idx64, int32_t* idx32, float* vals, float* img, float* xximg, hipStream_t st) {
+    int rc = launch_image<NSTEP>(x, sB, sC, sN, xx, B, C, N, img, xximg, st);
+    if (rc != DGX_OK) return rc;
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
-    dim3 grid(dgx_xcd_cloud_grid(B, nqb)), block(256);
-    if (sN == 1)
-        hipLaunchKernelGGL((knn_kernel<NSTEP, KB, true>), grid, block, 0, st, x, sB, sC, sN, xx, B, C, N, k,
-                           nqb, idx64, idx32, vals);
-    else
-        hipLaunchKernelGGL((knn_kernel<NSTEP, KB, false>), grid, block, 0, st, x, sB, sC, sN, xx, B, C, N, k,
-                           nqb, idx64, idx32, vals);
+    hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
+                       xximg, xx, B, N, k, nqb, idx64, idx32, vals);
     if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH;
     static const bool nofix = getenv("DGX_KNN_NOFIX") != nullptr;  // diagnostics: leave flagged rows marked
     if (nofix) return DGX_OK;
@@ -532,13 +632,20 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
 
 template <int NSTEP>
 int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, float* vals, hipStream_t st) {
-    if (k <= 16) return launch_knn<NSTEP, 16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    if (k <= 20) return launch_knn<NSTEP, 20>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    if (k <= 32) return launch_knn<NSTEP, 32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    if (k <= 40) return launch_knn<NSTEP, 40>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    return launch_knn<NSTEP, 64>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+               int64_t* idx64, int32_t* idx32, float* vals, float* img, float* xximg, hipStream_t st) {
+#define DGX_KNN_K(KBV) \
+    return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st)
+    if (k <= 16) DGX_KNN_K(16);
+    if (k <= 20) DGX_KNN_K(20);
+    if (k <= 32) DGX_KNN_K(32);
+    if (k <= 40) DGX_KNN_K(40);
+    DGX_KNN_K(64);
+#undef DGX_KNN_K
 }
+
+// image floats per cloud, then |x|^2 image floats per cloud
+inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
+inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
 
 }  // namespace
 
@@ -555,20 +662,36 @@ int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-size_t dgx_knn_workspace_bytes(int B, int N) { return (size_t)B * (size_t)N * sizeof(float); }
+size_t dgx_knn_image_bytes(int B, int C, int N) {
+    if (B < 0 || C < 1 || N < 1) return 0;
+    return (size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) * sizeof(float);
+}
+
+size_t dgx_knn_workspace_bytes(int B, int C, int N) {
+    if (B < 0 || C < 1 || N < 1) return 0;
+    // |x|^2 (B*N floats, rounded up to 16 bytes) | operand image
+    return ((((size_t)B * N + 3) & ~(size_t)3) * sizeof(float)) + dgx_knn_image_bytes(B, C, N);
+}
 
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                       int k, int64_t* idx64, int32_t* idx32, float* vals, void* stream) {
+                       int k, int64_t* idx64, int32_t* idx32, float* vals, void* image, size_t image_bytes,
+                       void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
     if (B == 0) return DGX_OK;
+    if (!image || image_bytes < dgx_knn_image_bytes(B, C, N)) return DGX_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(image) & 15) != 0) return DGX_EINVAL;  // 16-byte operand loads
+    float* img = static_cast<float*>(image);
+    float* xximg = img + (size_t)B * knn_image_floats(C, N);
     hipStream_t st = dgx_stream(stream);
-    if (C <= 4) return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    if (C <= 12) return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    if (C <= 32) return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    if (C <= 64) return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
-    return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, st);
+    switch (knn_nstep(C)) {
+        case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 3: return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 8: return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 16: return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        default: return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+    }
 }
 
 int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int k, int order,
@@ -576,12 +699,15 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C
     if (!x || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
-    if (workspace_bytes < dgx_knn_workspace_bytes(B, N) || !workspace) return DGX_EINVAL;
+    if (workspace_bytes < dgx_knn_workspace_bytes(B, C, N) || !workspace) return DGX_EINVAL;
     if (B == 0) return DGX_OK;
     float* xx = static_cast<float*>(workspace);
+    // image after xx, rounded up to 16 bytes
+    const size_t off = ((size_t)B * N + 3) & ~(size_t)3;
     int rc = dgx_sqnorm_f32(x, sB, sC, sN, B, C, N, order, xx, stream);
     if (rc != DGX_OK) return rc;
-    return dgx_knn_select_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, nullptr, stream);
+    return dgx_knn_select_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, nullptr, xx + off,
+                              dgx_knn_image_bytes(B, C, N), stream);
 }
 
 }  // extern "C"

@@ -27,10 +27,11 @@ _vp, _i64, _i32, _f32, _f64, _sz = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_in
 _SIGS = {
     "dgx_version": [],
     "dgx_strerror": [_i32],
-    "dgx_knn_workspace_bytes": [_i32, _i32],
+    "dgx_knn_workspace_bytes": [_i32, _i32, _i32],
+    "dgx_knn_image_bytes": [_i32, _i32, _i32],
     "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
     "dgx_sqnorm_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp],
-    "dgx_knn_select_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
+    "dgx_knn_select_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp],
     "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_edge_partials_rows": [_i32, _i32, _i32],
@@ -67,6 +68,7 @@ _RESTYPES = {
     "dgx_version": ctypes.c_char_p,
     "dgx_strerror": ctypes.c_char_p,
     "dgx_knn_workspace_bytes": _sz,
+    "dgx_knn_image_bytes": _sz,
 }
 
 

@@ -42,6 +42,8 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
     vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
     xx = torch.empty((B * N,), dtype=torch.float32, device=x.device)
+    img_bytes = L.dgx_knn_image_bytes(B, C, N)
+    img = torch.empty((max(img_bytes, 4) + 3) // 4, dtype=torch.float32, device=x.device)  # operand image scratch
     stream = nat.stream_of(x)
     with torch.cuda.device(x.device):
         nat.check(L.dgx_sqnorm_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx), stream), "sqnorm")
@@ -51,7 +53,8 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
             ev0.record()
         rc = L.dgx_knn_select_f32(nat.ptr(x), sB, sC, sN, nat.ptr(xx), B, C, N, k,
                                   nat.ptr(idx) if out_dtype == torch.int64 else None,
-                                  nat.ptr(idx) if out_dtype == torch.int32 else None, nat.ptr(vals), stream)
+                                  nat.ptr(idx) if out_dtype == torch.int32 else None, nat.ptr(vals),
+                                  nat.ptr(img), img_bytes, stream)
         if rec:
             ev1.record()
             _timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
