@@ -73,6 +73,20 @@ __device__ __forceinline__ float rowsum4(const float* e, int stride, int n) {
 // array (which would live in scratch memory).
 constexpr int SQ_THREADS = 64;
 
+// Sum of the C squares sq[c*stride] in the rounding order `order` selects.
+__device__ __forceinline__ float sqnorm_sum(const float* sq, int stride, int C, int order, bool tail) {
+#pragma clang fp contract(off)
+    if (order == DGX_ORDER_VEC8X4) {
+        if (C < 8) return rowsum4(sq, stride, C);
+        const int vs = C >> 3;
+        float fin = 0.f;
+        for (int c = 8 * vs; c < C; ++c) fin = fin + sq[c * stride];
+        for (int l = 0; l < 8; ++l) fin = fin + rowsum4(sq + l * stride, 8 * stride, vs);
+        return fin;
+    }
+    return tail ? rowsum4(sq, stride, C) : cascade16(sq, stride, C);
+}
+
 __device__ __forceinline__ float sqnorm_point(const float* __restrict__ p, int64_t sC, int C, int order,
                                               bool tail, float* sq) {
 #pragma clang fp contract(off)
@@ -84,15 +98,7 @@ __device__ __forceinline__ float sqnorm_point(const float* __restrict__ p, int64
         for (int u = 0; u < 16; ++u)
             if (c0 + u < C) sq[(c0 + u) * SQ_THREADS] = v[u] * v[u];
     }
-    if (order == DGX_ORDER_VEC8X4) {
-        if (C < 8) return rowsum4(sq, SQ_THREADS, C);
-        const int vs = C >> 3;
-        float fin = 0.f;
-        for (int c = 8 * vs; c < C; ++c) fin = fin + sq[c * SQ_THREADS];
-        for (int l = 0; l < 8; ++l) fin = fin + rowsum4(sq + l * SQ_THREADS, 8 * SQ_THREADS, vs);
-        return fin;
-    }
-    return tail ? rowsum4(sq, SQ_THREADS, C) : cascade16(sq, SQ_THREADS, C);
+    return sqnorm_sum(sq, SQ_THREADS, C, order, tail);
 }
 
 __global__ __launch_bounds__(SQ_THREADS) void sqnorm_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
@@ -157,15 +163,19 @@ __device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (ro
 // 4*NSTEP (they add exact zeros to the fmaf chain). xximg holds |x_j|^2 in the
 // same row order: xximg[(b*ntile + s)*16 + i]. A query's own operand (the B
 // side) is read from the same image.
-constexpr int KI_TILES = 4;  // tiles per image-builder block
+constexpr int KI_TILES = 1;  // tiles per image-builder block
+// One pass over x per layer: the operand image, the |x|^2 image and xx itself
+// (|x_i|^2 in the reference's rounding order, sqnorm_sum on the staged row).
 template <int NSTEP>
 __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
-                                                        int64_t sN, const float* __restrict__ xx, int B, int C,
-                                                        int N, int ntile, int tgroups, float* __restrict__ img,
-                                                        float* __restrict__ xximg) {
+                                                        int64_t sN, int B, int C, int N, int order, int ntile,
+                                                        int tgroups, float* __restrict__ xx,
+                                                        float* __restrict__ img, float* __restrict__ xximg) {
+#pragma clang fp contract(off)
     constexpr int CP = NSTEP * 4;
     constexpr int P = 16 * KI_TILES;
     __shared__ float rows[P][CP + 1];
+    __shared__ float nrm[P];
     const int b = blockIdx.x / tgroups;
     const int s0 = (blockIdx.x - b * tgroups) * KI_TILES;
     const int t = threadIdx.x;
@@ -177,10 +187,6 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
         const int n = s0 * 16 + p;
         rows[p][c] = (n < N && c < C) ? xb[c * sC + n * sN] : 0.f;
     }
-    if (t < P && s0 + t / 16 < ntile) {
-        const int n = (s0 + t / 16) * 16 + knn_cand(t & 15);
-        xximg[((int64_t)b * ntile + s0) * 16 + t] = n < N ? xx[(int64_t)b * N + n] : 0.f;
-    }
     __syncthreads();
     const int ntl = min(KI_TILES, ntile - s0);
     float* __restrict__ dst = img + ((int64_t)b * ntile + s0) * 64 * NSTEP;
@@ -190,6 +196,19 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
         const int l = r / NSTEP, st = r - l * NSTEP;
         dst[e] = rows[tl * 16 + knn_cand(l & 15)][4 * st + (l >> 4)];
     }
+    __syncthreads();
+    if (t < P) {  // each thread squares its own row in place, then sums it in the reference order
+        const int n = s0 * 16 + t;
+        float v = 0.f;
+        if (n < N) {
+            for (int c = 0; c < C; ++c) rows[t][c] = rows[t][c] * rows[t][c];
+            v = sqnorm_sum(&rows[t][0], 1, C, order, n >= (N & ~31));
+            xx[(int64_t)b * N + n] = v;
+        }
+        nrm[t] = v;
+    }
+    __syncthreads();
+    if (t < P && s0 + t / 16 < ntile) xximg[((int64_t)b * ntile + s0) * 16 + t] = nrm[(t & ~15) + knn_cand(t & 15)];
 }
 
 inline int knn_nstep(int C) { return C <= 4 ? 1 : (C <= 12 ? 3 : (C <= 32 ? 8 : (C <= 64 ? 16 : 32))); }
@@ -604,20 +623,19 @@ __global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ 
 }
 
 template <int NSTEP>
-int launch_image(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                 float* img, float* xximg, hipStream_t st) {
+int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,
+                   float* img, float* xximg, hipStream_t st) {
     const int ntile = knn_ntile(N);
     const int tgroups = (ntile + KI_TILES - 1) / KI_TILES;
-    hipLaunchKernelGGL(knn_image_kernel<NSTEP>, dim3((unsigned)(B * tgroups)), dim3(256), 0, st, x, sB, sC, sN, xx,
-                       B, C, N, ntile, tgroups, img, xximg);
+    hipLaunchKernelGGL(knn_image_kernel<NSTEP>, dim3((unsigned)(B * tgroups)), dim3(256), 0, st, x, sB, sC, sN, B, C,
+                       N, order, ntile, tgroups, xx, img, xximg);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-               int k, int64_t* idx64, int32_t* idx32, float* vals, float* img, float* xximg, hipStream_t st) {
-    int rc = launch_image<NSTEP>(x, sB, sC, sN, xx, B, C, N, img, xximg, st);
-    if (rc != DGX_OK) return rc;
+               int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
+               hipStream_t st) {
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
                        xximg, xx, B, N, k, nqb, idx64, idx32, vals);
@@ -632,7 +650,7 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
 
 template <int NSTEP>
 int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, float* vals, float* img, float* xximg, hipStream_t st) {
+               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, hipStream_t st) {
 #define DGX_KNN_K(KBV) \
     return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st)
     if (k <= 16) DGX_KNN_K(16);
@@ -673,17 +691,36 @@ size_t dgx_knn_workspace_bytes(int B, int C, int N) {
     return ((((size_t)B * N + 3) & ~(size_t)3) * sizeof(float)) + dgx_knn_image_bytes(B, C, N);
 }
 
+int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order,
+                        float* xx, void* image, size_t image_bytes, void* stream) {
+    if (!x || !xx || B < 0 || C < 1 || N < 1) return DGX_EINVAL;
+    if (C > 128) return DGX_EUNSUPPORTED;
+    if (B == 0) return DGX_OK;
+    if (!image || image_bytes < dgx_knn_image_bytes(B, C, N)) return DGX_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(image) & 15) != 0) return DGX_EINVAL;  // 16-byte operand loads
+    float* img = static_cast<float*>(image);
+    float* xximg = img + (size_t)B * knn_image_floats(C, N);
+    hipStream_t st = dgx_stream(stream);
+    switch (knn_nstep(C)) {
+        case 1: return launch_prepare<1>(x, sB, sC, sN, B, C, N, order, xx, img, xximg, st);
+        case 3: return launch_prepare<3>(x, sB, sC, sN, B, C, N, order, xx, img, xximg, st);
+        case 8: return launch_prepare<8>(x, sB, sC, sN, B, C, N, order, xx, img, xximg, st);
+        case 16: return launch_prepare<16>(x, sB, sC, sN, B, C, N, order, xx, img, xximg, st);
+        default: return launch_prepare<32>(x, sB, sC, sN, B, C, N, order, xx, img, xximg, st);
+    }
+}
+
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                       int k, int64_t* idx64, int32_t* idx32, float* vals, void* image, size_t image_bytes,
+                       int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes,
                        void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
     if (B == 0) return DGX_OK;
     if (!image || image_bytes < dgx_knn_image_bytes(B, C, N)) return DGX_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(image) & 15) != 0) return DGX_EINVAL;  // 16-byte operand loads
-    float* img = static_cast<float*>(image);
-    float* xximg = img + (size_t)B * knn_image_floats(C, N);
+    if ((reinterpret_cast<uintptr_t>(image) & 15) != 0) return DGX_EINVAL;
+    const float* img = static_cast<const float*>(image);
+    const float* xximg = img + (size_t)B * knn_image_floats(C, N);
     hipStream_t st = dgx_stream(stream);
     switch (knn_nstep(C)) {
         case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
@@ -702,12 +739,11 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C
     if (workspace_bytes < dgx_knn_workspace_bytes(B, C, N) || !workspace) return DGX_EINVAL;
     if (B == 0) return DGX_OK;
     float* xx = static_cast<float*>(workspace);
-    // image after xx, rounded up to 16 bytes
-    const size_t off = ((size_t)B * N + 3) & ~(size_t)3;
-    int rc = dgx_sqnorm_f32(x, sB, sC, sN, B, C, N, order, xx, stream);
+    float* image = xx + (((size_t)B * N + 3) & ~(size_t)3);  // 16-byte aligned after xx
+    const size_t ib = dgx_knn_image_bytes(B, C, N);
+    int rc = dgx_knn_prepare_f32(x, sB, sC, sN, B, C, N, order, xx, image, ib, stream);
     if (rc != DGX_OK) return rc;
-    return dgx_knn_select_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, nullptr, xx + off,
-                              dgx_knn_image_bytes(B, C, N), stream);
+    return dgx_knn_select_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, nullptr, image, ib, stream);
 }
 
 }  // extern "C"

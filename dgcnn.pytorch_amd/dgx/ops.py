@@ -46,7 +46,9 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     img = torch.empty((max(img_bytes, 4) + 3) // 4, dtype=torch.float32, device=x.device)  # operand image scratch
     stream = nat.stream_of(x)
     with torch.cuda.device(x.device):
-        nat.check(L.dgx_sqnorm_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx), stream), "sqnorm")
+        # |x|^2 and the MFMA operand image in one pass over x
+        nat.check(L.dgx_knn_prepare_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx), nat.ptr(img),
+                                        img_bytes, stream), "knn prepare")
         rec = _timing is not None
         if rec:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

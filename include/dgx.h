@@ -57,19 +57,23 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                 int64_t* idx64, int32_t* idx32,
                 void* workspace, size_t workspace_bytes, void* stream);
 
-/* The two stages of dgx_knn_f32, separately: |x_i|^2 in the reference's
- * rounding order into xx (B*N fp32, dgcnn.py:8), then the fused distance +
- * top-k pass given xx (dgcnn.py:7-11); vals (B,N,k), nullable, receives the
- * selected pd values (what pd.topk(k)[0] would hold). `image` (16-byte
- * aligned, dgx_knn_image_bytes(B,C,N)) is scratch for the MFMA operand image
- * the selection pass streams its candidates from. */
+/* The stages of dgx_knn_f32, separately. dgx_sqnorm_f32: |x_i|^2 in the
+ * reference's rounding order into xx (B*N fp32, dgcnn.py:8).
+ * dgx_knn_prepare_f32: the same xx plus the MFMA operand image of x in
+ * `image` (16-byte aligned, dgx_knn_image_bytes(B,C,N)) in one pass over x.
+ * dgx_knn_select_f32: the fused distance + top-k pass (dgcnn.py:7-11) over a
+ * prepared image and its xx; vals (B,N,k), nullable, receives the selected pd
+ * values (what pd.topk(k)[0] would hold). */
 size_t dgx_knn_image_bytes(int B, int C, int N);
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                    int B, int C, int N, int order, float* xx, void* stream);
+int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
+                        int B, int C, int N, int order, float* xx,
+                        void* image, size_t image_bytes, void* stream);
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                        const float* xx, int B, int C, int N, int k,
                        int64_t* idx64, int32_t* idx32, float* vals,
-                       void* image, size_t image_bytes, void* stream);
+                       const void* image, size_t image_bytes, void* stream);
 
 /* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
  * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in

@@ -132,3 +132,29 @@ def test_knn_all_points_equal(cuda):
     idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
     np.testing.assert_array_equal(idx, oracle.knn(_cpu_view(pts, "perm"), 20))
     np.testing.assert_array_equal(idx[0, 7], np.arange(20))
+
+
+@pytest.mark.parametrize("B,C,N", [(2, 3, 77), (1, 9, 1000), (2, 64, 1024), (1, 100, 257), (1, 128, 520)])
+@pytest.mark.parametrize("layout", ["bcn", "perm"])
+def test_knn_prepare_norms_match_sqnorm(cuda, B, C, N, layout):
+    """dgx_knn_prepare_f32's fused |x|^2 is bit-identical to dgx_sqnorm_f32 (and
+    to the oracle's restatement of the reference's reduction order)."""
+    from dgx import _native as nat
+    from dgx.ops import reduction_order
+    pts = synth.relu_normal(B * 7 + C + N, (B, N, C))
+    x = _view(pts, layout, cuda)
+    L = nat.lib()
+    sB, sC, sN = x.stride()
+    order = reduction_order(x)
+    xx0 = torch.empty(B * N, dtype=torch.float32, device=cuda)
+    xx1 = torch.full((B * N,), float("nan"), dtype=torch.float32, device=cuda)
+    nb = L.dgx_knn_image_bytes(B, C, N)
+    img = torch.empty((nb + 3) // 4, dtype=torch.float32, device=cuda)
+    s = nat.stream_of(x)
+    nat.check(L.dgx_sqnorm_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx0), s), "sqnorm")
+    nat.check(L.dgx_knn_prepare_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx1), nat.ptr(img), nb, s),
+              "prepare")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(xx0.cpu().numpy().view(np.uint32), xx1.cpu().numpy().view(np.uint32))
+    ref = oracle.sqnorm(_cpu_view(pts, layout)).reshape(-1)
+    np.testing.assert_array_equal(xx1.cpu().numpy().view(np.uint32), ref.astype(np.float32).view(np.uint32))
