@@ -539,16 +539,31 @@ int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int 
 // (the GEMM's B for X W^T), `tn` = its transpose (the B for dY W). For an
 // EdgeConv weight W (Co, 2C) (reference conv weight, dgcnn.py:55) the rows are
 // the stacked halves [W1; W2] (2Co, C); for conv5 W (Co, K) as is.
+// 64 x 64 tiles through LDS, so both the row-major copy and the transpose are
+// written with coalesced (row-contiguous) stores.
+constexpr int WP_T = 64;
 __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ W, int Co, int C, int stacked,
                                                           bf16* __restrict__ nt, bf16* __restrict__ tn) {
+    __shared__ bf16 tile[WP_T][WP_T + 2];
     const int rows = stacked ? 2 * Co : Co;
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= rows * C) return;
-    const int r = e / C, c = e - r * C;
-    const float v = stacked ? W[(r % Co) * 2 * C + (r / Co) * C + c] : W[r * C + c];
-    const bf16 h = (bf16)v;
-    nt[e] = h;
-    tn[c * rows + r] = h;
+    const int r0 = blockIdx.y * WP_T, c0 = blockIdx.x * WP_T;
+    const int t = threadIdx.x;
+    for (int e = t; e < WP_T * WP_T; e += 256) {
+        const int rr = e / WP_T, cc = e - rr * WP_T;
+        const int r = r0 + rr, c = c0 + cc;
+        if (r < rows && c < C) {
+            const float v = stacked ? W[(int64_t)(r % Co) * 2 * C + (r / Co) * C + c] : W[(int64_t)r * C + c];
+            const bf16 h = (bf16)v;
+            nt[(int64_t)r * C + c] = h;
+            tile[rr][cc] = h;
+        }
+    }
+    __syncthreads();
+    for (int e = t; e < WP_T * WP_T; e += 256) {
+        const int cc = e / WP_T, rr = e - cc * WP_T;
+        const int r = r0 + rr, c = c0 + cc;
+        if (r < rows && c < C) tn[(int64_t)c * rows + r] = tile[rr][cc];
+    }
 }
 
 template <typename TA, bool AIC, typename TB, bool BIC, int BN, int EPI>
@@ -654,9 +669,10 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
 
 int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt, void* tn, void* stream) {
     if (!W || !nt || !tn || Co < 1 || C < 1) return DGX_EINVAL;
-    const int total = (stacked ? 2 * Co : Co) * C;
-    hipLaunchKernelGGL(weight_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, dgx_stream(stream), W,
-                       Co, C, stacked, static_cast<bf16*>(nt), static_cast<bf16*>(tn));
+    const int rows = stacked ? 2 * Co : Co;
+    const dim3 grid((unsigned)((C + WP_T - 1) / WP_T), (unsigned)((rows + WP_T - 1) / WP_T));
+    hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, dgx_stream(stream), W, Co, C, stacked,
+                       static_cast<bf16*>(nt), static_cast<bf16*>(tn));
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

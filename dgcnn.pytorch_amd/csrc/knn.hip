@@ -170,7 +170,8 @@ template <int NSTEP>
 __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
                                                         int64_t sN, int B, int C, int N, int order, int ntile,
                                                         int tgroups, float* __restrict__ xx,
-                                                        float* __restrict__ img, float* __restrict__ xximg) {
+                                                        float* __restrict__ img, float* __restrict__ xximg,
+                                                        int* __restrict__ ctl) {
 #pragma clang fp contract(off)
     constexpr int CP = NSTEP * 4;
     constexpr int P = 16 * KI_TILES;
@@ -180,6 +181,7 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
     const int s0 = (blockIdx.x - b * tgroups) * KI_TILES;
     const int t = threadIdx.x;
     const float* __restrict__ xb = x + b * sB;
+    if (blockIdx.x == 0 && t < 2) ctl[t] = 0;  // empty fix-up list for the selection that follows
     for (int e = t; e < P * CP; e += 256) {
         int p, c;
         if (sN == 1) { c = e / P; p = e - c * P; }   // candidate-fastest: unit stride along n
@@ -255,7 +257,8 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
                                                          const float* __restrict__ xximg,
                                                          const float* __restrict__ xx, int B, int N, int k,
                                                          int nqb, int64_t* __restrict__ idx64,
-                                                         int32_t* __restrict__ idx32, float* __restrict__ vals) {
+                                                         int32_t* __restrict__ idx32, float* __restrict__ vals,
+                                                         int* __restrict__ ctl) {
 #pragma clang fp contract(off)
     constexpr int KL = KnnList<KB>::KL;
     constexpr int RPL = KnnList<KB>::RPL;
@@ -485,6 +488,7 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     __syncthreads();
     if (q < N) {
         const bool flag = flg[qq] != 0;
+        if (flag && h == 0 && g == 0) ctl[4 + atomicAdd(ctl, 1)] = b * N + q;  // fix-up list
         const int64_t row = ((int64_t)b * N + q) * k;
 #pragma unroll
         for (int t = 0; t < RPL; ++t) {
@@ -502,8 +506,9 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
 }
 
 // Exact recompute of the rows knn_kernel flagged (rank 0 = -1, rank 1 = the
-// bits of T0, the merged k-th value: at least k candidates reach T0). One block
-// per 256 consecutive rows scans their markers; for each flagged row the block
+// bits of T0, the merged k-th value: at least k candidates reach T0). knn_kernel
+// appends flagged rows to a list in the workspace (ctl[0] = count, rows from
+// ctl[4]); FIX_BLOCKS blocks take its rows round-robin; for each one a block
 // recomputes all N distances (the same k-ordered fmaf chain the MFMA performs,
 // the same rounding sequence), collects the candidates >= T0 (normally k plus
 // the few the overflowing list dropped) and ranks them canonically in one
@@ -513,31 +518,23 @@ constexpr int FIX_MAXN = 12288;
 constexpr int FIX_CB = 16;    // channels loaded per batch (loads in flight)
 constexpr int FIX_CAP = 1024;
 
+constexpr int FIX_BLOCKS = 64;
+
 __global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
                                                       int64_t sN, const float* __restrict__ xx, int B, int C,
                                                       int N, int k, int64_t* __restrict__ idx64,
-                                                      int32_t* __restrict__ idx32, float* __restrict__ vals) {
+                                                      int32_t* __restrict__ idx32, float* __restrict__ vals,
+                                                      int* __restrict__ ctl) {
 #pragma clang fp contract(off)
     __shared__ float pd[FIX_MAXN];
     __shared__ float cv[FIX_CAP];
     __shared__ int cj[FIX_CAP];
     __shared__ float xq[128];
-    __shared__ int rows[256];
-    __shared__ int nrows, ncand;
+    __shared__ int ncand;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t total = (int64_t)B * N;
-    const int64_t r0 = (int64_t)blockIdx.x * 256;
-    if (tid == 0) nrows = 0;
-    __syncthreads();
-    if (r0 + tid < total) {
-        const int64_t at = (r0 + tid) * k;
-        const bool flagged = idx64 ? idx64[at] < 0 : idx32[at] < 0;
-        if (flagged) rows[atomicAdd(&nrows, 1)] = tid;
-    }
-    __syncthreads();
-    const int nr = nrows;
-    for (int i = 0; i < nr; ++i) {
-        const int64_t row = r0 + rows[i];
+    const int nr = ctl[0];  // rows knn_kernel appended to the list
+    for (int i = blockIdx.x; i < nr; i += gridDim.x) {
+        const int64_t row = ctl[4 + i];
         const int b = (int)(row / N), q = (int)(row - (int64_t)b * N);
         const float* __restrict__ xb = x + b * sB;
         const float* __restrict__ xxb = xx + (int64_t)b * N;
@@ -620,15 +617,28 @@ __global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ 
         }
         __syncthreads();
     }
+    // the last block out resets the list for the next selection on this workspace
+    if (tid == 0) {
+        __threadfence();
+        if (atomicAdd(&ctl[1], 1) == (int)gridDim.x - 1) {
+            ctl[0] = 0;
+            ctl[1] = 0;
+        }
+    }
 }
+
+// image floats per cloud, then |x|^2 image floats per cloud
+inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
+inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
 
 template <int NSTEP>
 int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,
                    float* img, float* xximg, hipStream_t st) {
     const int ntile = knn_ntile(N);
     const int tgroups = (ntile + KI_TILES - 1) / KI_TILES;
+    int* ctl = reinterpret_cast<int*>(xximg + (size_t)B * knn_xximg_floats(N));
     hipLaunchKernelGGL(knn_image_kernel<NSTEP>, dim3((unsigned)(B * tgroups)), dim3(256), 0, st, x, sB, sC, sN, B, C,
-                       N, order, ntile, tgroups, xx, img, xximg);
+                       N, order, ntile, tgroups, xx, img, xximg, ctl);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -637,14 +647,14 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
                hipStream_t st) {
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
+    int* ctl = const_cast<int*>(reinterpret_cast<const int*>(xximg + (size_t)B * knn_xximg_floats(N)));
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
-                       xximg, xx, B, N, k, nqb, idx64, idx32, vals);
+                       xximg, xx, B, N, k, nqb, idx64, idx32, vals, ctl);
     if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH;
     static const bool nofix = getenv("DGX_KNN_NOFIX") != nullptr;  // diagnostics: leave flagged rows marked
     if (nofix) return DGX_OK;
-    const int64_t rows = (int64_t)B * N;
-    hipLaunchKernelGGL(knn_fix_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, x, sB, sC, sN, xx,
-                       B, C, N, k, idx64, idx32, vals);
+    hipLaunchKernelGGL(knn_fix_kernel, dim3(FIX_BLOCKS), dim3(256), 0, st, x, sB, sC, sN, xx, B, C, N, k, idx64,
+                       idx32, vals, ctl);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -660,10 +670,6 @@ int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
     DGX_KNN_K(64);
 #undef DGX_KNN_K
 }
-
-// image floats per cloud, then |x|^2 image floats per cloud
-inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
-inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
 
 }  // namespace
 
@@ -682,7 +688,8 @@ int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
 
 size_t dgx_knn_image_bytes(int B, int C, int N) {
     if (B < 0 || C < 1 || N < 1) return 0;
-    return (size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) * sizeof(float);
+    // operand image | |x|^2 image | fix-up control words + row list
+    return ((size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) + 4 + (size_t)B * N) * sizeof(float);
 }
 
 size_t dgx_knn_workspace_bytes(int B, int C, int N) {
