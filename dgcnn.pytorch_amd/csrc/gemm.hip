@@ -381,12 +381,12 @@ __device__ __forceinline__ bf16x8 frag_tn(const bf16* img, int s, int col0, int 
     return __builtin_bit_cast(bf16x8, v);
 }
 
-template <bool TN, int BN, int EPI>
+template <bool TN, int BM, int BN, int EPI>
 __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
     int kchunk, float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend,
     int64_t ldd) {
-    constexpr int BM = G2_BM;
+    static_assert(BM == G2_BM || (EPI != EPI_STATS && EPI != EPI_STATS16), "stats rows are per 128-row tile");
     constexpr int WN = BN >= 128 ? 2 : 1;
     constexpr int WM = 4 / WN;
     constexpr int TM = BM / WM / 16;
@@ -525,13 +525,29 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
 template <bool TN, int BN, int EPI>
 int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int M, int N, int K, int splits,
                     float* C, int64_t ldc, float* part, const float* addend, int64_t ldd, hipStream_t st) {
-    const int nI = (M + G2_BM - 1) / G2_BM, nJ = (N + BN - 1) / BN;
     int kchunk = (K + splits - 1) / splits;
     kchunk = (kchunk + G2_BK - 1) / G2_BK * G2_BK;
     const int sp = (K + kchunk - 1) / kchunk;
-    dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
-    hipLaunchKernelGGL((gemm_lds_kernel<TN, BN, EPI>), grid, dim3(GB_THREADS), 0, st, A, lda, B, ldb, M, N, K,
-                       EPI == EPI_SLAB ? kchunk : K, C, ldc, part, addend, ldd);
+    const int nJ = (N + BN - 1) / BN;
+    // skinny outputs (few 128-row tiles): 64-row tiles double the workgroups so
+    // two share each CU and hide each other's load latency
+    constexpr bool can_half = EPI != EPI_STATS && EPI != EPI_STATS16;
+    const bool half = can_half && ((M + G2_BM - 1) / G2_BM) * nJ * sp < 512;
+    if constexpr (can_half) {
+        if (half) {
+            const int nI = (M + 63) / 64;
+            dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
+            hipLaunchKernelGGL((gemm_lds_kernel<TN, 64, BN, EPI>), grid, dim3(GB_THREADS), 0, st, A, lda, B, ldb, M,
+                               N, K, EPI == EPI_SLAB ? kchunk : K, C, ldc, part, addend, ldd);
+            return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+        }
+    }
+    {
+        const int nI = (M + G2_BM - 1) / G2_BM;
+        dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
+        hipLaunchKernelGGL((gemm_lds_kernel<TN, G2_BM, BN, EPI>), grid, dim3(GB_THREADS), 0, st, A, lda, B, ldb, M,
+                           N, K, EPI == EPI_SLAB ? kchunk : K, C, ldc, part, addend, ldd);
+    }
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
