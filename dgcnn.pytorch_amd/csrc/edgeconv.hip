@@ -423,6 +423,27 @@ __global__ void bn_lrelu_apply_kernel(const float* __restrict__ ysel, int M, int
     }
 }
 
+// 4 channels per thread (Co, ldo multiples of 4): 16-byte loads and stores,
+// 8-byte bf16 twin stores.
+__global__ void bn_lrelu_apply4_kernel(const float* __restrict__ ysel, int M, int Co,
+                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                       float slope, float* __restrict__ out, int ldo, __bf16* __restrict__ out16) {
+    const int cq = Co >> 2;
+    const int64_t total = (int64_t)M * cq;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int o = (int)(t % cq) * 4;
+        const int64_t i = t / cq;
+        const float4 y = *reinterpret_cast<const float4*>(ysel + i * Co + o);
+        const float4 a = *reinterpret_cast<const float4*>(scale + o);
+        const float4 b = *reinterpret_cast<const float4*>(shift + o);
+        float v[4] = {lrelu(fmaf(a.x, y.x, b.x), slope), lrelu(fmaf(a.y, y.y, b.y), slope),
+                      lrelu(fmaf(a.z, y.z, b.z), slope), lrelu(fmaf(a.w, y.w, b.w), slope)};
+        gst_vec<4>(out + i * ldo + o, v);
+        if (out16) gst_bf16<4>(out16 + i * ldo + o, v);
+    }
+}
+
 // ------------------------------------------------------------ backward -----
 // dz at the selected edge (packed with its slot) and per-row-block partial
 // (sum dz, sum dz*yhat). grid (nrows, ceil(Co/64)).
@@ -1017,8 +1038,15 @@ int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
     if (!ysel || !scale || !shift || !out || M < 0 || Co < 1 || ldo < Co) return DGX_EINVAL;
     const int64_t total = (int64_t)M * Co;
     if (total == 0) return DGX_OK;
-    hipLaunchKernelGGL(bn_lrelu_apply_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), ysel, M,
-                       Co, scale, shift, slope, out, ldo, static_cast<__bf16*>(out_bf16));
+    const bool v4 = Co % 4 == 0 && ldo % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(ysel) % 16 == 0 && reinterpret_cast<uintptr_t>(scale) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(shift) % 16 == 0 && reinterpret_cast<uintptr_t>(out_bf16) % 8 == 0;
+    if (v4)
+        hipLaunchKernelGGL(bn_lrelu_apply4_kernel, dim3(grid_for(total / 4, 256)), dim3(256), 0, dgx_stream(stream),
+                           ysel, M, Co, scale, shift, slope, out, ldo, static_cast<__bf16*>(out_bf16));
+    else
+        hipLaunchKernelGGL(bn_lrelu_apply_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), ysel,
+                           M, Co, scale, shift, slope, out, ldo, static_cast<__bf16*>(out_bf16));
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

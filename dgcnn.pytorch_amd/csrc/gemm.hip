@@ -582,6 +582,45 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
     }
 }
 
+// Several weights in one launch (the EdgeConv blocks of one forward): job j
+// owns blocks [first[j], first[j+1]) of the 1-D grid, tiles row-major in it.
+constexpr int WP_MAXJ = 8;
+struct WeightPrepJobs {
+    const float* W[WP_MAXJ];
+    bf16* nt[WP_MAXJ];
+    bf16* tn[WP_MAXJ];
+    int Co[WP_MAXJ], C[WP_MAXJ], stacked[WP_MAXJ], first[WP_MAXJ + 1];
+    int n;
+};
+__global__ __launch_bounds__(256) void weight_prep_multi_kernel(WeightPrepJobs jobs) {
+    __shared__ bf16 tile[WP_T][WP_T + 2];
+    int j = 0;
+    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+    const int Co = jobs.Co[j], C = jobs.C[j], stacked = jobs.stacked[j];
+    const float* __restrict__ W = jobs.W[j];
+    const int rows = stacked ? 2 * Co : Co;
+    const int ntc = (C + WP_T - 1) / WP_T;
+    const int b = blockIdx.x - jobs.first[j];
+    const int r0 = (b / ntc) * WP_T, c0 = (b % ntc) * WP_T;
+    const int t = threadIdx.x;
+    for (int e = t; e < WP_T * WP_T; e += 256) {
+        const int rr = e / WP_T, cc = e - rr * WP_T;
+        const int r = r0 + rr, c = c0 + cc;
+        if (r < rows && c < C) {
+            const float v = stacked ? W[(int64_t)(r % Co) * 2 * C + (r / Co) * C + c] : W[(int64_t)r * C + c];
+            const bf16 h = (bf16)v;
+            jobs.nt[j][(int64_t)r * C + c] = h;
+            tile[rr][cc] = h;
+        }
+    }
+    __syncthreads();
+    for (int e = t; e < WP_T * WP_T; e += 256) {
+        const int cc = e / WP_T, rr = e - cc * WP_T;
+        const int r = r0 + rr, c = c0 + cc;
+        if (r < rows && c < C) jobs.tn[j][(int64_t)c * rows + r] = tile[rr][cc];
+    }
+}
+
 template <typename TA, bool AIC, typename TB, bool BIC, int BN, int EPI>
 int launch_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, int splits,
                 int vec_a, int vec_b, float* C, int64_t ldc, float* part, hipStream_t st) {
@@ -596,6 +635,47 @@ int launch_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, int M, i
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
+// Weight gradient with a narrow second operand (layer 1: dW = dPQ^T X, X has
+// 3 channels): C slab[y][i][j] = sum over k in split y of A[k][i] B[k][j], A bf16
+// (i contiguous), B fp32 rounded to bf16 like every operand of the bf16 GEMMs,
+// fp32 accumulation. One thread per output row i, the split's B rows staged in
+// LDS; the MFMA tile path would pad N to 64 columns (95 % idle at N = 3).
+constexpr int AS_ROWS = 256;
+template <int NB>
+__global__ __launch_bounds__(256) void atb_small_kernel(const bf16* __restrict__ A, int64_t lda,
+                                                        const float* __restrict__ B, int64_t ldb, int M, int N,
+                                                        int K, int kchunk, float* __restrict__ slab) {
+    __shared__ float bs[AS_ROWS][NB];
+    const int kbeg = blockIdx.x * kchunk, kend = min(K, kbeg + kchunk);
+    float* out = slab + (int64_t)blockIdx.x * M * N;
+    for (int i0 = 0; i0 < M; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        float acc[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = 0.f;
+        for (int k0 = kbeg; k0 < kend; k0 += AS_ROWS) {
+            const int nk = min(AS_ROWS, kend - k0);
+            __syncthreads();
+            for (int e = threadIdx.x; e < AS_ROWS * NB; e += 256) {
+                const int kk = e / NB, j = e - kk * NB;
+                bs[kk][j] = (kk < nk && j < N) ? (float)(bf16)B[(int64_t)(k0 + kk) * ldb + j] : 0.f;
+            }
+            __syncthreads();
+            if (i < M) {
+                const bf16* a = A + (int64_t)k0 * lda + i;
+#pragma unroll 8
+                for (int kk = 0; kk < nk; ++kk) {
+                    const float av = (float)a[(int64_t)kk * lda];
+#pragma unroll
+                    for (int j = 0; j < NB; ++j) acc[j] = fmaf(av, bs[kk][j], acc[j]);
+                }
+            }
+        }
+        if (i < M)
+            for (int j = 0; j < N; ++j) out[(int64_t)i * N + j] = acc[j];
+    }
+}
+
 bool aligned_to(const void* p, int bytes) { return (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
 
 }  // namespace
@@ -607,6 +687,10 @@ int dgx_gemm_stats_rows(int M) { return (M + GB_BM - 1) / GB_BM; }
 int dgx_gemm_splits(int M, int N, int K) {
     // split-K factor of a SLAB GEMM: about 2 workgroups per CU (256 CUs), each
     // split at least 8 K-steps deep
+    if (N <= 4) {  // atb_small_kernel: one block per split, 64+ rows each, ~2 blocks per CU
+        const int s = (K + 63) / 64;
+        return s < 1 ? 1 : (s > 512 ? 512 : s);
+    }
     const int BN = N > 64 ? 128 : 64;
     const int tiles = ((M + GB_BM - 1) / GB_BM) * ((N + BN - 1) / BN);
     int s = (512 + tiles - 1) / tiles;
@@ -645,6 +729,14 @@ int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda, const void* 
         if (a_bf16 && epi == EPI_STORE) DGX_GEMM(bf16, false, float, true, EPI_STORE);
     }
     if (a_ic && b_ic && !b_bf16 && epi == EPI_SLAB) {  // dPQ^T X / dZ^T X: weight gradients
+        if (a_bf16 && N <= 4) {  // same split geometry (kchunk, slab count) as launch_gemm
+            int kchunk = (K + splits - 1) / splits;
+            kchunk = (kchunk + GB_BK - 1) / GB_BK * GB_BK;
+            const int sp = (K + kchunk - 1) / kchunk;
+            hipLaunchKernelGGL(atb_small_kernel<4>, dim3((unsigned)sp), dim3(256), 0, st, static_cast<const bf16*>(A),
+                               lda, static_cast<const float*>(B), ldb, M, N, K, kchunk, C);
+            return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+        }
         if (a_bf16) DGX_GEMM(bf16, true, float, true, EPI_SLAB);
         DGX_GEMM(float, true, float, true, EPI_SLAB);
     }
@@ -689,6 +781,29 @@ int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt, v
     const dim3 grid((unsigned)((C + WP_T - 1) / WP_T), (unsigned)((rows + WP_T - 1) / WP_T));
     hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, dgx_stream(stream), W, Co, C, stacked,
                        static_cast<bf16*>(nt), static_cast<bf16*>(tn));
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, const int* C, const int* stacked,
+                               void* const* nt, void* const* tn, void* stream) {
+    if (n < 1 || n > WP_MAXJ || !W || !Co || !C || !stacked || !nt || !tn) return DGX_EINVAL;
+    WeightPrepJobs jobs = {};
+    jobs.n = n;
+    int blocks = 0;
+    for (int j = 0; j < n; ++j) {
+        if (!W[j] || !nt[j] || !tn[j] || Co[j] < 1 || C[j] < 1) return DGX_EINVAL;
+        jobs.W[j] = W[j];
+        jobs.nt[j] = static_cast<bf16*>(nt[j]);
+        jobs.tn[j] = static_cast<bf16*>(tn[j]);
+        jobs.Co[j] = Co[j];
+        jobs.C[j] = C[j];
+        jobs.stacked[j] = stacked[j];
+        jobs.first[j] = blocks;
+        const int rows = stacked[j] ? 2 * Co[j] : Co[j];
+        blocks += ((rows + WP_T - 1) / WP_T) * ((C[j] + WP_T - 1) / WP_T);
+    }
+    jobs.first[n] = blocks;
+    hipLaunchKernelGGL(weight_prep_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, dgx_stream(stream), jobs);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

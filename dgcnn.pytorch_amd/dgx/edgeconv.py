@@ -78,6 +78,12 @@ class _EdgeConvStack(torch.autograd.Function):
         off_in = None
         count = float(M * k)
         have16 = False  # xcat16 holds the previous block's output
+        # bf16 [W1;W2] and transposed copies of blocks 2.. in one launch (used when
+        # the block's input is the bf16 twin, i.e. after a batch-statistics block)
+        preps = [None] * len(layers)
+        if bf16 and len(layers) > 1:
+            jobs = [(params[3 * li], ly.cout, ly.cin, True) for li, ly in enumerate(layers) if li > 0]
+            preps[1:] = G.prep_weights(jobs)
         for li, ly in enumerate(layers):
             w, gamma, beta = params[3 * li: 3 * li + 3]
             cin, co = ly.cin, ly.cout
@@ -95,7 +101,7 @@ class _EdgeConvStack(torch.autograd.Function):
                 X16 = xcat16[:, off_in:off_in + cin] if li > 0 else None
                 if have16 and G.lds_ok_nt(X16, cin):
                     # bf16 operands by LDS-DMA; the weight's bf16 [W1;W2] and transpose serve fwd and bwd
-                    wprep = G.prep_weight(w, co, cin, True)
+                    wprep = preps[li]
                     PQ = G.lds_xwt(X16, wprep[0])
                 else:
                     PQ = G.mm_xwt(X, _split_weight(w, cin, co))  # fp32 operands rounded while staged

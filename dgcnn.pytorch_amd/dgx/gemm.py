@@ -196,6 +196,40 @@ def prep_weight(w, rows, cols, stacked):
     return nt, tn
 
 
+def prep_weights(jobs):
+    """prep_weight for several (w, rows, cols, stacked) jobs in one launch; the
+    bf16 copies share one allocation. Returns [(nt, tn), ...]."""
+    import ctypes
+    if not jobs:
+        return []
+    dev = jobs[0][0].device
+    sizes = [(2 * r if st else r) * c for (_, r, c, st) in jobs]
+    pad = [-(-n // 8) * 8 for n in sizes]  # 16-byte aligned views
+    buf = torch.empty(2 * sum(pad), dtype=torch.bfloat16, device=dev)
+    out, off = [], 0
+    for (w, r, c, st), n, p_ in zip(jobs, sizes, pad):
+        R = 2 * r if st else r
+        nt = buf[off:off + n].view(R, c)
+        tn = buf[off + p_:off + p_ + n].view(c, R)
+        off += 2 * p_
+        out.append((nt, tn))
+    n = len(jobs)
+    P = ctypes.c_void_p * n
+    I = ctypes.c_int * n
+    # host arrays kept in locals for the duration of the call
+    W = P(*[w.data_ptr() for (w, _, _, _) in jobs])
+    NT = P(*[o[0].data_ptr() for o in out])
+    TN = P(*[o[1].data_ptr() for o in out])
+    CO = I(*[r for (_, r, _, _) in jobs])
+    CI = I(*[c for (_, _, c, _) in jobs])
+    ST = I(*[int(st) for (_, _, _, st) in jobs])
+    with torch.cuda.device(dev):
+        nat.check(nat.lib().dgx_weight_prep_multi_bf16(
+            n, ctypes.addressof(W), ctypes.addressof(CO), ctypes.addressof(CI), ctypes.addressof(ST),
+            ctypes.addressof(NT), ctypes.addressof(TN), nat.stream_of(jobs[0][0])), "weight prep")
+    return out
+
+
 def lds_ok_nt(x, K):
     """Whether the DMA path takes this k-contiguous operand (else the register-staged kernel)."""
     return x.dtype == torch.bfloat16 and K % 64 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0

@@ -248,6 +248,10 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
  * [W1; W2]; else W is (Co, C) (conv5, dgcnn.py:74). */
 int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt,
                          void* tn, void* stream);
+/* dgx_weight_prep_bf16 for n <= 8 weights in one launch (host arrays of
+ * length n: one job per EdgeConv block of a forward). */
+int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, const int* C, const int* stacked,
+                               void* const* nt, void* const* tn, void* stream);
 
 #ifdef __cplusplus
 }

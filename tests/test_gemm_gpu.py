@@ -72,7 +72,7 @@ def test_xw_store_and_accumulate(cuda, a_dtype, M, N, K):
 
 @pytest.mark.parametrize("a_dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("R,M,N", [(32768, 1024, 512), (32768, 512, 128), (5000, 128, 64), (999, 128, 3),
-                                   (64, 40, 20)])
+                                   (64, 40, 20), (32768, 128, 3), (2048, 600, 4), (77, 300, 1)])
 def test_atb_split_k(cuda, a_dtype, R, M, N):
     from dgx import gemm as G
     torch.manual_seed(R + M)
@@ -187,3 +187,15 @@ def test_weight_prep(cuda, co, c, stacked):
     exp = torch.cat([w2[:, :c], w2[:, c:]], dim=0) if stacked else w2
     assert torch.equal(nt, exp.to(torch.bfloat16))
     assert torch.equal(tn, exp.t().contiguous().to(torch.bfloat16))
+
+
+def test_weight_prep_multi(cuda):
+    """The batched launch the EdgeConv forward uses equals per-weight prep."""
+    from dgx import gemm as G
+    torch.manual_seed(5)
+    shapes = [(64, 64, True), (128, 64, True), (256, 128, True), (40, 24, False)]
+    ws = [torch.randn(co, 2 * c if st else c, 1, 1, device=cuda) for (co, c, st) in shapes]
+    got = G.prep_weights([(w, co, c, st) for w, (co, c, st) in zip(ws, shapes)])
+    for w, (co, c, st), (nt, tn) in zip(ws, shapes, got):
+        ent, etn = G.prep_weight(w, co, c, st)
+        assert torch.equal(nt, ent) and torch.equal(tn, etn)
