@@ -300,6 +300,77 @@ __global__ __launch_bounds__(256) void bwd16_kernel(const float* __restrict__ do
     }
 }
 
+// PASS 0 over RS_LOOPS consecutive 128-point tiles per block: the per-channel
+// sums stay in registers across the tiles and are reduced once, so the
+// shuffle/LDS reduction is amortised over 4x the elements (pass 0 reads the
+// same bytes as pass 1 but writes nothing, so its cost was the reduction).
+constexpr int RS_LOOPS = 4;
+__global__ __launch_bounds__(256) void bwd16_stats_kernel(const float* __restrict__ dout, const bf16* __restrict__ Z,
+                                                          int N, int C, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, float slope,
+                                                          float* __restrict__ partials) {
+    __shared__ float red[2][4][64];
+    const int nt = (N + RT_P * RS_LOOPS - 1) / (RT_P * RS_LOOPS);
+    const int b = blockIdx.x / nt;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nb = (blockIdx.x - b * nt) * RT_P * RS_LOOPS + w * 32 + (lane >> 3) * 4;
+    const int o = blockIdx.y * 64 + (lane & 7) * 8;
+    float a[8], sh[8], mu[8], is[8], s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int oj = o + j < C ? o + j : 0;
+        a[j] = scale[oj];
+        sh[j] = shift[oj];
+        mu[j] = mean[oj];
+        is[j] = invstd[oj];
+        s1[j] = 0.f;
+        s2[j] = 0.f;
+    }
+#pragma unroll 1
+    for (int it = 0; it < RS_LOOPS; ++it) {
+        const int n = nb + it * RT_P;
+        if (n >= N) break;
+        float z[4][8], g[8][4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float4 v = load_row4(dout, ((int64_t)b * C + o + j) * N, n, N, o + j < C);
+            g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) load_z8(Z, (int64_t)b * N + n + i, C, o, n + i < N, z[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float d = g[j][i] * (fmaf(a[j], z[i][j], sh[j]) > 0.f ? 1.f : slope);
+                s1[j] += d;
+                s2[j] = fmaf(d, (z[i][j] - mu[j]) * is[j], s2[j]);
+            }
+        }
+    }
+    // lanes of one channel group: l, l^8, l^16, l^32 in the wave, then the 4 waves
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int m = 8; m < 64; m <<= 1) {
+            s1[j] += __shfl_xor(s1[j], m);
+            s2[j] += __shfl_xor(s2[j], m);
+        }
+    }
+    if (lane < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { red[0][w][lane * 8 + j] = s1[j]; red[1][w][lane * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+    const int t = threadIdx.x, o0 = blockIdx.y * 64;
+    if (t < 64 && o0 + t < C) {
+        partials[(int64_t)blockIdx.x * 2 * C + o0 + t] = ((red[0][0][t] + red[0][1][t]) + red[0][2][t]) + red[0][3][t];
+        partials[(int64_t)blockIdx.x * 2 * C + C + o0 + t] = ((red[1][0][t] + red[1][1][t]) + red[1][2][t]) + red[1][3][t];
+    }
+}
+
 inline int grid_for(int64_t total, int block) {
     int64_t g = (total + block - 1) / block;
     return (int)(g < 16384 ? (g < 1 ? 1 : g) : 16384);
@@ -360,7 +431,7 @@ int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M
 
 int dgx_pointconv_bf16_rows(int B, int N) {
     if (B < 1 || N < 1) return DGX_EINVAL;
-    return B * ((N + RT_P - 1) / RT_P);
+    return B * ((N + RT_P * RS_LOOPS - 1) / (RT_P * RS_LOOPS));  // pass-0 partial rows
 }
 
 int dgx_pointconv_apply_bf16(const void* Z, int B, int N, int C, const float* scale, const float* shift, float slope,
@@ -380,8 +451,9 @@ int dgx_pointconv_bwd_bf16(const float* dout, const void* Z, int B, int N, int C
     dim3 grid(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64);
     const bf16* z = static_cast<const bf16*>(Z);
     if (pass == 0)
-        hipLaunchKernelGGL(bwd16_kernel<0>, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean,
-                           invstd, slope, c0, c1, partials, static_cast<bf16*>(dZ));
+        hipLaunchKernelGGL(bwd16_stats_kernel, dim3(B * ((N + RT_P * RS_LOOPS - 1) / (RT_P * RS_LOOPS)), (C + 63) / 64),
+                           dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean, invstd, slope,
+                           partials);
     else
         hipLaunchKernelGGL(bwd16_kernel<1>, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean,
                            invstd, slope, c0, c1, partials, static_cast<bf16*>(dZ));

@@ -192,7 +192,7 @@ int dgx_to_bf16(const float* src, int64_t ld, int64_t rows, int cols, void* dst,
  * accumulators — what autocast stores for a conv output).
  *   dgx_pointconv_apply_bf16: out (B,C,N) = LeakyReLU(scale*z + shift).
  *   dgx_pointconv_bwd_bf16 pass 0: partials[dgx_pointconv_bf16_rows(B,N)][2][C]
- *     = per 128-point tile (sum d, sum d*zhat), d = dout * LeakyReLU'(scale*z + shift), zhat =
+ *     = per 512-point tile (sum d, sum d*zhat), d = dout * LeakyReLU'(scale*z + shift), zhat =
  *     (z - mean) * invstd; -> dgx_bn_bwd_finalize_f32 -> c0, c1.
  *   pass 1: dZ (bf16, M x C) = scale*d + c0 + c1*z — the GEMM operand of
  *     dW5 = dZ^T X and dX = dZ W5. Replace the reference's autograd of
