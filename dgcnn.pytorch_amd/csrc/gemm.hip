@@ -470,31 +470,24 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
 
     float* out = C;
     if (EPI == EPI_SLAB) out = C + (int64_t)blockIdx.y * M * N;
-    const int rb = i0 + wm * TM * 16 + (lane >> 4) * 4;
-    const int cb = j0 + wn * TN_ * 16 + (lane & 15);
-    float s1[TN_], s2[TN_];
-#pragma unroll
-    for (int b = 0; b < TN_; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = rb + a * 16 + r;
-            if (i >= M) continue;
-#pragma unroll
-            for (int b = 0; b < TN_; ++b) {
-                const int j = cb + b * 16;
-                if (j >= N) continue;
-                const float v = acc[a][b][r];
-                float* dst = out + (int64_t)i * ldc + j;
-                if (EPI == EPI_ACCUM) *dst = (addend ? addend[(int64_t)i * ldd + j] : *dst) + v;
-                else if (EPI == EPI_STATS16) reinterpret_cast<bf16*>(out)[(int64_t)i * ldc + j] = (bf16)v;
-                else *dst = v;
-                if (EPI == EPI_STATS || EPI == EPI_STATS16) { s1[b] += v; s2[b] = fmaf(v, v, s2[b]); }
-            }
-        }
-    }
     if (EPI == EPI_STATS || EPI == EPI_STATS16) {
+        // BatchNorm column partials from the fp32 accumulators
+        const int cb = j0 + wn * TN_ * 16 + (lane & 15);
+        const int rb = i0 + wm * TM * 16 + (lane >> 4) * 4;
+        float s1[TN_], s2[TN_];
+#pragma unroll
+        for (int b = 0; b < TN_; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int b = 0; b < TN_; ++b) {
+                    const bool ok = rb + a * 16 + r < M && cb + b * 16 < N;
+                    const float v = ok ? acc[a][b][r] : 0.f;
+                    s1[b] += v;
+                    s2[b] = fmaf(v, v, s2[b]);
+                }
         float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
 #pragma unroll
         for (int b = 0; b < TN_; ++b) {
@@ -518,6 +511,70 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
             for (int w = 0; w < WM; ++w) { t1 += red[(w * BN + jl) * 2]; t2 += red[(w * BN + jl) * 2 + 1]; }
             part[(int64_t)ti * 2 * N + j] = t1;
             part[(int64_t)ti * 2 * N + N + j] = t2;
+        }
+    }
+
+    // Output through LDS: the fp32 tile goes row-major into the idle stage
+    // buffers (in NR row rounds when it does not fit at once), then each thread
+    // moves 16-byte row pieces (4 fp32 or 8 bf16 outputs per store) instead of
+    // scalar stores of 16-lane column fragments.
+    constexpr int LDT = BN + 4;
+    constexpr int LDSB = 2 * STAGE * (int)sizeof(bf16);
+    constexpr int NR = BM * LDT * 4 <= LDSB ? 1 : 2;
+    constexpr int RR = BM / NR;
+    static_assert(RR * LDT * 4 <= LDSB && WM % NR == 0, "epilogue tile must fit the stage buffers");
+    constexpr int VO = EPI == EPI_STATS16 ? 8 : 4;  // outputs per 16-byte store
+    constexpr int CPR = BN / VO;
+    float* tile = reinterpret_cast<float*>(lds);
+    const bool vec_out = (ldc % VO) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                         (EPI != EPI_ACCUM || !addend ||
+                          ((ldd % 4) == 0 && (reinterpret_cast<uintptr_t>(addend) & 15) == 0));
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        __syncthreads();  // K loop / stats / previous round done with the buffers
+        if (wm / (WM / NR) == q) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int b = 0; b < TN_; ++b)
+                        tile[(wm * TM * 16 - q * RR + a * 16 + (lane >> 4) * 4 + r) * LDT + wn * TN_ * 16 + b * 16 +
+                             (lane & 15)] = acc[a][b][r];
+        }
+        __syncthreads();
+        for (int e = tid; e < RR * CPR; e += GB_THREADS) {
+            const int rr = e / CPR, c = (e - rr * CPR) * VO;
+            const int i = i0 + q * RR + rr, j = j0 + c;
+            if (i >= M || j >= N) continue;
+            const float* src = tile + rr * LDT + c;
+            if (vec_out && j + VO <= N) {
+                if constexpr (EPI == EPI_STATS16) {
+                    const float4 u = *reinterpret_cast<const float4*>(src);
+                    const float4 w = *reinterpret_cast<const float4*>(src + 4);
+                    bf16x8 h = {(bf16)u.x, (bf16)u.y, (bf16)u.z, (bf16)u.w, (bf16)w.x, (bf16)w.y, (bf16)w.z, (bf16)w.w};
+                    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(out) + (int64_t)i * ldc + j) = h;
+                } else {
+                    float4 v = *reinterpret_cast<const float4*>(src);
+                    float4* dst = reinterpret_cast<float4*>(out + (int64_t)i * ldc + j);
+                    if (EPI == EPI_ACCUM) {
+                        const float4 o = addend ? *reinterpret_cast<const float4*>(addend + (int64_t)i * ldd + j) : *dst;
+                        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+                    }
+                    *dst = v;
+                }
+            } else {
+                for (int u = 0; u < VO && j + u < N; ++u) {
+                    const float v = src[u];
+                    if (EPI == EPI_STATS16) {
+                        reinterpret_cast<bf16*>(out)[(int64_t)i * ldc + j + u] = (bf16)v;
+                    } else {
+                        float* dst = out + (int64_t)i * ldc + j + u;
+                        if (EPI == EPI_ACCUM) *dst = (addend ? addend[(int64_t)i * ldd + j + u] : *dst) + v;
+                        else *dst = v;
+                    }
+                }
+            }
         }
     }
 }
