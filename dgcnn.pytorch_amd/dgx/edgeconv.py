@@ -17,6 +17,8 @@ Backward per block (reverse order):
     reverse kNN graph + dPQ                   HIP
     dX += dPQ [W1; W2], dW = dPQ^T X          GEMM (accumulated into xcat's grad)
 """
+import ctypes
+
 import torch
 
 from . import _native as nat
@@ -43,6 +45,44 @@ def _bn_factor(bn):
             return 1.0 / float(bn.num_batches_tracked.item()), None
         return 0.0, None
     return float(bn.momentum), bn.num_batches_tracked
+
+
+_side_streams = {}
+
+
+def _side_stream(dev):
+    """One auxiliary HIP stream per device for work that only feeds the backward."""
+    s = _side_streams.get(dev)
+    if s is None:
+        s = _side_streams[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def _reverse_graph_async(idx, B, N, k, side, dev):
+    """Reverse kNN graph (CSR of in-edges, dgx_graph_reverse) of one block.
+    With a side stream: launched there after the current stream's work up to
+    now (the kNN that produced idx), returning (rowptr, edges, ready_event);
+    the consumer waits on the event. Without: on the current stream."""
+    M = B * N
+    rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    edges = torch.empty(M * k, dtype=torch.int32, device=dev)
+    L = nat.lib()
+    if side is None:
+        with torch.cuda.device(dev):
+            nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
+                                          nat.stream_of(idx)), "reverse graph")
+        return rowptr, edges, None
+    main = torch.cuda.current_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.device(dev), torch.cuda.stream(side):
+        nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
+                                      ctypes.c_void_p(side.cuda_stream)), "reverse graph")
+        ready = torch.cuda.Event()
+        ready.record(side)
+    # allocator bookkeeping: these buffers are used on the side stream too
+    for t in (idx, rowptr, edges):
+        t.record_stream(side)
+    return rowptr, edges, ready
 
 
 class _Layer:
@@ -78,6 +118,11 @@ class _EdgeConvStack(torch.autograd.Function):
         off_in = None
         count = float(M * k)
         have16 = False  # xcat16 holds the previous block's output
+        # The backward's reverse kNN graphs depend only on each block's indices:
+        # they are built on a side stream as soon as the indices exist, so they
+        # overlap the rest of the forward (and conv5's backward).
+        want_bwd = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+        side = _side_stream(dev) if want_bwd and training else None
         # bf16 [W1;W2] and transposed copies of blocks 2.. in one launch (used when
         # the block's input is the bf16 twin, i.e. after a batch-statistics block)
         preps = [None] * len(layers)
@@ -96,6 +141,9 @@ class _EdgeConvStack(torch.autograd.Function):
                 # dim -1 of a contiguous tensor), hence the strided rounding order
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
                               strides=(N * total, 1, total), shape=(B, cin, N))
+            graph = None
+            if want_bwd and training:
+                graph = _reverse_graph_async(idx, B, N, k, side, dev)
             wprep = None
             if bf16:
                 X16 = xcat16[:, off_in:off_in + cin] if li > 0 else None
@@ -143,7 +191,8 @@ class _EdgeConvStack(torch.autograd.Function):
                                                        float(ly.slope), nat.ptr(out), total, nat.ptr(out16), stream),
                               "bn apply")
                     have16 = bf16
-                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group if sync else None))
+                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group if sync else None,
+                                  graph))
                     if _debug is not None:
                         # sign of fmaf(scale, ysel, shift) as the kernels evaluate it: the fp64
                         # product of two fp32 values is exact, so this sign is fma's sign
@@ -191,8 +240,6 @@ class _EdgeConvStack(torch.autograd.Function):
         grads = [None] * len(params)
         dx_in = None
         count = float(M * k)
-        rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
-        edges = torch.empty(M * k, dtype=torch.int32, device=dev)
         nl = len(layers)
         if bf16:
             # The incoming gradient stays read-only: block l's input gradient is written
@@ -206,7 +253,12 @@ class _EdgeConvStack(torch.autograd.Function):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
             w = params[3 * li]
-            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group = ctx.layer_state[li]
+            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group, graph = ctx.layer_state[li]
+            if graph is None:  # forward ran without a pending backward (e.g. under no_grad + enable_grad)
+                graph = _reverse_graph_async(idx, B, N, k, None, dev)
+            rowptr, edges, ready = graph
+            if ready is not None:
+                torch.cuda.current_stream(dev).wait_event(ready)
             off = sum(widths[:li])
             prev = off - widths[li - 1] if li > 0 else None
             X = x_pm if li == 0 else xcat[:, prev: prev + cin]
@@ -241,8 +293,6 @@ class _EdgeConvStack(torch.autograd.Function):
                         None, None, nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
                     dbeta.copy_(loc[0])
                     dgamma.copy_(loc[1])
-                nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges), stream),
-                          "reverse graph")
                 nat.check(L.dgx_edge_bwd_scatter_f32(
                     nat.ptr(PQ), 2 * co, nat.ptr(rowptr), nat.ptr(edges), nat.ptr(dz), nat.ptr(sumP), B, N, k, co,
                     nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), int(bf16), stream), "edge bwd scatter")
