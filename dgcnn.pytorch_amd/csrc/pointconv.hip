@@ -143,37 +143,11 @@ __global__ void to_bf16_kernel(const float* __restrict__ src, int64_t lds_, int6
 
 // ---- bf16 Z (precision "bf16": the conv5 GEMM stores Z as bf16, as autocast
 // stores a conv output; statistics come from the fp32 accumulators) ----------
-// Register transposes, no LDS: a lane owns a 4-point x 8-channel micro-tile.
-// Z / dZ (point-major bf16) move as one 16-B access per point, dout / out
-// ((B,C,N) fp32) as one 16-B access per channel; lane = (channel group
-// cg = lane & 7, point group pg = lane >> 3), so every wave-instruction covers
-// 8 segments of 128 contiguous bytes on both sides. Block = 4 waves = 64
-// channels x 128 points; grid (B * ceil(N/128), ceil(C/64)).
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int RT_P = 128;  // points per block
 
-struct RtTile {
-    int b, n, o;  // cloud, first point, first channel of this lane's micro-tile
-    __device__ __forceinline__ RtTile(int N) {
-        const int nt = (N + RT_P - 1) / RT_P;
-        b = blockIdx.x / nt;
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        n = (blockIdx.x - b * nt) * RT_P + w * 32 + (lane >> 3) * 4;
-        o = blockIdx.y * 64 + (lane & 7) * 8;
-    }
-};
 
-__device__ __forceinline__ void load_z8(const bf16* __restrict__ Z, int64_t row, int C, int o, bool ok, float (&z)[8]) {
-    if (ok && o + 8 <= C && (C % 8) == 0) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Z + row * C + o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) z[j] = (float)v[j];
-    } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) z[j] = (ok && o + j < C) ? (float)Z[row * C + o + j] : 0.f;
-    }
-}
 
 // 4 consecutive points of channel row `oo` of a (B,C,N) fp32 tensor
 __device__ __forceinline__ float4 load_row4(const float* __restrict__ p, int64_t rowbase, int n, int N, bool ok) {
@@ -193,134 +167,158 @@ __device__ __forceinline__ void store_row4(float* __restrict__ p, int64_t rowbas
     }
 }
 
-// out(b, o, n) = LeakyReLU(a_o z + b_o)
-__global__ __launch_bounds__(256) void apply16_T_kernel(const bf16* __restrict__ Z, int N, int C,
-                                                        const float* __restrict__ scale,
-                                                        const float* __restrict__ shift, float slope,
-                                                        float* __restrict__ out) {
-    const RtTile T(N);
-    float z[4][8];
+// LDS-transposed tiles (128 points x 64 channels per block, 4 waves). Z / dZ
+// (point-major bf16) move as 16-B row pieces of the tile through LDS; dout /
+// out ((B,C,N) fp32) move with lanes along the points: lane = (pg = lane & 31,
+// half = lane >> 5), thread owns points 4pg..4pg+3 and channels 8cg..8cg+7 with
+// cg = 2*wave + half, so a wave-instruction covers 2 channel rows x 512
+// contiguous bytes. The Z tile's 16-B chunk c of row r sits at c ^ ((r>>2)&7):
+// the per-thread 16-B reads of rows 4pg+i are bank-conflict-free.
+constexpr int ZT_LD = 72;  // bf16 per LDS row (64 + 8 pad)
+
+struct ZTile {
+    int b, n0, o0, pg, cg;
+    __device__ __forceinline__ explicit ZTile(int N) {
+        const int nt = (N + RT_P - 1) / RT_P;
+        const int bt = blockIdx.x;
+        b = bt / nt;
+        n0 = (bt - b * nt) * RT_P;
+        o0 = blockIdx.y * 64;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        pg = lane & 31;
+        cg = 2 * w + (lane >> 5);
+    }
+};
+
+__device__ __forceinline__ int zt_off(int row, int chunk) { return row * ZT_LD + ((chunk ^ ((row >> 2) & 7)) << 3); }
+
+// rows [n0, n0+128) x channels [o0, o0+64) of Z into zt (zeros outside)
+__device__ __forceinline__ void stage_ztile(const bf16* __restrict__ Z, int b, int n0, int o0, int N, int C,
+                                            bf16* zt) {
+    for (int e = threadIdx.x; e < RT_P * 8; e += 256) {
+        const int row = e >> 3, ch = e & 7;
+        const int n = n0 + row, o = o0 + 8 * ch;
+        bf16x8 v;
+        if (n < N && o + 8 <= C && (C % 8) == 0) {
+            v = *reinterpret_cast<const bf16x8*>(Z + ((int64_t)b * N + n) * C + o);
+        } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) load_z8(Z, (int64_t)T.b * N + T.n + i, C, T.o, T.n + i < N, z[i]);
+            for (int j = 0; j < 8; ++j) v[j] = (n < N && o + j < C) ? Z[((int64_t)b * N + n) * C + o + j] : (bf16)0.f;
+        }
+        *reinterpret_cast<bf16x8*>(zt + zt_off(row, ch)) = v;
+    }
+}
+
+__device__ __forceinline__ void read_z48(const bf16* zt, int pg, int cg, float (&z)[4][8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(zt + zt_off(4 * pg + i, cg));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[i][j] = (float)v[j];
+    }
+}
+
+// out(b, o, n) = LeakyReLU(a_o z + b_o)
+__global__ __launch_bounds__(256) void apply16_lt_kernel(const bf16* __restrict__ Z, int N, int C,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, float slope,
+                                                         float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) bf16 zt[RT_P * ZT_LD];
+    const ZTile T(N);
+    stage_ztile(Z, T.b, T.n0, T.o0, N, C, zt);
+    __syncthreads();
+    float z[4][8];
+    read_z48(zt, T.pg, T.cg, z);
+    const int n = T.n0 + 4 * T.pg;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int oo = T.o + j;
+        const int oo = T.o0 + 8 * T.cg + j;
         if (oo >= C) break;
         const float a = scale[oo], sh = shift[oo];
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(a, z[i][j], sh), slope);
-        store_row4(out, ((int64_t)T.b * C + oo) * N, T.n, N, v);
+        store_row4(out, ((int64_t)T.b * C + oo) * N, n, N, v);
     }
 }
 
-// PASS 0: per-block partial (sum d, sum d*zhat) with d = dout * LeakyReLU'(a z + b)
-//         (the train-mode BatchNorm backward reductions); nothing else is written.
-// PASS 1: dZ = a d + c0 + c1 z (BN train-mode input gradient, bf16 point-major):
-//         the operand of the two weight/input-gradient GEMMs.
-template <int PASS>
-__global__ __launch_bounds__(256) void bwd16_kernel(const float* __restrict__ dout, const bf16* __restrict__ Z, int N,
-                                                    int C, const float* __restrict__ scale,
-                                                    const float* __restrict__ shift, const float* __restrict__ mean,
-                                                    const float* __restrict__ invstd, float slope,
-                                                    const float* __restrict__ c0, const float* __restrict__ c1,
-                                                    float* __restrict__ partials, bf16* __restrict__ dZ) {
-    __shared__ float red[2][4][64];
-    const RtTile T(N);
-    float z[4][8], g[8][4];
+// PASS 1 of the BN backward with the transposed tile: dZ = a d + c0 + c1 z,
+// d = dout * LeakyReLU'(a z + b); dZ goes back through the LDS tile so the
+// point-major bf16 rows are written as 16-B pieces.
+__global__ __launch_bounds__(256) void bwd16_dz_lt_kernel(const float* __restrict__ dout, const bf16* __restrict__ Z,
+                                                          int N, int C, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float slope,
+                                                          const float* __restrict__ c0, const float* __restrict__ c1,
+                                                          bf16* __restrict__ dZ) {
+    __shared__ __attribute__((aligned(16))) bf16 zt[RT_P * ZT_LD];
+    const ZTile T(N);
+    const int n = T.n0 + 4 * T.pg;
+    float g[8][4];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float4 v = load_row4(dout, ((int64_t)T.b * C + T.o + j) * N, T.n, N, T.o + j < C);
+        const int oo = T.o0 + 8 * T.cg + j;
+        const float4 v = load_row4(dout, ((int64_t)T.b * C + oo) * N, n, N, oo < C);
         g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) load_z8(Z, (int64_t)T.b * N + T.n + i, C, T.o, T.n + i < N, z[i]);
-    float s1[8], s2[8];
+    stage_ztile(Z, T.b, T.n0, T.o0, N, C, zt);
+    __syncthreads();
+    float z[4][8];
+    read_z48(zt, T.pg, T.cg, z);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const bool ok = T.o + j < C;
-        const int oj = ok ? T.o + j : 0;
-        const float a = scale[oj], sh = shift[oj];
-        if (PASS == 0) {
-            const float mu = mean[oj], is = invstd[oj];
-            float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float d = g[j][i] * (fmaf(a, z[i][j], sh) > 0.f ? 1.f : slope);
-                t1 += d;
-                t2 = fmaf(d, (z[i][j] - mu) * is, t2);
-            }
-            s1[j] = t1;
-            s2[j] = t2;
-        } else {
-            const float k0 = c0[oj], k1 = c1[oj];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float d = g[j][i] * (fmaf(a, z[i][j], sh) > 0.f ? 1.f : slope);
-                z[i][j] = fmaf(a, d, fmaf(k1, z[i][j], k0));  // dZ, reusing the registers
-            }
-        }
-    }
-    if (PASS == 1) {
+        const int oo = min(T.o0 + 8 * T.cg + j, C - 1);
+        const float a = scale[oo], sh = shift[oo], k0 = c0[oo], k1 = c1[oo];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int n = T.n + i;
-            if (n >= N) break;
-            const int64_t row = (int64_t)T.b * N + n;
-            if (T.o + 8 <= C && (C % 8) == 0) {
-                bf16x8 w;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) w[j] = (bf16)z[i][j];
-                *reinterpret_cast<bf16x8*>(dZ + row * C + T.o) = w;
-            } else {
-                for (int j = 0; j < 8 && T.o + j < C; ++j) dZ[row * C + T.o + j] = (bf16)z[i][j];
-            }
-        }
-        return;
-    }
-    // lanes of one channel group: l, l^8, l^16, l^32 in the wave, then the 4 waves
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-        for (int m = 8; m < 64; m <<= 1) {
-            s1[j] += __shfl_xor(s1[j], m);
-            s2[j] += __shfl_xor(s2[j], m);
+            const float d = g[j][i] * (fmaf(a, z[i][j], sh) > 0.f ? 1.f : slope);
+            z[i][j] = fmaf(a, d, fmaf(k1, z[i][j], k0));
         }
     }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane < 8) {
+    __syncthreads();  // every thread has read its Z values
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { red[0][w][lane * 8 + j] = s1[j]; red[1][w][lane * 8 + j] = s2[j]; }
+    for (int i = 0; i < 4; ++i) {
+        bf16x8 w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = (bf16)z[i][j];
+        *reinterpret_cast<bf16x8*>(zt + zt_off(4 * T.pg + i, T.cg)) = w;
     }
     __syncthreads();
-    const int t = threadIdx.x, o0 = blockIdx.y * 64;
-    if (t < 64 && o0 + t < C) {
-        partials[(int64_t)blockIdx.x * 2 * C + o0 + t] = ((red[0][0][t] + red[0][1][t]) + red[0][2][t]) + red[0][3][t];
-        partials[(int64_t)blockIdx.x * 2 * C + C + o0 + t] = ((red[1][0][t] + red[1][1][t]) + red[1][2][t]) + red[1][3][t];
+    for (int e = threadIdx.x; e < RT_P * 8; e += 256) {
+        const int row = e >> 3, ch = e & 7;
+        const int nn = T.n0 + row, o = T.o0 + 8 * ch;
+        if (nn >= N) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(zt + zt_off(row, ch));
+        bf16* dst = dZ + ((int64_t)T.b * N + nn) * C + o;
+        if (o + 8 <= C && (C % 8) == 0) {
+            *reinterpret_cast<bf16x8*>(dst) = v;
+        } else {
+            for (int j = 0; j < 8 && o + j < C; ++j) dst[j] = v[j];
+        }
     }
 }
 
-// PASS 0 over RS_LOOPS consecutive 128-point tiles per block: the per-channel
-// sums stay in registers across the tiles and are reduced once, so the
-// shuffle/LDS reduction is amortised over 4x the elements (pass 0 reads the
-// same bytes as pass 1 but writes nothing, so its cost was the reduction).
-constexpr int RS_LOOPS = 4;
-__global__ __launch_bounds__(256) void bwd16_stats_kernel(const float* __restrict__ dout, const bf16* __restrict__ Z,
-                                                          int N, int C, const float* __restrict__ scale,
-                                                          const float* __restrict__ shift,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd, float slope,
-                                                          float* __restrict__ partials) {
-    __shared__ float red[2][4][64];
-    const int nt = (N + RT_P * RS_LOOPS - 1) / (RT_P * RS_LOOPS);
+// PASS 0 with the transposed tile over RS_LT consecutive 128-point tiles per
+// block: per-thread sums over its 4 points, then over the 32 lanes of its
+// channel group (one shuffle tree), one partial row per block.
+constexpr int RS_LT = 1;
+__global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __restrict__ dout,
+                                                             const bf16* __restrict__ Z, int N, int C,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, float slope,
+                                                             float* __restrict__ partials) {
+    __shared__ __attribute__((aligned(16))) bf16 zt[RT_P * ZT_LD];
+    const int nt = (N + RT_P * RS_LT - 1) / (RT_P * RS_LT);
     const int b = blockIdx.x / nt;
+    const int nb = (blockIdx.x - b * nt) * RT_P * RS_LT;
+    const int o0 = blockIdx.y * 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nb = (blockIdx.x - b * nt) * RT_P * RS_LOOPS + w * 32 + (lane >> 3) * 4;
-    const int o = blockIdx.y * 64 + (lane & 7) * 8;
+    const int pg = lane & 31, cg = 2 * w + (lane >> 5);
     float a[8], sh[8], mu[8], is[8], s1[8], s2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int oj = o + j < C ? o + j : 0;
+        const int oj = min(o0 + 8 * cg + j, C - 1);
         a[j] = scale[oj];
         sh[j] = shift[oj];
         mu[j] = mean[oj];
@@ -329,17 +327,22 @@ __global__ __launch_bounds__(256) void bwd16_stats_kernel(const float* __restric
         s2[j] = 0.f;
     }
 #pragma unroll 1
-    for (int it = 0; it < RS_LOOPS; ++it) {
-        const int n = nb + it * RT_P;
-        if (n >= N) break;
-        float z[4][8], g[8][4];
+    for (int it = 0; it < RS_LT; ++it) {
+        const int n0 = nb + it * RT_P;
+        if (n0 >= N) break;
+        const int n = n0 + 4 * pg;
+        float g[8][4];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float4 v = load_row4(dout, ((int64_t)b * C + o + j) * N, n, N, o + j < C);
+            const int oo = o0 + 8 * cg + j;
+            const float4 v = load_row4(dout, ((int64_t)b * C + oo) * N, n, N, oo < C);
             g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) load_z8(Z, (int64_t)b * N + n + i, C, o, n + i < N, z[i]);
+        __syncthreads();  // previous tile's reads done
+        stage_ztile(Z, b, n0, o0, N, C, zt);
+        __syncthreads();
+        float z[4][8];
+        read_z48(zt, pg, cg, z);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
 #pragma unroll
@@ -350,24 +353,23 @@ __global__ __launch_bounds__(256) void bwd16_stats_kernel(const float* __restric
             }
         }
     }
-    // lanes of one channel group: l, l^8, l^16, l^32 in the wave, then the 4 waves
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
 #pragma unroll
-        for (int m = 8; m < 64; m <<= 1) {
+        for (int m = 1; m < 32; m <<= 1) {
             s1[j] += __shfl_xor(s1[j], m);
             s2[j] += __shfl_xor(s2[j], m);
         }
     }
-    if (lane < 8) {
+    if (pg == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { red[0][w][lane * 8 + j] = s1[j]; red[1][w][lane * 8 + j] = s2[j]; }
-    }
-    __syncthreads();
-    const int t = threadIdx.x, o0 = blockIdx.y * 64;
-    if (t < 64 && o0 + t < C) {
-        partials[(int64_t)blockIdx.x * 2 * C + o0 + t] = ((red[0][0][t] + red[0][1][t]) + red[0][2][t]) + red[0][3][t];
-        partials[(int64_t)blockIdx.x * 2 * C + C + o0 + t] = ((red[1][0][t] + red[1][1][t]) + red[1][2][t]) + red[1][3][t];
+        for (int j = 0; j < 8; ++j) {
+            const int oo = o0 + 8 * cg + j;
+            if (oo < C) {
+                partials[(int64_t)blockIdx.x * 2 * C + oo] = s1[j];
+                partials[(int64_t)blockIdx.x * 2 * C + C + oo] = s2[j];
+            }
+        }
     }
 }
 
@@ -431,14 +433,14 @@ int dgx_pointconv_input_grad(const float* dz, const float* Z, int ldz, int64_t M
 
 int dgx_pointconv_bf16_rows(int B, int N) {
     if (B < 1 || N < 1) return DGX_EINVAL;
-    return B * ((N + RT_P * RS_LOOPS - 1) / (RT_P * RS_LOOPS));  // pass-0 partial rows
+    return B * ((N + RT_P * RS_LT - 1) / (RT_P * RS_LT));  // pass-0 partial rows
 }
 
 int dgx_pointconv_apply_bf16(const void* Z, int B, int N, int C, const float* scale, const float* shift, float slope,
                              float* out, void* stream) {
     if (!Z || !scale || !shift || !out || B < 1 || N < 1 || C < 1) return DGX_EINVAL;
     dim3 grid(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64);
-    hipLaunchKernelGGL(apply16_T_kernel, grid, dim3(256), 0, dgx_stream(stream), static_cast<const bf16*>(Z), N, C,
+    hipLaunchKernelGGL(apply16_lt_kernel, grid, dim3(256), 0, dgx_stream(stream), static_cast<const bf16*>(Z), N, C,
                        scale, shift, slope, out);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
@@ -451,12 +453,12 @@ int dgx_pointconv_bwd_bf16(const float* dout, const void* Z, int B, int N, int C
     dim3 grid(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64);
     const bf16* z = static_cast<const bf16*>(Z);
     if (pass == 0)
-        hipLaunchKernelGGL(bwd16_stats_kernel, dim3(B * ((N + RT_P * RS_LOOPS - 1) / (RT_P * RS_LOOPS)), (C + 63) / 64),
+        hipLaunchKernelGGL(bwd16_stats_lt_kernel, dim3(B * ((N + RT_P * RS_LT - 1) / (RT_P * RS_LT)), (C + 63) / 64),
                            dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean, invstd, slope,
                            partials);
     else
-        hipLaunchKernelGGL(bwd16_kernel<1>, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift, mean,
-                           invstd, slope, c0, c1, partials, static_cast<bf16*>(dZ));
+        hipLaunchKernelGGL(bwd16_dz_lt_kernel, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift,
+                           slope, c0, c1, static_cast<bf16*>(dZ));
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
