@@ -100,7 +100,7 @@ def _split_weight(w, cin, cout):
 
 class _EdgeConvStack(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, layers, training, *params):
+    def forward(ctx, x, k, layers, training, ctx_preps, *params):
         dev = x.device
         B, C0, N = x.shape
         M = B * N
@@ -125,8 +125,8 @@ class _EdgeConvStack(torch.autograd.Function):
         side = _side_stream(dev) if want_bwd and training else None
         # bf16 [W1;W2] and transposed copies of blocks 2.. in one launch (used when
         # the block's input is the bf16 twin, i.e. after a batch-statistics block)
-        preps = [None] * len(layers)
-        if bf16 and len(layers) > 1:
+        preps = list(ctx_preps) if ctx_preps is not None else [None] * len(layers)
+        if bf16 and len(layers) > 1 and ctx_preps is None:
             jobs = [(params[3 * li], ly.cout, ly.cin, True) for li, ly in enumerate(layers) if li > 0]
             preps[1:] = G.prep_weights(jobs)
         for li, ly in enumerate(layers):
@@ -224,7 +224,7 @@ class _EdgeConvStack(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dxcat, _unused):
         if dxcat is None:
-            return (None,) * (4 + len(ctx.saved_tensors) - 3)
+            return (None,) * (5 + len(ctx.saved_tensors) - 3)
         if any(s is None for s in ctx.layer_state):
             raise RuntimeError("dgx EdgeConv: backward through an eval-mode (running-stats) forward is not supported")
         x_pm, xcat, xcat16, *params = ctx.saved_tensors
@@ -331,12 +331,14 @@ class _EdgeConvStack(torch.autograd.Function):
                     dxcat[:, prev:prev + cin] += prec.mm(dPQ, wcat)
                 elif ctx.x_needs_grad:
                     dx_in = prec.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
-        return (dx_in, None, None, None, *grads)
+        return (dx_in, None, None, None, None, *grads)
 
 
-def edgeconv_stack_pair(x, k, convs, training):
+def edgeconv_stack_pair(x, k, convs, training, preps=None):
     """As edgeconv_stack, also returning the bf16 twin of the concat buffer
-    (empty unless precision "bf16" produced it): conv5's GEMM operand."""
+    (empty unless precision "bf16" produced it): conv5's GEMM operand.
+    ``preps``: optional per-block bf16 weight copies (gemm.prep_weights) made
+    by the caller in one launch with other layers' (None for block 1)."""
     nat.require_device(x)
     if x.dtype != torch.float32:
         x = x.float()
@@ -348,7 +350,7 @@ def edgeconv_stack_pair(x, k, convs, training):
             raise NotImplementedError("dgx EdgeConv expects affine BatchNorm (as the reference builds it)")
         layers.append(_Layer(c2 // 2, co, bn, act.negative_slope))
         params += [conv.weight, bn.weight, bn.bias]
-    return _EdgeConvStack.apply(x, k, layers, training, *params)
+    return _EdgeConvStack.apply(x, k, layers, training, preps, *params)
 
 
 def edgeconv_stack(x, k, convs, training):

@@ -20,7 +20,7 @@ from .edgeconv import _bn_factor
 
 class _PointConvBNLReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, X, X16, B, N, bn, slope, training, weight, gamma, beta):
+    def forward(ctx, X, X16, B, N, bn, slope, training, wprep_in, weight, gamma, beta):
         L = nat.lib()
         dev = X.device
         stream = nat.stream_of(X)
@@ -38,7 +38,7 @@ class _PointConvBNLReLU(torch.autograd.Function):
                 # bf16 twin of the concat buffer + bf16 W / W^T: LDS-DMA staged operands;
                 # Z is stored bf16 (as autocast stores a conv output), stats from fp32 sums
                 Xop = X16
-                wprep = G.prep_weight(weight, Co, K, False)
+                wprep = wprep_in if wprep_in is not None else G.prep_weight(weight, Co, K, False)
                 with G.tag("conv5_fwd"):
                     Z, gemm_part = G.lds_xwt(X16, wprep[0], stats=True, out_bf16=True)
                 z16 = True
@@ -107,8 +107,8 @@ class _PointConvBNLReLU(torch.autograd.Function):
         partials = torch.empty((rows, 2, Co), dtype=torch.float32, device=dev)
         dgamma = torch.empty(Co, dtype=torch.float32, device=dev)
         dbeta = torch.empty_like(dgamma)
-        c0 = torch.zeros_like(dgamma)
-        c1 = torch.zeros_like(dgamma)
+        c0 = torch.empty_like(dgamma)
+        c1 = torch.empty_like(dgamma)
         dZ = torch.empty((M, Co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
         with torch.cuda.device(dev):
             if z16:  # two passes over (dout, Z): BN-backward reductions, then dZ directly
@@ -134,6 +134,8 @@ class _PointConvBNLReLU(torch.autograd.Function):
                                                     nat.ptr(mean), nat.ptr(invstd), nat.ptr(dgamma), nat.ptr(dbeta),
                                                     nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
             else:  # running-stats BN: affine only
+                c0.zero_()
+                c1.zero_()
                 sums = partials.sum(0)
                 dbeta.copy_(sums[0])
                 dgamma.copy_(sums[1])
@@ -158,16 +160,18 @@ class _PointConvBNLReLU(torch.autograd.Function):
         else:
             dW = torch.mm(dZ.t(), Xop)
             dX = torch.mm(dZ, W)
-        return dX, None, None, None, None, None, None, dW.view(Co, -1, 1, 1), dgamma, dbeta
+        return dX, None, None, None, None, None, None, None, dW.view(Co, -1, 1, 1), dgamma, dbeta
 
 
-def pointconv_bn_lrelu(X, B, N, seq, training, X16=None):
+def pointconv_bn_lrelu(X, B, N, seq, training, X16=None, wprep=None):
     """X (B*N, K) point-major -> (B, Co, N) = LeakyReLU(BN(Conv1x1(X))) with the
     modules of ``seq`` = nn.Sequential(Conv2d(K,Co,1,bias=False), BatchNorm2d,
     LeakyReLU) (reference dgcnn.py:74-78). ``X16``: optional bf16 twin of X
-    (precision "bf16"), the GEMM operand."""
+    (precision "bf16"), the GEMM operand. ``wprep``: optional bf16 (W, W^T) of
+    the conv weight already made for this step (gemm.prep_weights)."""
     nat.require_device(X)
     conv, bn, act = seq[0], seq[1], seq[2]
     if conv.bias is not None or bn.weight is None:
         raise NotImplementedError("dgx pointconv expects Conv(bias=False) + affine BatchNorm")
-    return _PointConvBNLReLU.apply(X, X16, B, N, bn, act.negative_slope, training, conv.weight, bn.weight, bn.bias)
+    return _PointConvBNLReLU.apply(X, X16, B, N, bn, act.negative_slope, training, wprep, conv.weight, bn.weight,
+                                   bn.bias)

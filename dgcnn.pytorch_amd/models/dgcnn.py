@@ -15,7 +15,9 @@ unchanged. The work runs in libdgx.so on the MI355X:
 import torch
 import torch.nn as nn
 
+from dgx import gemm as _gemm
 from dgx import ops as _ops
+from dgx import precision as _prec
 from dgx.edgeconv import edgeconv_stack_pair
 from dgx.pointconv import pointconv_bn_lrelu
 
@@ -36,6 +38,21 @@ def _edge_block(c_in, c_out):
     return nn.Sequential(nn.Conv2d(2 * c_in, c_out, kernel_size=1, bias=False),
                          nn.BatchNorm2d(c_out),
                          nn.LeakyReLU(negative_slope=0.2, inplace=True))
+
+
+def _bf16_weight_copies(model):
+    """bf16 operand copies ([W1;W2] / W and transposes) of conv2..conv5 for the
+    engine's bf16 GEMMs, all in one launch per step (precision "bf16" only)."""
+    if _prec.get() != "bf16":
+        return None
+    jobs = []
+    for conv in (model.conv2, model.conv3, model.conv4):
+        w = conv[0].weight
+        jobs.append((w, w.shape[0], w.shape[1] // 2, True))
+    w5 = model.conv5[0].weight
+    jobs.append((w5, w5.shape[0], w5.shape[1], False))
+    out = _gemm.prep_weights(jobs)
+    return [None] + out
 
 
 class DGCNN(nn.Module):
@@ -62,7 +79,10 @@ class DGCNN(nn.Module):
 
     def forward(self, x):
         batch_size, _, num_points = x.size()
+        preps = _bf16_weight_copies(self) if self.training else None
         # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)
-        feats, feats16 = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training)   # (B*N, 512)
+        feats, feats16 = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training,
+                                             preps=None if preps is None else preps[:4])   # (B*N, 512)
         # conv5 -> BN -> LeakyReLU (dgcnn.py:100-102), written as (B, emb, N)
-        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training, X16=feats16)
+        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training, X16=feats16,
+                                  wprep=None if preps is None else preps[4])
