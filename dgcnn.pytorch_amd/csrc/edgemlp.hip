@@ -1,0 +1,326 @@
+// Per-edge two-layer MLP of the PositionEmbedding block (reference
+// models/layers.py:45-52):
+//     e  = get_graph_feature(x, k)                       (B, 2C, N, k)
+//     h1 = LeakyReLU(BN1(Conv2d(2C -> C1, 1x1)(e)))       per edge, NOT maxed
+//     z2 = Conv2d(C1 -> C2, 1x1)(h1)                      per edge
+//     t  = max_k LeakyReLU(BN2(z2))                       (B, C2, N)
+// Layout: edges are rows e = i*k + s (i = global point, s = neighbour slot),
+// point-major like the EdgeConv chain. The first conv is decomposed as in
+// edgeconv.hip (y_e = P_j + Q_i from PQ = X [W1;W2]^T), so only h1 (E x C1)
+// and z2 (E x C2) exist per edge; both feed / come from the caller's MFMA GEMM
+// (gemm.hip) as dense row-major operands. BN1 statistics come from
+// dgx_edge_fwd_gather_f32 (sums over all edges of P_j + Q_i), BN2 statistics
+// from the z2 GEMM's epilogue (or dgx_colstats_f32).
+//
+// Kernels (all HBM/L2 streaming, 16-byte accesses along channels):
+//   mlp_h1_kernel        h1 = LReLU(a1 (P_j + Q_i) + b1), fp32 or bf16 rows
+//   mlp_max_kernel       max_k (min_k where a2 < 0) of z2 and its slot
+//   mlp_dz2_kernel       dZ2 = a2 dz [slot] + c0 + c1 z2 (BN2 backward), dense
+//   mlp_h1_bwd_kernel    g = dH1 * LReLU'(z1) in place + BN1-backward partials
+//   mlp_h1_scatter_kernel dP_j / dQ_i from g over the kNN graph and its reverse
+#include "common.h"
+
+namespace {
+
+constexpr int EM_THREADS = 256;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 ld4_any(const void* base, int64_t off, bool b16) {
+    if (b16) {
+        const bf16x4_t h = *reinterpret_cast<const bf16x4_t*>(static_cast<const __bf16*>(base) + off);
+        return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+    }
+    return ld4(static_cast<const float*>(base) + off);
+}
+
+__device__ __forceinline__ void st4_any(void* base, int64_t off, float4 v, bool b16) {
+    if (b16) {
+        const bf16x4_t h = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        *reinterpret_cast<bf16x4_t*>(static_cast<__bf16*>(base) + off) = h;
+    } else {
+        *reinterpret_cast<float4*>(static_cast<float*>(base) + off) = v;
+    }
+}
+
+__device__ __forceinline__ float comp(const float4& v, int u) {
+    return u == 0 ? v.x : (u == 1 ? v.y : (u == 2 ? v.z : v.w));
+}
+
+inline int grid_of(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
+// h1[e][c] = LReLU(fmaf(a_c, P_j[c] + Q_i[c], b_c)), 4 channels per thread.
+template <bool OUT16>
+__global__ __launch_bounds__(EM_THREADS) void mlp_h1_kernel(const float* __restrict__ PQ, int ldpq,
+                                                            const int32_t* __restrict__ idx, int N, int k, int C1,
+                                                            int64_t E, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, float slope,
+                                                            void* __restrict__ H1) {
+    const int cq = C1 >> 2;
+    const int64_t total = E * cq;
+    for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * EM_THREADS) {
+        const int c = (int)(t % cq) * 4;
+        const int64_t e = t / cq;
+        const int64_t i = e / k;
+        const int64_t j = (i / N) * N + idx[e];
+        const float4 p = ld4(PQ + j * ldpq + c), q = ld4(PQ + i * ldpq + C1 + c);
+        const float4 a = ld4(scale + c), b = ld4(shift + c);
+        const float4 h = make_float4(lrelu(fmaf(a.x, p.x + q.x, b.x), slope), lrelu(fmaf(a.y, p.y + q.y, b.y), slope),
+                                     lrelu(fmaf(a.z, p.z + q.z, b.z), slope), lrelu(fmaf(a.w, p.w + q.w, b.w), slope));
+        st4_any(H1, e * C1 + c, h, OUT16);
+    }
+}
+
+// ysel[i][c] = max_s z2[i*k+s][c] (min where scale[c] < 0: BN's affine is
+// decreasing there, so LReLU(BN(.)) is maximised by the smallest z), arg = s
+// of the first extremum (the order torch.max keeps on ties).
+template <bool IN16>
+__global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restrict__ Z, int64_t M, int k, int C2,
+                                                             const float* __restrict__ scale,
+                                                             float* __restrict__ ysel, uint8_t* __restrict__ arg) {
+    const int cq = C2 >> 2;
+    const int64_t total = M * cq;
+    for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * EM_THREADS) {
+        const int c = (int)(t % cq) * 4;
+        const int64_t i = t / cq;
+        const float4 a = ld4(scale + c);
+        const bool mn[4] = {a.x < 0.f, a.y < 0.f, a.z < 0.f, a.w < 0.f};
+        float4 best = ld4_any(Z, i * k * C2 + c, IN16);
+        float bv[4] = {best.x, best.y, best.z, best.w};
+        int bs[4] = {0, 0, 0, 0};
+        for (int s = 1; s < k; ++s) {
+            const float4 v = ld4_any(Z, (i * k + s) * C2 + c, IN16);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float x = comp(v, u);
+                if (mn[u] ? x < bv[u] : x > bv[u]) { bv[u] = x; bs[u] = s; }
+            }
+        }
+        *reinterpret_cast<float4*>(ysel + i * C2 + c) = make_float4(bv[0], bv[1], bv[2], bv[3]);
+        const uint32_t packed = (uint32_t)bs[0] | ((uint32_t)bs[1] << 8) | ((uint32_t)bs[2] << 16) |
+                                ((uint32_t)bs[3] << 24);
+        *reinterpret_cast<uint32_t*>(arg + i * C2 + c) = packed;
+    }
+}
+
+// BN2 backward, dense over edges: dZ2[e][c] = a_c dz_i[c] [s == slot_i[c]] + c0_c + c1_c z2[e][c].
+template <bool IO16>
+__global__ __launch_bounds__(EM_THREADS) void mlp_dz2_kernel(const float* __restrict__ dzp, const void* __restrict__ Z,
+                                                             int64_t M, int k, int C2, const float* __restrict__ scale,
+                                                             const float* __restrict__ c0,
+                                                             const float* __restrict__ c1, void* __restrict__ dZ) {
+    const int cq = C2 >> 2;
+    const int64_t total = M * k * cq;
+    for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * EM_THREADS) {
+        const int c = (int)(t % cq) * 4;
+        const int64_t e = t / cq;
+        const int64_t i = e / k;
+        const int s = (int)(e - i * k);
+        const float4 z = ld4_any(Z, e * C2 + c, IO16);
+        const float4 d = ld4(dzp + i * C2 + c);
+        const float4 a = ld4(scale + c), k0 = ld4(c0 + c), k1 = ld4(c1 + c);
+        float r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float v = fmaf(comp(k1, u), comp(z, u), comp(k0, u));
+            const float du = comp(d, u);
+            if (unpack_slot(du) == s) v = fmaf(comp(a, u), unpack_dz(du), v);
+            r[u] = v;
+        }
+        st4_any(dZ, e * C2 + c, make_float4(r[0], r[1], r[2], r[3]), IO16);
+    }
+}
+
+// LReLU + BN1 backward, first half: g = dH1 * LReLU'(z1) (written over dH1)
+// and per-block partials (sum g, sum g * yhat) per channel -> partials[block][2][C1].
+// Block = (256 / cq) edge rows x cq channel quads; each thread keeps fixed
+// channels, so the block's partial is a fixed-order sum (deterministic).
+__global__ __launch_bounds__(EM_THREADS) void mlp_h1_bwd_kernel(
+    float* __restrict__ dH, const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int N, int k,
+    int C1, int64_t E, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float slope, float* __restrict__ partials) {
+    __shared__ float red[2][EM_THREADS][4];
+    const int cq = C1 >> 2;
+    const int epb = EM_THREADS / cq;
+    const int tid = threadIdx.x;
+    const int er = tid / cq, c = (tid - er * cq) * 4;
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    if (er < epb) {
+        const float4 a = ld4(scale + c), b = ld4(shift + c), mu = ld4(mean + c), is = ld4(invstd + c);
+        for (int64_t e = (int64_t)blockIdx.x * epb + er; e < E; e += (int64_t)gridDim.x * epb) {
+            const int64_t i = e / k;
+            const int64_t j = (i / N) * N + idx[e];
+            const float4 p = ld4(PQ + j * ldpq + c), q = ld4(PQ + i * ldpq + C1 + c);
+            const float4 dh = ld4(dH + e * C1 + c);
+            float g[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float y = comp(p, u) + comp(q, u);
+                const float z = fmaf(comp(a, u), y, comp(b, u));
+                g[u] = comp(dh, u) * (z > 0.f ? 1.f : slope);
+                s1[u] += g[u];
+                s2[u] = fmaf(g[u], (y - comp(mu, u)) * comp(is, u), s2[u]);
+            }
+            *reinterpret_cast<float4*>(dH + e * C1 + c) = make_float4(g[0], g[1], g[2], g[3]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        red[0][tid][u] = s1[u];
+        red[1][tid][u] = s2[u];
+    }
+    __syncthreads();
+    if (tid < cq) {
+        float t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < epb; ++r) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                t1[u] += red[0][r * cq + tid][u];
+                t2[u] += red[1][r * cq + tid][u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            partials[(int64_t)blockIdx.x * 2 * C1 + c + u] = t1[u];
+            partials[(int64_t)blockIdx.x * 2 * C1 + C1 + c + u] = t2[u];
+        }
+    }
+}
+
+// BN1 backward, second half, one wave per point p (lanes = channels):
+//   dy_e = a g_e + c0 + c1 (P_j + Q_i) for edge e = (i, s), j = idx[e]
+//   dQ_p = sum over p's own k edges of dy,  dP_p = sum over p's in-edges of dy
+// (in-edges from dgx_graph_reverse: id = (i << 6) | s, sorted lists).
+__global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
+    const float* __restrict__ g, const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges, int64_t M, int N, int k, int C1,
+    const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
+    float* __restrict__ dPQ) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * (EM_THREADS / 64) + (threadIdx.x >> 6);
+    if (p >= M) return;
+    const int64_t base = (p / N) * N;
+    const int32_t beg = rowptr[p], end = rowptr[p + 1];
+    const float kf = (float)k, deg = (float)(end - beg);
+    for (int c = lane; c < C1; c += 64) {
+        const float a = scale[c], k0 = c0[c], k1 = c1[c];
+        float sg = 0.f, sp = 0.f;
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = p * k + s;
+            sg += g[e * C1 + c];
+            sp += PQ[(base + idx[e]) * ldpq + c];
+        }
+        float ig = 0.f, iq = 0.f;
+        for (int32_t r = beg; r < end; ++r) {
+            const int32_t id = edges[r];
+            const int64_t src = (int64_t)(id >> 6);
+            ig += g[(src * k + (id & 63)) * C1 + c];
+            iq += PQ[src * ldpq + C1 + c];
+        }
+        const float Pp = PQ[p * ldpq + c], Qp = PQ[p * ldpq + C1 + c];
+        dPQ[p * 2 * C1 + c] = fmaf(a, ig, fmaf(k0, deg, k1 * fmaf(deg, Pp, iq)));
+        dPQ[p * 2 * C1 + C1 + c] = fmaf(a, sg, fmaf(k0, kf, k1 * fmaf(kf, Qp, sp)));
+    }
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
+                        const float* scale, const float* shift, float slope, void* H1, int out_bf16, void* stream) {
+    if (!PQ || !idx || !scale || !shift || !H1 || B < 1 || N < 1 || k < 1 || C1 < 4 || ldpq < 2 * C1)
+        return DGX_EINVAL;
+    if (C1 % 4 || ldpq % 4 || !al16(PQ) || !al16(scale) || !al16(shift) || !al16(H1)) return DGX_EUNSUPPORTED;
+    const int64_t E = (int64_t)B * N * k;
+    const int grid = grid_of(E * (C1 / 4), EM_THREADS);
+    if (out_bf16)
+        hipLaunchKernelGGL(mlp_h1_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), PQ, ldpq, idx, N,
+                           k, C1, E, scale, shift, slope, H1);
+    else
+        hipLaunchKernelGGL(mlp_h1_kernel<false>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), PQ, ldpq, idx,
+                           N, k, C1, E, scale, shift, slope, H1);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2, const float* scale, float* ysel,
+                         uint8_t* arg, void* stream) {
+    if (!Z || !scale || !ysel || !arg || B < 1 || N < 1 || k < 1 || k > 64 || C2 < 4) return DGX_EINVAL;
+    if (C2 % 4 || !al16(Z) || !al16(scale) || !al16(ysel) || (reinterpret_cast<uintptr_t>(arg) & 3))
+        return DGX_EUNSUPPORTED;
+    const int64_t M = (int64_t)B * N;
+    const int grid = grid_of(M * (C2 / 4), EM_THREADS);
+    if (z_bf16)
+        hipLaunchKernelGGL(mlp_max_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), Z, M, k, C2,
+                           scale, ysel, arg);
+    else
+        hipLaunchKernelGGL(mlp_max_kernel<false>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), Z, M, k, C2,
+                           scale, ysel, arg);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_mlp_dz_f32(const float* dzp, const void* Z, int bf16, int B, int N, int k, int C2, const float* scale,
+                        const float* c0, const float* c1, void* dZ, void* stream) {
+    if (!dzp || !Z || !scale || !c0 || !c1 || !dZ || B < 1 || N < 1 || k < 1 || k > 64 || C2 < 4) return DGX_EINVAL;
+    if (C2 % 4 || !al16(dzp) || !al16(Z) || !al16(dZ) || !al16(scale) || !al16(c0) || !al16(c1))
+        return DGX_EUNSUPPORTED;
+    const int64_t M = (int64_t)B * N;
+    const int grid = grid_of(M * k * (C2 / 4), EM_THREADS);
+    if (bf16)
+        hipLaunchKernelGGL(mlp_dz2_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dzp, Z, M, k, C2,
+                           scale, c0, c1, dZ);
+    else
+        hipLaunchKernelGGL(mlp_dz2_kernel<false>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dzp, Z, M, k,
+                           C2, scale, c0, c1, dZ);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_mlp_h1_bwd_rows(int B, int N, int k, int C1) {
+    if (B < 1 || N < 1 || k < 1 || C1 < 4) return DGX_EINVAL;
+    const int64_t E = (int64_t)B * N * k;
+    const int epb = EM_THREADS / (C1 / 4 > 0 ? C1 / 4 : 1);
+    int64_t rows = (E + epb * 8 - 1) / (epb * 8);  // ~8 edge rows per thread
+    return (int)(rows < 1 ? 1 : (rows > 2048 ? 2048 : rows));
+}
+
+int dgx_edge_mlp_h1_bwd_f32(float* dH, const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
+                            const float* scale, const float* shift, const float* mean, const float* invstd,
+                            float slope, float* partials, int nrows, void* stream) {
+    if (!dH || !PQ || !idx || !scale || !shift || !mean || !invstd || !partials || B < 1 || N < 1 || k < 1 ||
+        ldpq < 2 * C1 || nrows != dgx_edge_mlp_h1_bwd_rows(B, N, k, C1))
+        return DGX_EINVAL;
+    // fixed channel quads per thread: C1/4 must divide the block
+    if (C1 % 4 || EM_THREADS % (C1 / 4) || ldpq % 4 || !al16(dH) || !al16(PQ) || !al16(scale) || !al16(shift) ||
+        !al16(mean) || !al16(invstd))
+        return DGX_EUNSUPPORTED;
+    const int64_t E = (int64_t)B * N * k;
+    hipLaunchKernelGGL(mlp_h1_bwd_kernel, dim3(nrows), dim3(EM_THREADS), 0, dgx_stream(stream), dH, PQ, ldpq, idx, N,
+                       k, C1, E, scale, shift, mean, invstd, slope, partials);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const int32_t* idx, const int32_t* rowptr,
+                             const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
+                             const float* c1, float* dPQ, void* stream) {
+    if (!g || !PQ || !idx || !rowptr || !edges || !scale || !c0 || !c1 || !dPQ || B < 1 || N < 1 || k < 1 ||
+        k > 64 || C1 < 1 || ldpq < 2 * C1)
+        return DGX_EINVAL;
+    const int64_t M = (int64_t)B * N;
+    const int64_t blocks = (M + EM_THREADS / 64 - 1) / (EM_THREADS / 64);
+    if (blocks > 0x7fffffff) return DGX_EUNSUPPORTED;
+    hipLaunchKernelGGL(mlp_h1_scatter_kernel, dim3((unsigned)blocks), dim3(EM_THREADS), 0, dgx_stream(stream), g, PQ,
+                       ldpq, idx, rowptr, edges, M, N, k, C1, scale, c0, c1, dPQ);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+}  // extern "C"

@@ -65,6 +65,13 @@ _SIGS = {
     "dgx_pointconv_bf16_rows": [_i32, _i32],
     "dgx_pointconv_apply_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],
     "dgx_pointconv_bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dgx_edge_mlp_h1_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
+    "dgx_edge_mlp_max_f32": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
+    "dgx_edge_mlp_dz_f32": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "dgx_edge_mlp_h1_bwd_rows": [_i32, _i32, _i32, _i32],
+    "dgx_edge_mlp_h1_bwd_f32": [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i32,
+                                _vp],
+    "dgx_edge_mlp_scatter_f32": [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {
     "dgx_version": ctypes.c_char_p,

@@ -7,12 +7,19 @@ with BN + LeakyReLU, max over k, a per-point 128->1024 conv, max over points,
 an MLP to a 3x3 matrix (identity-initialised) and ``bmm`` with the input.
 Parameter and buffer names match the reference, including the ``bn1/bn2/bn3``
 aliases of ``conv{1,2,3}.1``.
+
+The edge stage (layers.py:45-52: graph feature -> conv1 -> conv2 -> max over
+k) runs as one engine op, ``dgx.edgemlp.edge_mlp2``: conv1 decomposed over the
+kNN graph (the (B,6,N,k) edge tensor is never built), conv2 as an MFMA GEMM
+over the B*N*k edge rows, BN statistics, LeakyReLU and the max fused into HIP
+kernels (csrc/edgemlp.hip).
 """
 import torch
 import torch.nn as nn
 import torch.nn.init as init
 
-from models.dgcnn import get_graph_feature
+from dgx.edgemlp import edge_mlp2
+from models.dgcnn import get_graph_feature  # noqa: F401  (bound by name as at layers.py:6)
 
 
 def _lrelu(inplace=False):
@@ -39,8 +46,8 @@ class PositionEmbedding(nn.Module):
 
     def forward(self, x):
         n_clouds = x.size(0)
-        edges = get_graph_feature(x, k=self.k)                   # (B, 6, N, k)    layers.py:45
-        t = self.conv2(self.conv1(edges)).max(dim=-1)[0]          # (B, 128, N)     layers.py:48-52
+        # get_graph_feature + conv1 + conv2 + max over k, fused   (B, 128, N)     layers.py:45-52
+        t = edge_mlp2(x, self.k, self.conv1, self.conv2, self.training)
         t = self.conv3(t).max(dim=-1)[0]                          # (B, 1024)       layers.py:55-57
         t = self.transform(self.linear(t)).view(n_clouds, 3, 3)   # (B, 3, 3)       layers.py:60-65
         return torch.bmm(x.transpose(2, 1), t).transpose(2, 1)    # (B, 3, N)       layers.py:68-72

@@ -253,6 +253,40 @@ int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt,
 int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, const int* C, const int* stacked,
                                void* const* nt, void* const* tn, void* stream);
 
+/* ---- a6: PositionEmbedding's per-edge MLP, replaces
+ *   get_graph_feature -> conv1 (Conv2d 2C->C1, BN, LeakyReLU, per edge)
+ *   -> conv2 (Conv2d C1->C2, BN, LeakyReLU) -> max(dim=-1)
+ *                                             (models/layers.py:45-52, 17-22)
+ * Edge rows e = i*k + s (i = global point, s = slot), E = B*N*k. conv1 is
+ * decomposed as in a3 (PQ = X [W1;W2]^T, y_e = P_j + Q_i, BN1 statistics from
+ * dgx_edge_fwd_gather_f32); conv2 is the caller's GEMM Z2 = H1 W^T over the E
+ * edge rows (BN2 statistics from its epilogue / dgx_colstats_f32).
+ *   dgx_edge_mlp_h1: H1 (E x C1) = LeakyReLU(a1 (P_j + Q_i) + b1), fp32 or
+ *     bf16 (out_bf16 != 0: the GEMM operand).
+ *   dgx_edge_mlp_max: ysel (M x C2) = max_s Z2 (min where a2 < 0), arg = the
+ *     first extremal slot; then dgx_bn_lrelu_apply_f32 gives the output.
+ * Backward: dgx_edge_bwd_dz_f32 + dgx_bn_bwd_finalize_f32 on (ysel, arg) ->
+ *   dgx_edge_mlp_dz: dZ2 (E x C2) = a2 dz [s == slot] + c0 + c1 Z2 (dense BN2
+ *     backward; Z2/dZ2 both fp32 or both bf16);
+ *   caller's GEMMs dH1 = dZ2 W2, dW2 = dZ2^T H1;
+ *   dgx_edge_mlp_h1_bwd: dH1 *= LeakyReLU'(z1) in place + partials (sum g,
+ *     sum g*yhat) [dgx_edge_mlp_h1_bwd_rows][2][C1] -> dgx_bn_bwd_finalize_f32;
+ *   dgx_edge_mlp_scatter: dPQ (M x 2C1) fp32, dQ_i = sum over i's edges and
+ *     dP_j = sum over j's in-edges (dgx_graph_reverse) of a1 g + c0 + c1 y. */
+int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
+                        const float* scale, const float* shift, float slope, void* H1, int out_bf16, void* stream);
+int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2, const float* scale, float* ysel,
+                         uint8_t* arg, void* stream);
+int dgx_edge_mlp_dz_f32(const float* dzp, const void* Z, int bf16, int B, int N, int k, int C2, const float* scale,
+                        const float* c0, const float* c1, void* dZ, void* stream);
+int dgx_edge_mlp_h1_bwd_rows(int B, int N, int k, int C1);
+int dgx_edge_mlp_h1_bwd_f32(float* dH, const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
+                            const float* scale, const float* shift, const float* mean, const float* invstd,
+                            float slope, float* partials, int nrows, void* stream);
+int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const int32_t* idx, const int32_t* rowptr,
+                             const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
+                             const float* c1, float* dPQ, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

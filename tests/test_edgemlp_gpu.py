@@ -1,0 +1,205 @@
+"""a6 parity: PositionEmbedding's fused per-edge MLP (dgx.edgemlp, csrc/edgemlp.hip)
+against the reference op sequence (models/layers.py:45-52: get_graph_feature ->
+conv1 -> conv2 -> max over k) recomputed in fp64 on the CPU from the same
+neighbour sets (the engine's kNN is bit-exact with the reference, tested in
+test_knn_gpu.py)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import rel_err
+from oracle import reference as R
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+
+
+def _convs(seed, cin2=6, c1=64, c2=128, neg=True):
+    g = torch.Generator().manual_seed(seed)
+
+    def block(ci, co):
+        blk = torch.nn.Sequential(torch.nn.Conv2d(ci, co, 1, bias=False), torch.nn.BatchNorm2d(co),
+                                  torch.nn.LeakyReLU(0.2))
+        with torch.no_grad():
+            blk[0].weight.copy_(torch.randn(co, ci, 1, 1, generator=g) / np.sqrt(ci))
+            gam = 1.0 + 0.3 * torch.randn(co, generator=g)
+            if neg:
+                gam[::5] *= -1.0  # decreasing BN affine on some channels: min-over-k path
+            blk[1].weight.copy_(gam)
+            blk[1].bias.copy_(0.2 * torch.randn(co, generator=g))
+        return blk
+    return block(cin2, c1), block(c1, c2)
+
+
+def _reference(x64, idx, conv1, conv2):
+    e = R.graph_feature(x64, idx.shape[-1], idx=idx)
+    return conv2(conv1(e)).max(dim=-1)[0]
+
+
+def _frac_close(a, b, tol):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float((np.abs(a - b) <= tol * max(np.abs(b).max(), 1e-30)).mean())
+
+
+@pytest.mark.parametrize("B,N,k", [(2, 256, 20), (1, 500, 40), (3, 128, 7)])
+def test_edge_mlp_train_matches_reference(cuda, B, N, k):
+    from dgx import synth
+    from dgx.edgemlp import edge_mlp2
+    conv1, conv2 = _convs(11 + k)
+    ref1, ref2 = _convs(11 + k)
+    ref1, ref2 = ref1.double().train(), ref2.double().train()
+    conv1, conv2 = conv1.to(cuda).train(), conv2.to(cuda).train()
+    pts = synth.cube_clouds(B, N, 40 + N)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1).requires_grad_(True)
+    y = edge_mlp2(x, k, conv1, conv2, True)
+    assert y.shape == (B, 128, N)
+    gout = torch.from_numpy(synth.uniform(9, (B, 128, N)) - 0.5).float()
+    y.backward(gout.to(cuda))
+
+    x64 = torch.from_numpy(pts).double().permute(0, 2, 1).requires_grad_(True)
+    idx = oracle.knn(torch.from_numpy(pts).permute(0, 2, 1), k)
+    ref = _reference(x64, torch.as_tensor(idx).long(), ref1, ref2)
+    ref.backward(gout.double())
+
+    assert rel_err(y.detach().cpu(), ref.detach()) < TOL
+    # running statistics of both BatchNorms (momentum update, unbiased var)
+    for got, want in ((conv1[1], ref1[1]), (conv2[1], ref2[1])):
+        assert rel_err(got.running_mean.cpu(), want.running_mean) < 1e-4
+        assert rel_err(got.running_var.cpu(), want.running_var) < 1e-4
+        assert int(got.num_batches_tracked) == 1
+    # gradients: a LeakyReLU kink or near-tie max that fp32 rounding flips moves a
+    # handful of elements; everything else must agree to 1e-3 of the tensor's scale
+    pairs = [(x.grad, x64.grad)]
+    for got, want in ((conv1, ref1), (conv2, ref2)):
+        pairs += [(got[0].weight.grad, want[0].weight.grad), (got[1].weight.grad, want[1].weight.grad),
+                  (got[1].bias.grad, want[1].bias.grad)]
+    for got, want in pairs:
+        g, w = got.cpu().double(), want.detach()
+        assert rel_err(g, w) < 1e-2 and _frac_close(g, w, TOL) >= 0.99, (rel_err(g, w), _frac_close(g, w, TOL))
+
+
+def test_edge_mlp_eval_matches_reference(cuda):
+    from dgx import synth
+    from dgx.edgemlp import edge_mlp2
+    B, N, k = 2, 300, 16
+    conv1, conv2 = _convs(5)
+    ref1, ref2 = _convs(5)
+    for blk in (conv1, conv2, ref1, ref2):
+        with torch.no_grad():
+            blk[1].running_mean.copy_(torch.linspace(-0.3, 0.3, blk[1].running_mean.numel()))
+            blk[1].running_var.copy_(torch.linspace(0.5, 2.0, blk[1].running_var.numel()))
+    ref1, ref2 = ref1.double().eval(), ref2.double().eval()
+    conv1, conv2 = conv1.to(cuda).eval(), conv2.to(cuda).eval()
+    pts = synth.cube_clouds(B, N, 3)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1)
+    with torch.no_grad():
+        y = edge_mlp2(x, k, conv1, conv2, False)
+        idx = oracle.knn(torch.from_numpy(pts).permute(0, 2, 1), k)
+        ref = _reference(torch.from_numpy(pts).double().permute(0, 2, 1), torch.as_tensor(idx).long(), ref1, ref2)
+    assert rel_err(y.cpu(), ref) < TOL
+
+
+def test_edge_mlp_bf16_mode(cuda):
+    """bf16 GEMM operands (h1, dZ2 rounded to bf16, z2 stored bf16): within
+    bf16 operand rounding (3e-2) of the fp64 reference."""
+    from dgx import precision, synth
+    from dgx.edgemlp import edge_mlp2
+    B, N, k = 2, 512, 20
+    conv1, conv2 = _convs(21)
+    ref1, ref2 = _convs(21)
+    ref1, ref2 = ref1.double().train(), ref2.double().train()
+    conv1, conv2 = conv1.to(cuda).train(), conv2.to(cuda).train()
+    pts = synth.cube_clouds(B, N, 8)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1).requires_grad_(True)
+    gout = torch.from_numpy(synth.uniform(10, (B, 128, N)) - 0.5).float()
+    precision.set("bf16")
+    try:
+        y = edge_mlp2(x, k, conv1, conv2, True)
+        y.backward(gout.to(cuda))
+    finally:
+        precision.set("fp32")
+    x64 = torch.from_numpy(pts).double().permute(0, 2, 1).requires_grad_(True)
+    idx = oracle.knn(torch.from_numpy(pts).permute(0, 2, 1), k)
+    ref = _reference(x64, torch.as_tensor(idx).long(), ref1, ref2)
+    ref.backward(gout.double())
+    assert rel_err(y.detach().cpu(), ref.detach()) < 3e-2
+    # z2 is stored bf16 (8-bit mantissa): the max over k routes a point's gradient
+    # through a different, equally valid slot wherever bf16 rounding ties or
+    # reorders near-equal edge values, so the per-point input gradient is compared
+    # normwise; the parameter gradients sum over all edges and stay within bf16
+    # operand rounding
+    def fro(g, w):
+        return float((g - w).norm() / w.norm())
+    errs = {n: fro(got.cpu().double(), want.detach()) for n, got, want in (
+        ("x", x.grad, x64.grad), ("w1", conv1[0].weight.grad, ref1[0].weight.grad),
+        ("g1", conv1[1].weight.grad, ref1[1].weight.grad), ("w2", conv2[0].weight.grad, ref2[0].weight.grad),
+        ("g2", conv2[1].weight.grad, ref2[1].weight.grad), ("b2", conv2[1].bias.grad, ref2[1].bias.grad))}
+    assert errs["x"] < 0.25 and all(v < 0.1 for n, v in errs.items() if n != "x"), errs
+
+
+def test_edge_mlp_bf16_kernels_equal_fp32_kernels(cuda):
+    """The bf16 variants of the edge-MLP kernels compute exactly what the fp32
+    variants compute, rounded once (RNE) where they store: with the fp32 mode's
+    1e-3 parity above, the bf16 mode differs from it only by operand rounding."""
+    from dgx import _native as nat
+    from dgx.ops import knn_raw, reduction_order
+    L = nat.lib()
+    B, N, k, C1, C2 = 2, 200, 12, 64, 128
+    M, E = B * N, B * N * k
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.rand(B, 3, N, generator=g).to(cuda)
+    idx = knn_raw(x, k, order=reduction_order(x), out_dtype=torch.int32)
+    PQ = torch.randn(M, 2 * C1, generator=g).to(cuda)
+    sc1, sh1 = torch.randn(C1, generator=g).to(cuda), torch.randn(C1, generator=g).to(cuda)
+    st = nat.stream_of(x)
+    h32 = torch.empty(E, C1, device=cuda)
+    h16 = torch.empty(E, C1, device=cuda, dtype=torch.bfloat16)
+    for out, flag in ((h32, 0), (h16, 1)):
+        nat.check(L.dgx_edge_mlp_h1_f32(nat.ptr(PQ), 2 * C1, nat.ptr(idx), B, N, k, C1, nat.ptr(sc1), nat.ptr(sh1),
+                                        0.2, nat.ptr(out), flag, st), "h1")
+    assert torch.equal(h32.to(torch.bfloat16), h16)
+    # the fp32 h1 itself: LReLU(a (P_j + Q_i) + b) on the engine's neighbour sets
+    il = idx.long().view(M, k) + (torch.arange(M, device=cuda) // N * N).view(M, 1)
+    y = PQ[il.reshape(-1), :C1] + PQ[:, C1:].repeat_interleave(k, dim=0)
+    z = torch.addcmul(sh1, sc1, y)
+    assert rel_err(h32.cpu(), torch.where(z > 0, z, 0.2 * z).cpu()) < 1e-6
+    # max over k: bf16 Z vs the same values in fp32 -> identical selection
+    z16 = torch.randn(E, C2, generator=g).to(cuda).to(torch.bfloat16)
+    sc2 = torch.randn(C2, generator=g).to(cuda)
+    sel = [torch.empty(M, C2, device=cuda) for _ in range(2)]
+    arg = [torch.empty(M, C2, device=cuda, dtype=torch.uint8) for _ in range(2)]
+    for i, (zz, flag) in enumerate(((z16.float().contiguous(), 0), (z16, 1))):
+        nat.check(L.dgx_edge_mlp_max_f32(nat.ptr(zz), flag, B, N, k, C2, nat.ptr(sc2), nat.ptr(sel[i]),
+                                         nat.ptr(arg[i]), st), "max")
+    assert torch.equal(sel[0], sel[1]) and torch.equal(arg[0], arg[1])
+    zf = z16.float().view(M, k, C2)
+    want = torch.where(sc2 < 0, zf.min(dim=1)[0], zf.max(dim=1)[0])
+    assert torch.equal(sel[0], want)
+    assert torch.equal(torch.gather(zf, 1, arg[0].long().unsqueeze(1)).squeeze(1), want)
+    # dense BN2 backward: bf16 in/out == fp32 in/out rounded
+    dzp = torch.randn(M, C2, generator=g).to(cuda)
+    dzp = (dzp.view(torch.int32) & ~63 | torch.randint(0, k, (M, C2), generator=g).to(cuda).int()).view(torch.float32)
+    c0, c1 = torch.randn(C2, generator=g).to(cuda), torch.randn(C2, generator=g).to(cuda)
+    d32 = torch.empty(E, C2, device=cuda)
+    d16 = torch.empty(E, C2, device=cuda, dtype=torch.bfloat16)
+    for zz, out, flag in ((z16.float().contiguous(), d32, 0), (z16, d16, 1)):
+        nat.check(L.dgx_edge_mlp_dz_f32(nat.ptr(dzp), nat.ptr(zz), flag, B, N, k, C2, nat.ptr(sc2), nat.ptr(c0),
+                                        nat.ptr(c1), nat.ptr(out), st), "dz2")
+    assert torch.equal(d32.to(torch.bfloat16), d16)
+    slot = (dzp.view(torch.int32) & 63).long()
+    dzv = (dzp.view(torch.int32) & ~63).view(torch.float32)
+    hit = slot.unsqueeze(1) == torch.arange(k, device=cuda).view(1, k, 1)
+    ref = torch.addcmul(c0, c1, zf) + torch.where(hit, sc2 * dzv.unsqueeze(1), torch.zeros((), device=cuda))
+    assert rel_err(d32.view(M, k, C2).cpu(), ref.cpu()) < 1e-6
+
+
+def test_edge_mlp_rejects_cpu_and_bad_shapes(cuda):
+    from dgx.edgemlp import edge_mlp2
+    conv1, conv2 = _convs(1)
+    with pytest.raises(RuntimeError):
+        edge_mlp2(torch.zeros(1, 3, 64), 8, conv1, conv2, True)  # CPU tensor: no fallback
+    conv1, conv2 = conv1.to(cuda), conv2.to(cuda)
+    with pytest.raises(RuntimeError):
+        edge_mlp2(torch.zeros(1, 4, 64, device=cuda), 8, conv1, conv2, True)  # conv1 expects 2*3 channels
