@@ -63,6 +63,8 @@ def parse():
                    help="GEMM operand precision (BASELINE cfg2 is bf16; fp32 is the parity mode)")
     p.add_argument("--no-fp32-leg", action="store_true", help="skip the extra fp32-mode timing")
     p.add_argument("--no-edgeconv-leg", action="store_true", help="skip the EdgeConv-only fwd+bwd timing")
+    p.add_argument("--no-posemb-leg", action="store_true",
+                   help="skip the PositionEmbedding edge-MLP timing (partseg geometry)")
     p.add_argument("--sync-bn", action="store_true",
                    help="N>1: SyncBatchNorm (global-batch BN statistics, main_partseg_dist.py:189) instead of "
                         "per-replica BN (main_cls.py:62 DataParallel semantics)")
@@ -178,6 +180,58 @@ def eager_reference_step_ms(x, k, emb, reps=5):
     torch.cuda.synchronize()
     del F
     return (time.perf_counter() - t0) / reps * 1e3
+
+
+def posemb_edge_leg(dev, B=32, N=2048, k=40, reps=5):
+    """a6: PositionEmbedding's edge stage (reference models/layers.py:45-52:
+    get_graph_feature -> conv1 -> conv2 -> max over k), fwd+bwd, at the partseg
+    geometry (BASELINE cfg4 per GPU: B 32, N 2048, k 40): the engine's fused op
+    (dgx.edgemlp) next to the reference's op sequence in PyTorch-ROCm eager."""
+    import torch.nn as nn
+    from dgx.edgemlp import edge_mlp2
+    from models.dgcnn import get_graph_feature  # noqa: F401
+    torch.manual_seed(1)
+
+    def blocks():
+        return (nn.Sequential(nn.Conv2d(6, 64, 1, bias=False), nn.BatchNorm2d(64), nn.LeakyReLU(0.2)).to(dev),
+                nn.Sequential(nn.Conv2d(64, 128, 1, bias=False), nn.BatchNorm2d(128), nn.LeakyReLU(0.2)).to(dev))
+    x = (torch.rand(B, 3, N, device=dev) * 2 - 1).requires_grad_(True)
+    g = torch.randn(B, 128, N, device=dev)
+    c1, c2 = blocks()
+
+    def engine():
+        edge_mlp2(x, k, c1, c2, True).backward(g)
+
+    def eager():
+        B_, C, N_ = x.shape
+        inner = -2 * torch.matmul(x.transpose(2, 1).contiguous(), x)
+        xx = torch.sum(x ** 2, dim=1, keepdim=True)
+        idx = (-xx - inner - xx.transpose(2, 1).contiguous()).topk(k=k, dim=-1)[1]
+        idx = (idx + torch.arange(B_, device=dev).view(-1, 1, 1) * N_).view(-1)
+        rows = x.transpose(2, 1).contiguous()
+        nb = rows.view(B_ * N_, -1)[idx, :].view(B_, N_, k, C)
+        ctr = rows.view(B_, N_, 1, C).repeat(1, 1, k, 1)
+        e = torch.cat((nb, ctr), dim=3).permute(0, 3, 1, 2).contiguous()
+        e1, e2 = eager_blocks
+        e2(e1(e)).max(dim=-1)[0].backward(g)
+    eager_blocks = blocks()
+
+    def ms(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+    out = {"config": f"B={B} N={N} k={k}, conv 6->64->128, train-mode BN, fwd+bwd"}
+    out["engine_ms"] = round(ms(engine), 3)
+    try:
+        out["torch_eager_gpu_ms"] = round(ms(eager), 2)
+        out["speedup"] = round(out["torch_eager_gpu_ms"] / out["engine_ms"], 2)
+    except RuntimeError as e:
+        out["torch_eager_gpu_ms"] = {"error": str(e)[:200]}
+    return out
 
 
 def cpu_baseline(args):
@@ -342,6 +396,8 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_edgeconv_leg:
             result["edgeconv_fwd_bwd_ms"] = round(edgeconv_only_ms(model, x), 3)
+        if not args.no_posemb_leg:
+            result["posemb_edge_mlp"] = posemb_edge_leg(dev)
         if not args.no_eager_baseline:
             try:
                 ms = eager_reference_step_ms(x, args.k, args.emb)

@@ -17,7 +17,7 @@
 //   mlp_max_kernel       max_k (min_k where a2 < 0) of z2 and its slot
 //   mlp_dz2_kernel       dZ2 = a2 dz [slot] + c0 + c1 z2 (BN2 backward), dense
 //   mlp_h1_bwd_kernel    g = dH1 * LReLU'(z1) in place + BN1-backward partials
-//   mlp_h1_scatter_kernel dP_j / dQ_i from g over the kNN graph and its reverse
+//   mlp_h1_scatter_kernel dP_j / dQ_i from g over the edge rows and the reverse kNN graph
 #include "common.h"
 
 namespace {
@@ -27,6 +27,13 @@ constexpr int EM_THREADS = 256;
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+// 8 consecutive floats as two float4 loads into v[0..7]
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+    const float4 a = ld4(p), b = ld4(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 
 __device__ __forceinline__ float4 ld4_any(const void* base, int64_t off, bool b16) {
     if (b16) {
@@ -95,6 +102,7 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restr
         float4 best = ld4_any(Z, i * k * C2 + c, IN16);
         float bv[4] = {best.x, best.y, best.z, best.w};
         int bs[4] = {0, 0, 0, 0};
+#pragma unroll 4
         for (int s = 1; s < k; ++s) {
             const float4 v = ld4_any(Z, (i * k + s) * C2 + c, IN16);
 #pragma unroll
@@ -111,31 +119,49 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restr
 }
 
 // BN2 backward, dense over edges: dZ2[e][c] = a_c dz_i[c] [s == slot_i[c]] + c0_c + c1_c z2[e][c].
+// 8 channels per thread (16-byte bf16 rows / two float4), one edge row per
+// thread-group of C2/8 lanes.
 template <bool IO16>
 __global__ __launch_bounds__(EM_THREADS) void mlp_dz2_kernel(const float* __restrict__ dzp, const void* __restrict__ Z,
                                                              int64_t M, int k, int C2, const float* __restrict__ scale,
                                                              const float* __restrict__ c0,
                                                              const float* __restrict__ c1, void* __restrict__ dZ) {
-    const int cq = C2 >> 2;
-    const int64_t total = M * k * cq;
+    const int co = C2 >> 3;
+    const int64_t total = M * k * co;
     for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * EM_THREADS) {
-        const int c = (int)(t % cq) * 4;
-        const int64_t e = t / cq;
+        const int c = (int)(t % co) * 8;
+        const int64_t e = t / co;
         const int64_t i = e / k;
         const int s = (int)(e - i * k);
-        const float4 z = ld4_any(Z, e * C2 + c, IO16);
-        const float4 d = ld4(dzp + i * C2 + c);
-        const float4 a = ld4(scale + c), k0 = ld4(c0 + c), k1 = ld4(c1 + c);
-        float r[4];
+        float z[8], d[8], a[8], k0[8], k1[8];
+        if (IO16) {
+            const bf16x8_t h = *reinterpret_cast<const bf16x8_t*>(static_cast<const __bf16*>(Z) + e * C2 + c);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float v = fmaf(comp(k1, u), comp(z, u), comp(k0, u));
-            const float du = comp(d, u);
-            if (unpack_slot(du) == s) v = fmaf(comp(a, u), unpack_dz(du), v);
+            for (int u = 0; u < 8; ++u) z[u] = (float)h[u];
+        } else {
+            ld8(static_cast<const float*>(Z) + e * C2 + c, z);
+        }
+        ld8(dzp + i * C2 + c, d);
+        ld8(scale + c, a);
+        ld8(c0 + c, k0);
+        ld8(c1 + c, k1);
+        float r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            float v = fmaf(k1[u], z[u], k0[u]);
+            if (unpack_slot(d[u]) == s) v = fmaf(a[u], unpack_dz(d[u]), v);
             r[u] = v;
         }
-        st4_any(dZ, e * C2 + c, make_float4(r[0], r[1], r[2], r[3]), IO16);
+        if (IO16) {
+            bf16x8_t h;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) h[u] = (__bf16)r[u];
+            *reinterpret_cast<bf16x8_t*>(static_cast<__bf16*>(dZ) + e * C2 + c) = h;
+        } else {
+            *reinterpret_cast<float4*>(static_cast<float*>(dZ) + e * C2 + c) = make_float4(r[0], r[1], r[2], r[3]);
+            *reinterpret_cast<float4*>(static_cast<float*>(dZ) + e * C2 + c + 4) = make_float4(r[4], r[5], r[6], r[7]);
+        }
     }
 }
 
@@ -198,36 +224,61 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_bwd_kernel(
 // BN1 backward, second half, one wave per point p (lanes = channels):
 //   dy_e = a g_e + c0 + c1 (P_j + Q_i) for edge e = (i, s), j = idx[e]
 //   dQ_p = sum over p's own k edges of dy,  dP_p = sum over p's in-edges of dy
-// (in-edges from dgx_graph_reverse: id = (i << 6) | s, sorted lists).
+// (in-edges from dgx_graph_reverse: id = (i << 6) | s, sorted lists; sumP_p =
+// sum_s P_j from the BN1-statistics gather). The row loads are issued EM_U at
+// a time into separate accumulators so several HBM/L2 requests are in flight
+// per wave (the loop is latency-bound otherwise); the combination order is
+// fixed, so the result is deterministic.
+constexpr int EM_U = 8;
 __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
-    const float* __restrict__ g, const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx,
-    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges, int64_t M, int N, int k, int C1,
+    const float* __restrict__ g, const float* __restrict__ PQ, int ldpq, const float* __restrict__ sumP,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges, int64_t M, int k, int C1,
     const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
     float* __restrict__ dPQ) {
     const int lane = threadIdx.x & 63;
     const int64_t p = (int64_t)blockIdx.x * (EM_THREADS / 64) + (threadIdx.x >> 6);
     if (p >= M) return;
-    const int64_t base = (p / N) * N;
     const int32_t beg = rowptr[p], end = rowptr[p + 1];
     const float kf = (float)k, deg = (float)(end - beg);
     for (int c = lane; c < C1; c += 64) {
         const float a = scale[c], k0 = c0[c], k1 = c1[c];
-        float sg = 0.f, sp = 0.f;
-        for (int s = 0; s < k; ++s) {
-            const int64_t e = p * k + s;
-            sg += g[e * C1 + c];
-            sp += PQ[(base + idx[e]) * ldpq + c];
+        const float* __restrict__ gp = g + p * k * C1 + c;
+        float sgv[EM_U];
+#pragma unroll
+        for (int u = 0; u < EM_U; ++u) sgv[u] = 0.f;
+        int s = 0;
+        for (; s + EM_U <= k; s += EM_U) {
+#pragma unroll
+            for (int u = 0; u < EM_U; ++u) sgv[u] += gp[(int64_t)(s + u) * C1];
         }
-        float ig = 0.f, iq = 0.f;
-        for (int32_t r = beg; r < end; ++r) {
+        for (; s < k; ++s) sgv[0] += gp[(int64_t)s * C1];
+        float igv[EM_U], iqv[EM_U];
+#pragma unroll
+        for (int u = 0; u < EM_U; ++u) { igv[u] = 0.f; iqv[u] = 0.f; }
+        int32_t r = beg;
+        for (; r + EM_U <= end; r += EM_U) {
+            int32_t id[EM_U];
+#pragma unroll
+            for (int u = 0; u < EM_U; ++u) id[u] = edges[r + u];
+#pragma unroll
+            for (int u = 0; u < EM_U; ++u) {
+                const int64_t src = (int64_t)(id[u] >> 6);
+                igv[u] += g[(src * k + (id[u] & 63)) * C1 + c];
+                iqv[u] += PQ[src * ldpq + C1 + c];
+            }
+        }
+        for (; r < end; ++r) {
             const int32_t id = edges[r];
             const int64_t src = (int64_t)(id >> 6);
-            ig += g[(src * k + (id & 63)) * C1 + c];
-            iq += PQ[src * ldpq + C1 + c];
+            igv[0] += g[(src * k + (id & 63)) * C1 + c];
+            iqv[0] += PQ[src * ldpq + C1 + c];
         }
+        float sg = 0.f, ig = 0.f, iq = 0.f;
+#pragma unroll
+        for (int u = 0; u < EM_U; ++u) { sg += sgv[u]; ig += igv[u]; iq += iqv[u]; }
         const float Pp = PQ[p * ldpq + c], Qp = PQ[p * ldpq + C1 + c];
         dPQ[p * 2 * C1 + c] = fmaf(a, ig, fmaf(k0, deg, k1 * fmaf(deg, Pp, iq)));
-        dPQ[p * 2 * C1 + C1 + c] = fmaf(a, sg, fmaf(k0, kf, k1 * fmaf(kf, Qp, sp)));
+        dPQ[p * 2 * C1 + C1 + c] = fmaf(a, sg, fmaf(k0, kf, k1 * fmaf(kf, Qp, sumP[p * C1 + c])));
     }
 }
 
@@ -272,10 +323,10 @@ int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2,
 int dgx_edge_mlp_dz_f32(const float* dzp, const void* Z, int bf16, int B, int N, int k, int C2, const float* scale,
                         const float* c0, const float* c1, void* dZ, void* stream) {
     if (!dzp || !Z || !scale || !c0 || !c1 || !dZ || B < 1 || N < 1 || k < 1 || k > 64 || C2 < 4) return DGX_EINVAL;
-    if (C2 % 4 || !al16(dzp) || !al16(Z) || !al16(dZ) || !al16(scale) || !al16(c0) || !al16(c1))
+    if (C2 % 8 || !al16(dzp) || !al16(Z) || !al16(dZ) || !al16(scale) || !al16(c0) || !al16(c1))
         return DGX_EUNSUPPORTED;
     const int64_t M = (int64_t)B * N;
-    const int grid = grid_of(M * k * (C2 / 4), EM_THREADS);
+    const int grid = grid_of(M * k * (C2 / 8), EM_THREADS);
     if (bf16)
         hipLaunchKernelGGL(mlp_dz2_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dzp, Z, M, k, C2,
                            scale, c0, c1, dZ);
@@ -309,17 +360,17 @@ int dgx_edge_mlp_h1_bwd_f32(float* dH, const float* PQ, int ldpq, const int32_t*
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const int32_t* idx, const int32_t* rowptr,
+int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const float* sumP, const int32_t* rowptr,
                              const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
                              const float* c1, float* dPQ, void* stream) {
-    if (!g || !PQ || !idx || !rowptr || !edges || !scale || !c0 || !c1 || !dPQ || B < 1 || N < 1 || k < 1 ||
+    if (!g || !PQ || !sumP || !rowptr || !edges || !scale || !c0 || !c1 || !dPQ || B < 1 || N < 1 || k < 1 ||
         k > 64 || C1 < 1 || ldpq < 2 * C1)
         return DGX_EINVAL;
     const int64_t M = (int64_t)B * N;
     const int64_t blocks = (M + EM_THREADS / 64 - 1) / (EM_THREADS / 64);
     if (blocks > 0x7fffffff) return DGX_EUNSUPPORTED;
     hipLaunchKernelGGL(mlp_h1_scatter_kernel, dim3((unsigned)blocks), dim3(EM_THREADS), 0, dgx_stream(stream), g, PQ,
-                       ldpq, idx, rowptr, edges, M, N, k, C1, scale, c0, c1, dPQ);
+                       ldpq, sumP, rowptr, edges, M, k, C1, scale, c0, c1, dPQ);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -95,6 +95,7 @@ class _EdgeMLP2(torch.autograd.Function):
         use1 = training or bn1.running_mean is None
         use2 = training or bn2.running_mean is None
         st1 = st2 = None
+        sumP1 = None
         with torch.cuda.device(dev):
             # ---- conv1: BN1 statistics over all E edges, then h1 per edge row
             if use1:
@@ -106,7 +107,7 @@ class _EdgeMLP2(torch.autograd.Function):
                 nat.check(L.dgx_edge_fwd_gather_f32(nat.ptr(PQ), 2 * C1, nat.ptr(idx), B, N, k, C1, nat.ptr(g1),
                                                     nat.ptr(ysel1), nat.ptr(arg1), nat.ptr(sumP1), nat.ptr(part1),
                                                     prow, stream), "edge gather (bn1 stats)")
-                del ysel1, arg1, sumP1
+                del ysel1, arg1  # only the statistics and sum_k P_j (for dQ) are used
                 st1 = _bn_forward(L, dev, stream, part1, prow, float(E), bn1, g1, b1, training)
                 scale1, shift1 = st1[0], st1[1]
             else:
@@ -151,7 +152,8 @@ class _EdgeMLP2(torch.autograd.Function):
         ctx.slopes = (float(slope1), float(slope2))
         ctx.st = (st1, st2)
         ctx.wprep = wprep
-        ctx.save_for_backward(X, idx, PQ, H1, Z2, ysel, arg, w1, w2)
+        ctx.bf16 = bf16
+        ctx.save_for_backward(X, idx, PQ, sumP1, H1, Z2, ysel, arg, w1, w2)
         return out.view(B, N, C2).permute(0, 2, 1)
 
     @staticmethod
@@ -159,7 +161,7 @@ class _EdgeMLP2(torch.autograd.Function):
         st1, st2 = ctx.st
         if st1 is None or st2 is None:
             raise RuntimeError("dgx edge MLP: backward through an eval-mode (running-stats) forward is not supported")
-        X, idx, PQ, H1, Z2, ysel, arg, w1, w2 = ctx.saved_tensors
+        X, idx, PQ, sumP1, H1, Z2, ysel, arg, w1, w2 = ctx.saved_tensors
         B, C, N, k, C1, C2 = ctx.dims
         slope1, slope2 = ctx.slopes
         M, E = B * N, B * N * k
@@ -203,15 +205,22 @@ class _EdgeMLP2(torch.autograd.Function):
             nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges), stream),
                       "reverse graph")
             dPQ = torch.empty((M, 2 * C1), dtype=torch.float32, device=dev)
-            nat.check(L.dgx_edge_mlp_scatter_f32(nat.ptr(dH1), nat.ptr(PQ), 2 * C1, nat.ptr(idx), nat.ptr(rowptr),
+            nat.check(L.dgx_edge_mlp_scatter_f32(nat.ptr(dH1), nat.ptr(PQ), 2 * C1, nat.ptr(sumP1), nat.ptr(rowptr),
                                                  nat.ptr(edges), B, N, k, C1, nat.ptr(scale1), nat.ptr(e0),
                                                  nat.ptr(e1), nat.ptr(dPQ), stream), "edge h1 scatter")
         # ---- conv1 (K = C, tiny): dW1 = [dP^T X | dQ^T X], dX = dP W1a + dQ W1b
-        dwcat = prec.mm(dPQ.t(), X)  # (2C1, C)
-        gw1 = torch.cat([dwcat[:C1], dwcat[C1:]], dim=1).reshape(w1.shape)
         dx = None
-        if ctx.needs_input_grad[0]:
-            dx = prec.mm(dPQ, _split_weight(w1, C, C1)).view(B, N, C).permute(0, 2, 1)
+        if ctx.bf16:  # the engine's GEMMs (split-K over the M rows, un-stacked in the slab sum)
+            gw1 = torch.empty((C1, 2 * C), dtype=torch.float32, device=dev)
+            G.mm_atb(dPQ, X, gw1, split_rows=C1)
+            gw1 = gw1.view(w1.shape)
+            if ctx.needs_input_grad[0]:
+                dx = G.mm_xw(dPQ, _split_weight(w1, C, C1)).view(B, N, C).permute(0, 2, 1)
+        else:
+            dwcat = prec.mm(dPQ.t(), X)  # (2C1, C)
+            gw1 = torch.cat([dwcat[:C1], dwcat[C1:]], dim=1).reshape(w1.shape)
+            if ctx.needs_input_grad[0]:
+                dx = prec.mm(dPQ, _split_weight(w1, C, C1)).view(B, N, C).permute(0, 2, 1)
         return (dx, None, None, None, None, None, None, gw1, dg1, db1, gw2.view(w2.shape), dg2, db2)
 
 

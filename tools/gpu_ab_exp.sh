@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eager-baseline --no-fp32-leg --no-edgeconv-leg"
+B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eager-baseline --no-fp32-leg --no-edgeconv-leg --no-posemb-leg"
 for e in 1 2; do
     DGX_LIB=$PWD/tools/libdgx_exp$e.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/exp$e -o e \
         --output-format csv -- $B > gpurun_out/exp$e.log 2>&1 || exit $?

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/pmcb
 mkdir -p $OUT
 export PYTHONDONTWRITEBYTECODE=1
-CMD="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-eager-baseline --no-fp32-leg --no-edgeconv-leg"
+CMD="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-eager-baseline --no-fp32-leg --no-edgeconv-leg --no-posemb-leg"
 pass() {
     local name=$1; shift
     timeout -s KILL 180 rocprofv3 --pmc "$@" --kernel-trace -d $OUT/$name -o $name --output-format csv -- $CMD \

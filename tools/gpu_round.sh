@@ -24,6 +24,6 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-eager-baseline --no-fp32-leg --no-edgeconv-leg
+        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-eager-baseline --no-fp32-leg --no-edgeconv-leg --no-posemb-leg
 fi
 echo "=== done"
