@@ -17,8 +17,6 @@ Backward per block (reverse order):
     reverse kNN graph + dPQ                   HIP
     dX += dPQ [W1; W2], dW = dPQ^T X          GEMM (accumulated into xcat's grad)
 """
-import ctypes
-
 import torch
 
 from . import _native as nat
@@ -47,42 +45,19 @@ def _bn_factor(bn):
     return float(bn.momentum), bn.num_batches_tracked
 
 
-_side_streams = {}
-
-
-def _side_stream(dev):
-    """One auxiliary HIP stream per device for work that only feeds the backward."""
-    s = _side_streams.get(dev)
-    if s is None:
-        s = _side_streams[dev] = torch.cuda.Stream(dev)
-    return s
-
-
-def _reverse_graph_async(idx, B, N, k, side, dev):
-    """Reverse kNN graph (CSR of in-edges, dgx_graph_reverse) of one block.
-    With a side stream: launched there after the current stream's work up to
-    now (the kNN that produced idx), returning (rowptr, edges, ready_event);
-    the consumer waits on the event. Without: on the current stream."""
+def _reverse_graph(idx, B, N, k, dev):
+    """Reverse kNN graph (CSR of in-edges, dgx_graph_reverse) of one block, on
+    the current stream. Built in the backward, right before its consumer: a
+    build on a side stream overlapping the forward measured slower (1.63 vs
+    1.56 ms/step at cfg2; the concurrent kernels contend for the L2 the kNN
+    operand images live in)."""
     M = B * N
     rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
     edges = torch.empty(M * k, dtype=torch.int32, device=dev)
-    L = nat.lib()
-    if side is None:
-        with torch.cuda.device(dev):
-            nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
-                                          nat.stream_of(idx)), "reverse graph")
-        return rowptr, edges, None
-    main = torch.cuda.current_stream(dev)
-    side.wait_stream(main)
-    with torch.cuda.device(dev), torch.cuda.stream(side):
-        nat.check(L.dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
-                                      ctypes.c_void_p(side.cuda_stream)), "reverse graph")
-        ready = torch.cuda.Event()
-        ready.record(side)
-    # allocator bookkeeping: these buffers are used on the side stream too
-    for t in (idx, rowptr, edges):
-        t.record_stream(side)
-    return rowptr, edges, ready
+    with torch.cuda.device(dev):
+        nat.check(nat.lib().dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
+                                              nat.stream_of(idx)), "reverse graph")
+    return rowptr, edges
 
 
 class _Layer:
@@ -118,11 +93,6 @@ class _EdgeConvStack(torch.autograd.Function):
         off_in = None
         count = float(M * k)
         have16 = False  # xcat16 holds the previous block's output
-        # The backward's reverse kNN graphs depend only on each block's indices:
-        # they are built on a side stream as soon as the indices exist, so they
-        # overlap the rest of the forward (and conv5's backward).
-        want_bwd = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
-        side = _side_stream(dev) if want_bwd and training else None
         # bf16 [W1;W2] and transposed copies of blocks 2.. in one launch (used when
         # the block's input is the bf16 twin, i.e. after a batch-statistics block)
         preps = list(ctx_preps) if ctx_preps is not None else [None] * len(layers)
@@ -141,9 +111,6 @@ class _EdgeConvStack(torch.autograd.Function):
                 # dim -1 of a contiguous tensor), hence the strided rounding order
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
                               strides=(N * total, 1, total), shape=(B, cin, N))
-            graph = None
-            if want_bwd and training:
-                graph = _reverse_graph_async(idx, B, N, k, side, dev)
             wprep = None
             if bf16:
                 X16 = xcat16[:, off_in:off_in + cin] if li > 0 else None
@@ -191,8 +158,8 @@ class _EdgeConvStack(torch.autograd.Function):
                                                        float(ly.slope), nat.ptr(out), total, nat.ptr(out16), stream),
                               "bn apply")
                     have16 = bf16
-                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group if sync else None,
-                                  graph))
+                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep,
+                                  group if sync else None))
                     if _debug is not None:
                         # sign of fmaf(scale, ysel, shift) as the kernels evaluate it: the fp64
                         # product of two fp32 values is exact, so this sign is fma's sign
@@ -253,12 +220,8 @@ class _EdgeConvStack(torch.autograd.Function):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
             w = params[3 * li]
-            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group, graph = ctx.layer_state[li]
-            if graph is None:  # forward ran without a pending backward (e.g. under no_grad + enable_grad)
-                graph = _reverse_graph_async(idx, B, N, k, None, dev)
-            rowptr, edges, ready = graph
-            if ready is not None:
-                torch.cuda.current_stream(dev).wait_event(ready)
+            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group = ctx.layer_state[li]
+            rowptr, edges = _reverse_graph(idx, B, N, k, dev)
             off = sum(widths[:li])
             prev = off - widths[li - 1] if li > 0 else None
             X = x_pm if li == 0 else xcat[:, prev: prev + cin]
