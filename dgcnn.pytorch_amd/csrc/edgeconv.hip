@@ -802,6 +802,7 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
 // work (edge-id decode, addresses, 16-B LDS reads of Q_i and dz_i) is shared
 // by CS channels. In-edge lists and row pointers are read from HBM/L2 directly
 // (contiguous per point, consecutive points -> consecutive ranges).
+constexpr int BW_EB = 16;  // in-edge ids loaded per batch (edge_bwd_wide_kernel)
 template <int CS, bool OUT16>
 __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
@@ -864,15 +865,16 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
                 sd[u] += (__float_as_uint(d[u]) & 63u) == slot ? unpack_dz(d[u]) : 0.f;
             }
         };
-        int32_t u0 = beg;
-        for (; u0 + 4 <= end; u0 += 4) {
-            const int4 e4 = make_int4(edges[u0], edges[u0 + 1], edges[u0 + 2], edges[u0 + 3]);
-            edge(e4.x);
-            edge(e4.y);
-            edge(e4.z);
-            edge(e4.w);
+        // in-edge ids EB at a time, all loads issued before the first is used:
+        // one memory latency per EB edges instead of one per 4
+        for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
+            int32_t ids[BW_EB];
+#pragma unroll
+            for (int v = 0; v < BW_EB; ++v) ids[v] = u0 + v < end ? edges[u0 + v] : 0;
+#pragma unroll
+            for (int v = 0; v < BW_EB; ++v)
+                if (u0 + v < end) edge(ids[v]);
         }
-        for (; u0 < end; ++u0) edge(edges[u0]);
         const float deg = (float)(end - beg);
         float qn[CS], dn[CS];
         lds_vec<CS>(qs + n * CS, qn);
