@@ -61,60 +61,96 @@ inline int grid_of(int64_t work, int block) {
     return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
 }
 
-// h1[e][c] = LReLU(fmaf(a_c, P_j[c] + Q_i[c], b_c)), 4 channels per thread.
+// h1[e][c] = LReLU(fmaf(a_c, P_j[c] + Q_i[c], b_c)), 8 channels per thread
+// (two float4 loads of P_j and Q_i, one 16-byte bf16 or two float4 stores).
 template <bool OUT16>
 __global__ __launch_bounds__(EM_THREADS) void mlp_h1_kernel(const float* __restrict__ PQ, int ldpq,
                                                             const int32_t* __restrict__ idx, int N, int k, int C1,
                                                             int64_t E, const float* __restrict__ scale,
                                                             const float* __restrict__ shift, float slope,
                                                             void* __restrict__ H1) {
-    const int cq = C1 >> 2;
-    const int64_t total = E * cq;
+    const int co = C1 >> 3;
+    const int64_t total = E * co;
     for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * EM_THREADS) {
-        const int c = (int)(t % cq) * 4;
-        const int64_t e = t / cq;
+        const int c = (int)(t % co) * 8;
+        const int64_t e = t / co;
         const int64_t i = e / k;
         const int64_t j = (i / N) * N + idx[e];
-        const float4 p = ld4(PQ + j * ldpq + c), q = ld4(PQ + i * ldpq + C1 + c);
-        const float4 a = ld4(scale + c), b = ld4(shift + c);
-        const float4 h = make_float4(lrelu(fmaf(a.x, p.x + q.x, b.x), slope), lrelu(fmaf(a.y, p.y + q.y, b.y), slope),
-                                     lrelu(fmaf(a.z, p.z + q.z, b.z), slope), lrelu(fmaf(a.w, p.w + q.w, b.w), slope));
-        st4_any(H1, e * C1 + c, h, OUT16);
+        float p[8], q[8], a[8], b[8], h[8];
+        ld8(PQ + j * ldpq + c, p);
+        ld8(PQ + i * ldpq + C1 + c, q);
+        ld8(scale + c, a);
+        ld8(shift + c, b);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) h[u] = lrelu(fmaf(a[u], p[u] + q[u], b[u]), slope);
+        if (OUT16) {
+            bf16x8_t o;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = (__bf16)h[u];
+            *reinterpret_cast<bf16x8_t*>(static_cast<__bf16*>(H1) + e * C1 + c) = o;
+        } else {
+            float* dst = static_cast<float*>(H1) + e * C1 + c;
+            *reinterpret_cast<float4*>(dst) = make_float4(h[0], h[1], h[2], h[3]);
+            *reinterpret_cast<float4*>(dst + 4) = make_float4(h[4], h[5], h[6], h[7]);
+        }
+    }
+}
+
+// 8 consecutive values of a fp32 or bf16 row as floats
+template <bool B16>
+__device__ __forceinline__ void ld8_any(const void* base, int64_t off, float* v) {
+    if (B16) {
+        const bf16x8_t h = *reinterpret_cast<const bf16x8_t*>(static_cast<const __bf16*>(base) + off);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (float)h[u];
+    } else {
+        ld8(static_cast<const float*>(base) + off, v);
     }
 }
 
 // ysel[i][c] = max_s z2[i*k+s][c] (min where scale[c] < 0: BN's affine is
 // decreasing there, so LReLU(BN(.)) is maximised by the smallest z), arg = s
-// of the first extremum (the order torch.max keeps on ties).
+// of the first extremum (the order torch.max keeps on ties). 8 channels per
+// thread, 16-byte row loads, EM_MU rows in flight.
+constexpr int EM_MU = 4;
 template <bool IN16>
 __global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restrict__ Z, int64_t M, int k, int C2,
                                                              const float* __restrict__ scale,
                                                              float* __restrict__ ysel, uint8_t* __restrict__ arg) {
-    const int cq = C2 >> 2;
-    const int64_t total = M * cq;
+    const int co = C2 >> 3;
+    const int64_t total = M * co;
     for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * EM_THREADS) {
-        const int c = (int)(t % cq) * 4;
-        const int64_t i = t / cq;
-        const float4 a = ld4(scale + c);
-        const bool mn[4] = {a.x < 0.f, a.y < 0.f, a.z < 0.f, a.w < 0.f};
-        float4 best = ld4_any(Z, i * k * C2 + c, IN16);
-        float bv[4] = {best.x, best.y, best.z, best.w};
-        int bs[4] = {0, 0, 0, 0};
-#pragma unroll 4
-        for (int s = 1; s < k; ++s) {
-            const float4 v = ld4_any(Z, (i * k + s) * C2 + c, IN16);
+        const int c = (int)(t % co) * 8;
+        const int64_t i = t / co;
+        float a[8];
+        ld8(scale + c, a);
+        float bv[8];
+        int bs[8];
+        ld8_any<IN16>(Z, i * k * C2 + c, bv);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float x = comp(v, u);
-                if (mn[u] ? x < bv[u] : x > bv[u]) { bv[u] = x; bs[u] = s; }
+        for (int u = 0; u < 8; ++u) bs[u] = 0;
+        for (int s0 = 1; s0 < k; s0 += EM_MU) {
+            float v[EM_MU][8];
+#pragma unroll
+            for (int m = 0; m < EM_MU; ++m) ld8_any<IN16>(Z, (i * k + min(s0 + m, k - 1)) * C2 + c, v[m]);
+#pragma unroll
+            for (int m = 0; m < EM_MU; ++m) {
+                if (s0 + m >= k) break;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float x = v[m][u];
+                    if (a[u] < 0.f ? x < bv[u] : x > bv[u]) { bv[u] = x; bs[u] = s0 + m; }
+                }
             }
         }
         *reinterpret_cast<float4*>(ysel + i * C2 + c) = make_float4(bv[0], bv[1], bv[2], bv[3]);
-        const uint32_t packed = (uint32_t)bs[0] | ((uint32_t)bs[1] << 8) | ((uint32_t)bs[2] << 16) |
-                                ((uint32_t)bs[3] << 24);
-        *reinterpret_cast<uint32_t*>(arg + i * C2 + c) = packed;
+        *reinterpret_cast<float4*>(ysel + i * C2 + c + 4) = make_float4(bv[4], bv[5], bv[6], bv[7]);
+        uint2 packed;
+        packed.x = (uint32_t)bs[0] | ((uint32_t)bs[1] << 8) | ((uint32_t)bs[2] << 16) | ((uint32_t)bs[3] << 24);
+        packed.y = (uint32_t)bs[4] | ((uint32_t)bs[5] << 8) | ((uint32_t)bs[6] << 16) | ((uint32_t)bs[7] << 24);
+        *reinterpret_cast<uint2*>(arg + i * C2 + c) = packed;
     }
 }
 
@@ -292,9 +328,9 @@ int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, in
                         const float* scale, const float* shift, float slope, void* H1, int out_bf16, void* stream) {
     if (!PQ || !idx || !scale || !shift || !H1 || B < 1 || N < 1 || k < 1 || C1 < 4 || ldpq < 2 * C1)
         return DGX_EINVAL;
-    if (C1 % 4 || ldpq % 4 || !al16(PQ) || !al16(scale) || !al16(shift) || !al16(H1)) return DGX_EUNSUPPORTED;
+    if (C1 % 8 || ldpq % 4 || !al16(PQ) || !al16(scale) || !al16(shift) || !al16(H1)) return DGX_EUNSUPPORTED;
     const int64_t E = (int64_t)B * N * k;
-    const int grid = grid_of(E * (C1 / 4), EM_THREADS);
+    const int grid = grid_of(E * (C1 / 8), EM_THREADS);
     if (out_bf16)
         hipLaunchKernelGGL(mlp_h1_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), PQ, ldpq, idx, N,
                            k, C1, E, scale, shift, slope, H1);
@@ -307,10 +343,10 @@ int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, in
 int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2, const float* scale, float* ysel,
                          uint8_t* arg, void* stream) {
     if (!Z || !scale || !ysel || !arg || B < 1 || N < 1 || k < 1 || k > 64 || C2 < 4) return DGX_EINVAL;
-    if (C2 % 4 || !al16(Z) || !al16(scale) || !al16(ysel) || (reinterpret_cast<uintptr_t>(arg) & 3))
+    if (C2 % 8 || !al16(Z) || !al16(scale) || !al16(ysel) || (reinterpret_cast<uintptr_t>(arg) & 7))
         return DGX_EUNSUPPORTED;
     const int64_t M = (int64_t)B * N;
-    const int grid = grid_of(M * (C2 / 4), EM_THREADS);
+    const int grid = grid_of(M * (C2 / 8), EM_THREADS);
     if (z_bf16)
         hipLaunchKernelGGL(mlp_max_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), Z, M, k, C2,
                            scale, ysel, arg);

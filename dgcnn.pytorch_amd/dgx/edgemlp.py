@@ -236,8 +236,8 @@ def edge_mlp2(x, k, conv1, conv2, training):
     if bn1.weight is None or bn2.weight is None:
         raise NotImplementedError("dgx edge MLP expects affine BatchNorm (as the reference builds it)")
     c1w, c2w = cv1.weight.shape[0], cv2.weight.shape[0]
-    if c1w < 4 or c1w % 4 or 256 % (c1w // 4) or c2w % 8:
-        raise NotImplementedError("dgx edge MLP: conv1 width a multiple of 4 dividing 1024, conv2 width a "
+    if c1w < 8 or c1w % 8 or 256 % (c1w // 4) or c2w % 8:
+        raise NotImplementedError("dgx edge MLP: conv1 width a multiple of 8 dividing 1024, conv2 width a "
                                   "multiple of 8 (PositionEmbedding: 64, 128)")
     if cv1.weight.shape[1] != 2 * x.shape[1]:
         raise RuntimeError(f"dgx edge MLP: conv1 expects {cv1.weight.shape[1]} edge channels, input has C={x.shape[1]}")

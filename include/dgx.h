@@ -274,7 +274,8 @@ int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, cons
  *   dgx_edge_mlp_scatter: dPQ (M x 2C1) fp32, dQ_i = sum over i's edges and
  *     dP_j = sum over j's in-edges (dgx_graph_reverse) of a1 g + c0 + c1 y
  *     (sumP = sum_k P_j per point, as dgx_edge_fwd_gather_f32 writes it).
- * Edge-MLP kernels need C1 % 4 == 0, C2 % 8 == 0 and 16-byte aligned rows. */
+ * Edge-MLP kernels need C1 % 8 == 0 (and C1/4 dividing 256), C2 % 8 == 0 and
+ * 16-byte aligned rows. */
 int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
                         const float* scale, const float* shift, float slope, void* H1, int out_bf16, void* stream);
 int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2, const float* scale, float* ysel,
