@@ -155,48 +155,57 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restr
 }
 
 // BN2 backward, dense over edges: dZ2[e][c] = a_c dz_i[c] [s == slot_i[c]] + c0_c + c1_c z2[e][c].
-// 8 channels per thread (16-byte bf16 rows / two float4), one edge row per
-// thread-group of C2/8 lanes.
+// A thread owns 8 channels of one point: the point's packed dz and the
+// per-channel constants are loaded once, then its k edge rows stream through
+// (16-byte bf16 rows, or two float4).
 template <bool IO16>
 __global__ __launch_bounds__(EM_THREADS) void mlp_dz2_kernel(const float* __restrict__ dzp, const void* __restrict__ Z,
                                                              int64_t M, int k, int C2, const float* __restrict__ scale,
                                                              const float* __restrict__ c0,
                                                              const float* __restrict__ c1, void* __restrict__ dZ) {
     const int co = C2 >> 3;
-    const int64_t total = M * k * co;
+    const int64_t total = M * co;
     for (int64_t t = (int64_t)blockIdx.x * EM_THREADS + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * EM_THREADS) {
         const int c = (int)(t % co) * 8;
-        const int64_t e = t / co;
-        const int64_t i = e / k;
-        const int s = (int)(e - i * k);
-        float z[8], d[8], a[8], k0[8], k1[8];
-        if (IO16) {
-            const bf16x8_t h = *reinterpret_cast<const bf16x8_t*>(static_cast<const __bf16*>(Z) + e * C2 + c);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) z[u] = (float)h[u];
-        } else {
-            ld8(static_cast<const float*>(Z) + e * C2 + c, z);
-        }
+        const int64_t i = t / co;
+        float d[8], a[8], k0[8], k1[8];
         ld8(dzp + i * C2 + c, d);
         ld8(scale + c, a);
         ld8(c0 + c, k0);
         ld8(c1 + c, k1);
-        float r[8];
+        int slot[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            float v = fmaf(k1[u], z[u], k0[u]);
-            if (unpack_slot(d[u]) == s) v = fmaf(a[u], unpack_dz(d[u]), v);
-            r[u] = v;
+            slot[u] = unpack_slot(d[u]);
+            d[u] = a[u] * unpack_dz(d[u]);
         }
-        if (IO16) {
-            bf16x8_t h;
+#pragma unroll 2
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = i * k + s;
+            float z[8], r[8];
+            if (IO16) {
+                const bf16x8_t h = *reinterpret_cast<const bf16x8_t*>(static_cast<const __bf16*>(Z) + e * C2 + c);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) h[u] = (__bf16)r[u];
-            *reinterpret_cast<bf16x8_t*>(static_cast<__bf16*>(dZ) + e * C2 + c) = h;
-        } else {
-            *reinterpret_cast<float4*>(static_cast<float*>(dZ) + e * C2 + c) = make_float4(r[0], r[1], r[2], r[3]);
-            *reinterpret_cast<float4*>(static_cast<float*>(dZ) + e * C2 + c + 4) = make_float4(r[4], r[5], r[6], r[7]);
+                for (int u = 0; u < 8; ++u) z[u] = (float)h[u];
+            } else {
+                ld8(static_cast<const float*>(Z) + e * C2 + c, z);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float v = fmaf(k1[u], z[u], k0[u]);
+                r[u] = slot[u] == s ? v + d[u] : v;
+            }
+            if (IO16) {
+                bf16x8_t h;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) h[u] = (__bf16)r[u];
+                *reinterpret_cast<bf16x8_t*>(static_cast<__bf16*>(dZ) + e * C2 + c) = h;
+            } else {
+                float* dst = static_cast<float*>(dZ) + e * C2 + c;
+                *reinterpret_cast<float4*>(dst) = make_float4(r[0], r[1], r[2], r[3]);
+                *reinterpret_cast<float4*>(dst + 4) = make_float4(r[4], r[5], r[6], r[7]);
+            }
         }
     }
 }
@@ -362,7 +371,7 @@ int dgx_edge_mlp_dz_f32(const float* dzp, const void* Z, int bf16, int B, int N,
     if (C2 % 8 || !al16(dzp) || !al16(Z) || !al16(dZ) || !al16(scale) || !al16(c0) || !al16(c1))
         return DGX_EUNSUPPORTED;
     const int64_t M = (int64_t)B * N;
-    const int grid = grid_of(M * k * (C2 / 8), EM_THREADS);
+    const int grid = grid_of(M * (C2 / 8), EM_THREADS);
     if (bf16)
         hipLaunchKernelGGL(mlp_dz2_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dzp, Z, M, k, C2,
                            scale, c0, c1, dZ);
