@@ -113,7 +113,7 @@ __device__ __forceinline__ void ld8_any(const void* base, int64_t off, float* v)
 // decreasing there, so LReLU(BN(.)) is maximised by the smallest z), arg = s
 // of the first extremum (the order torch.max keeps on ties). 8 channels per
 // thread, 16-byte row loads, EM_MU rows in flight.
-constexpr int EM_MU = 4;
+constexpr int EM_MU = 8;
 template <bool IN16>
 __global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restrict__ Z, int64_t M, int k, int C2,
                                                              const float* __restrict__ scale,
