@@ -19,11 +19,18 @@ def main():
     from dgx import precision as prec
     from dgx import synth
     from models.dgcnn import DGCNN
+    from models.layers import PositionEmbedding
     prec.set(precision)
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    model = DGCNN(types.SimpleNamespace(emb_dim=64, k=10))
-    if mode == "syncbn":
+    posemb = mode.startswith("posemb")
+    if posemb:  # PositionEmbedding (a6) as main_partseg_dist.py converts Net's modules
+        model = PositionEmbedding(types.SimpleNamespace(k=10))
+        with torch.no_grad():
+            model.transform.weight.normal_(0, 0.05)
+    else:
+        model = DGCNN(types.SimpleNamespace(emb_dim=64, k=10))
+    if mode.endswith("syncbn"):
         model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
     model = model.to(dev).train()
     ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
@@ -31,11 +38,12 @@ def main():
     pts = synth.cube_clouds(B * world, 256, 5)[rank * B:(rank + 1) * B]
     x = torch.from_numpy(pts).to(dev).permute(0, 2, 1)
     y = ddp(x)
-    g = torch.from_numpy(synth.uniform(6, (B * world, 64, 256)) - 0.5)[rank * B:(rank + 1) * B].to(dev)
+    co = 3 if posemb else 64
+    g = torch.from_numpy(synth.uniform(6, (B * world, co, 256)) - 0.5)[rank * B:(rank + 1) * B].to(dev)
     (y * g).sum().backward()
     torch.cuda.synchronize()
     res = {"y": y.detach().cpu(),
-           "grads": {n: p.grad.detach().cpu() for n, p in model.named_parameters()},
+           "grads": {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None},
            "running": {n: b.detach().cpu() for n, b in model.named_buffers()}}
     torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()

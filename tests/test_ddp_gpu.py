@@ -80,3 +80,31 @@ def test_ddp_plain_bn_is_per_replica(cuda, tmp_path):
     for n in shards[0]["grads"]:
         mean = (shards[0]["grads"][n] + shards[1]["grads"][n]) / 2
         assert rel_err(ranks[0]["grads"][n], mean) < 1e-4, n
+
+
+def test_ddp_syncbn_position_embedding_matches_full_batch(cuda, tmp_path):
+    """a6 under SyncBatchNorm: the edge MLP's BN1/BN2 statistics (and their
+    backward sums) are all-reduced by the engine; the rest of the block is
+    torch's SyncBatchNorm. Each rank must equal its half of the full batch."""
+    from dgx import synth
+    from models.layers import PositionEmbedding
+    ranks = _run_ranks(tmp_path, "posemb_syncbn")
+    torch.manual_seed(0)
+    m = PositionEmbedding(types.SimpleNamespace(k=10))
+    with torch.no_grad():
+        m.transform.weight.normal_(0, 0.05)
+    m = m.to(cuda).train()
+    x = torch.from_numpy(synth.cube_clouds(4, 256, 5)).to(cuda).permute(0, 2, 1)
+    g = torch.from_numpy(synth.uniform(6, (4, 3, 256)) - 0.5).to(cuda)
+    y = m(x)
+    (y * g).sum().backward()
+    for r in range(2):
+        assert rel_err(ranks[r]["y"], y.detach().cpu()[2 * r:2 * r + 2]) < 1e-4
+    alias = {"conv1.1": "bn1", "conv2.1": "bn2", "conv3.1": "bn3"}  # layers.py:12-14 shares these modules
+    for n in ("conv1.0.weight", "conv1.1.weight", "conv1.1.bias", "conv2.0.weight", "conv2.1.weight",
+              "conv2.1.bias", "conv3.0.weight", "transform.weight"):
+        mod, attr = n.rsplit(".", 1)
+        full = getattr(m.get_submodule(mod), attr).grad.cpu()
+        got = ranks[0]["grads"].get(n, ranks[0]["grads"].get(f"{alias.get(mod, mod)}.{attr}"))
+        assert got is not None, n
+        assert rel_err(got * 2, full) < 1e-3, n
