@@ -189,7 +189,6 @@ def posemb_edge_leg(dev, B=32, N=2048, k=40, reps=5):
     (dgx.edgemlp) next to the reference's op sequence in PyTorch-ROCm eager."""
     import torch.nn as nn
     from dgx.edgemlp import edge_mlp2
-    from models.dgcnn import get_graph_feature  # noqa: F401
     torch.manual_seed(1)
 
     def blocks():
