@@ -533,6 +533,10 @@ __global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ 
     __shared__ int ncand;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nr = ctl[0];  // rows knn_kernel appended to the list
+    // Nothing flagged (the common case): no block touches the list or the
+    // exit counter, so there is nothing to reset and no device-scope fence.
+    // Uniform: the list is only reset after every block has read it.
+    if (nr == 0) return;
     for (int i = blockIdx.x; i < nr; i += gridDim.x) {
         const int64_t row = ctl[4 + i];
         const int b = (int)(row / N), q = (int)(row - (int64_t)b * N);
