@@ -445,15 +445,29 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
     if (ok) {
         const float a = scale[o], sh = shift[o], mu = mean[o], is = invstd[o];
         const int64_t i0 = (int64_t)blockIdx.x * rows_per_blk;
-        for (int r = wave; r < rows_per_blk; r += 4) {
-            const int64_t i = i0 + r;
-            if (i >= M) break;
-            const float y = ysel[i * Co + o];
-            const float z = fmaf(a, y, sh);
-            const float d = dY[i * lddy + o] * (z > 0.f ? 1.f : slope);
-            dzp[i * Co + o] = pack_dz(d, arg[i * Co + o]);
-            acc1 += d;
-            acc2 = fmaf(d, (y - mu) * is, acc2);
+        // DZ_U rows per wave per iteration, loads issued together (the pass is
+        // latency-bound with one row in flight); accumulation order unchanged
+        constexpr int DZ_U = 4;
+        for (int r0 = wave; r0 < rows_per_blk; r0 += 4 * DZ_U) {
+            float yv[DZ_U], gv[DZ_U];
+            int av[DZ_U];
+#pragma unroll
+            for (int u = 0; u < DZ_U; ++u) {
+                const int64_t i = min(i0 + r0 + 4 * u, (int64_t)M - 1);
+                yv[u] = ysel[i * Co + o];
+                gv[u] = dY[i * lddy + o];
+                av[u] = arg[i * Co + o];
+            }
+#pragma unroll
+            for (int u = 0; u < DZ_U; ++u) {
+                const int64_t i = i0 + r0 + 4 * u;
+                if (r0 + 4 * u >= rows_per_blk || i >= M) break;
+                const float z = fmaf(a, yv[u], sh);
+                const float d = gv[u] * (z > 0.f ? 1.f : slope);
+                dzp[i * Co + o] = pack_dz(d, av[u]);
+                acc1 += d;
+                acc2 = fmaf(d, (yv[u] - mu) * is, acc2);
+            }
         }
     }
     red[0][wave][lane] = acc1;
