@@ -25,15 +25,9 @@
 // compulsory M*Co*(bytes) instead of M*k*Co*(bytes).
 #include <math.h>
 
-#include <stdlib.h>
-
 #include <algorithm>
 
 #include "common.h"
-
-#ifndef DGX_EXP
-#define DGX_EXP 0  // experiment switch for profiling builds (0 = product)
-#endif
 
 namespace {
 
@@ -185,9 +179,7 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     const int64_t base = (int64_t)b * N;
     const int per = (N + nparts - 1) / nparts;
     const int n_beg = part * per, n_end = min(N, n_beg + per);
-#if DGX_EXP != 2
     stage_slice<CS, EC_THREADS>(lds, PQ + base * ldpq, ldpq, N, o0, Co, (ldpq % 4) == 0 && (o0 % 4) == 0);
-#endif
 
     // Pass = PP consecutive points; their idx rows (PP*k ints, contiguous in
     // HBM) are staged in LDS, the next pass's rows prefetched into registers
@@ -268,9 +260,6 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
                 }
             };
             int kk = 0;
-#if DGX_EXP == 1
-            kk = k;
-#endif
             for (; kk + 4 <= k; kk += 4) {
                 const int j0 = row[kk], j1 = row[kk + 1], j2 = row[kk + 2], j3 = row[kk + 3];
                 take(j0, kk);
@@ -339,8 +328,10 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     }
 }
 
-// one block per channel: fp64 tree reduction of the partial rows
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ partials, int nrows, int Co,
+// one block per channel: fp64 tree reduction of the partial rows (fp32 per-block
+// partials, or fp64 global sums after a SyncBatchNorm all-reduce)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ partials, int nrows, int Co,
                                                           double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, double momentum, double eps,
@@ -480,7 +471,8 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
     }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partials, int nrows,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const T* __restrict__ partials, int nrows,
                                                               int Co, double count, const float* __restrict__ scale,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
@@ -698,10 +690,8 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
     };
 
     if (npass > 0) load_pass(0);
-#if DGX_EXP != 2
     stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
     stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
-#endif
     if (npass > 0) store_pass();
     __syncthreads();
     const int tp = t % TPP, pl = t / TPP;
@@ -753,9 +743,6 @@ __global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
                 }
             };
             int32_t u0 = beg;
-#if DGX_EXP == 1
-            u0 = end;
-#endif
             for (; u0 + 8 <= end; u0 += 8) {
                 int32_t e[8];
 #pragma unroll
@@ -1020,8 +1007,18 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count, 
                         float* scale, float* shift, float* mean, float* invstd, int64_t* num_batches_tracked,
                         void* stream) {
     if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co, count,
-                       gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
+                       count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
+                       num_batches_tracked);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_bn_finalize_f64(const double* sums, int nrows, int Co, double count, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, double momentum, double eps, float* scale,
+                        float* shift, float* mean, float* invstd, int64_t* num_batches_tracked, void* stream) {
+    if (!sums || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
+                       count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
                        num_batches_tracked);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
@@ -1067,7 +1064,17 @@ int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co, double cou
                             float* c1, int accumulate, void* stream) {
     if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !mean || !invstd || !c0 || !c1)
         return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows,
+                       Co, count, scale, mean, invstd, dgamma, dbeta, c0, c1, accumulate);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co, double count, const float* scale,
+                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* c0,
+                            float* c1, int accumulate, void* stream) {
+    if (!sums || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !mean || !invstd || !c0 || !c1)
+        return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, scale, mean, invstd, dgamma, dbeta, c0, c1, accumulate);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
@@ -1109,8 +1116,7 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, c
             hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, false>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
                                edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                    \
         break;
-    static const bool narrow = getenv("DGX_EDGE_BWD_NARROW") != nullptr;  // A/B switch for profiling
-    if (cs <= 8 && !narrow) {
+    if (cs <= 8) {  // wide form: one point per thread, all slice channels
         const size_t wl = (size_t)2 * N * cs * sizeof(float);
 #define DGX_WIDE_CASE(CSV)                                                                                    \
     case CSV:                                                                                                \

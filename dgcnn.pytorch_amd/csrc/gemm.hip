@@ -735,9 +735,57 @@ __global__ __launch_bounds__(256) void atb_small_kernel(const bf16* __restrict__
 
 bool aligned_to(const void* p, int bytes) { return (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
 
+// Exact fp32 GEMM for a short reduction (K <= 16): C (M x N) = X (M x K) W^T
+// with W (N x K), every output an fmaf chain over k in order. Used for the
+// layer-1 per-point GEMM on raw coordinates (K = 3, dgcnn.py:55 / layers.py:17):
+// bf16 rounding of xyz there is the largest single error term of the bf16 mode
+// (edge values y = P_j + Q_i of close neighbours nearly cancel in BN), and the
+// work (2*M*N*K flops) is a few microseconds of HBM writes, not a GEMM.
+// Block = 64 rows; W and the rows' X staged in LDS; each thread writes 4
+// consecutive columns (16-B stores along the row).
+constexpr int SK_ROWS = 64;
+constexpr int SK_MAXK = 16;
+__global__ __launch_bounds__(256) void smallk_gemm_kernel(const float* __restrict__ X, int64_t ldx,
+                                                          const float* __restrict__ W, int M, int N, int K,
+                                                          float* __restrict__ C, int64_t ldc) {
+    extern __shared__ float sk[];  // W [N][K] | X [SK_ROWS][K]
+    float* ws = sk;
+    float* xs = sk + N * K;
+    const int r0 = blockIdx.x * SK_ROWS;
+    const int rows = min(SK_ROWS, M - r0);
+    for (int e = threadIdx.x; e < N * K; e += 256) ws[e] = W[e];
+    for (int e = threadIdx.x; e < rows * K; e += 256) {
+        const int r = e / K, c = e - r * K;
+        xs[e] = X[(int64_t)(r0 + r) * ldx + c];
+    }
+    __syncthreads();
+    const int nq = N >> 2;  // N % 4 == 0 (checked by the launcher)
+    for (int e = threadIdx.x; e < rows * nq; e += 256) {
+        const int r = e / nq, j = (e - r * nq) * 4;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < K; ++c) {
+            const float xv = xs[r * K + c];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = fmaf(xv, ws[(j + u) * K + c], acc[u]);
+        }
+        *reinterpret_cast<float4*>(C + (int64_t)(r0 + r) * ldc + j) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int dgx_gemm_smallk_f32(const float* X, int64_t ldx, const float* W, int M, int N, int K, float* C, int64_t ldc,
+                        void* stream) {
+    if (!X || !W || !C || M < 1 || N < 4 || K < 1 || ldx < K || ldc < N) return DGX_EINVAL;
+    if (K > SK_MAXK || N % 4 || ldc % 4 || reinterpret_cast<uintptr_t>(C) % 16) return DGX_EUNSUPPORTED;
+    if ((size_t)(N + SK_ROWS) * K * sizeof(float) > 64 * 1024) return DGX_EUNSUPPORTED;
+    const size_t lds = (size_t)(N + SK_ROWS) * K * sizeof(float);
+    hipLaunchKernelGGL(smallk_gemm_kernel, dim3((M + SK_ROWS - 1) / SK_ROWS), dim3(256), lds, dgx_stream(stream), X,
+                       ldx, W, M, N, K, C, ldc);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
 
 int dgx_gemm_stats_rows(int M) { return (M + GB_BM - 1) / GB_BM; }
 

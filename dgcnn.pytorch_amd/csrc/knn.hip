@@ -10,16 +10,20 @@
 //     in registers: 8 lanes per query (4 lanes x 2 candidate halves), merged
 //     at the end.
 //
-// Workgroup = 8 waves = 4 query groups x 2 candidate halves: 64 queries of one
-// cloud. The two waves of a query group share the query operand and split each
-// candidate chunk's 16-candidate tiles (even / odd), so a cloud's 32768 query
-// rows keep 4 waves per SIMD busy. Candidates stream through an LDS chunk laid
-// out [j/16][c][row(j%16)] (padded, see knn_tile_stride) so the MFMA A operand
-// read (lane l -> c = 4t + l/16, row l%16) and the chunk stores are
-// bank-conflict-free.
+// Three launches per call:
+//   knn_image_kernel  one pass over x: |x|^2 in the reference's order and an
+//                     MFMA A-operand "image" of each cloud (16-candidate tiles,
+//                     lane-ordered so a wave fetches a tile with 16-B loads).
+//   knn_kernel        workgroup = 4 waves = 2 query groups of 16 x 2 candidate
+//                     halves (even / odd tiles). Each wave keeps its 16 queries'
+//                     operands in registers and streams its half of the cloud's
+//                     image straight from L2 through a two-slot register ring;
+//                     no LDS staging, no barrier until the final merge. Each
+//                     query's candidates are dealt over 8 register lists (4 lanes
+//                     x 2 halves) with an admission bound shared through LDS.
+//   knn_fix_kernel    exact recompute of the (rare) rows whose list overflowed.
 #include <math.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "common.h"
 
@@ -655,8 +659,6 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
                        xximg, xx, B, N, k, nqb, idx64, idx32, vals, ctl);
     if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH;
-    static const bool nofix = getenv("DGX_KNN_NOFIX") != nullptr;  // diagnostics: leave flagged rows marked
-    if (nofix) return DGX_OK;
     hipLaunchKernelGGL(knn_fix_kernel, dim3(FIX_BLOCKS), dim3(256), 0, st, x, sB, sC, sN, xx, B, C, N, k, idx64,
                        idx32, vals, ctl);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;

@@ -39,6 +39,8 @@ _SIGS = {
     "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dgx_bn_finalize_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dgx_bn_bwd_finalize_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
     "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp],
     "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
@@ -57,6 +59,7 @@ _SIGS = {
     "dgx_gemm_splits": [_i32, _i32, _i32],
     "dgx_gemm_bf16": [_vp, _i32, _i32, _i64, _vp, _i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp,
                       _vp],
+    "dgx_gemm_smallk_f32": [_vp, _i64, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_slab_reduce_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_gemm_lds_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64,
                           _vp],
@@ -110,8 +113,36 @@ def check(rc, what):
         raise RuntimeError(f"dgx: {what} failed ({rc}: {msg})")
 
 
-def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+def ptr(t, *dtypes):
+    """Device pointer of ``t`` (None passes through). With ``dtypes`` the tensor
+    must have one of them: every kernel argument's element type is fixed by the
+    C ABI (include/dgx.h), and a tensor of another dtype (e.g. an fp16 product
+    made under autocast) would be read with the wrong element size."""
+    if t is None:
+        return None
+    if dtypes and t.dtype not in dtypes:
+        raise RuntimeError(f"dgx: kernel operand has dtype {t.dtype}, expected {' or '.join(map(str, dtypes))}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+F32, BF16, I32, I64, U8, F64 = (torch.float32, torch.bfloat16, torch.int32, torch.int64, torch.uint8,
+                               torch.float64)
+
+
+def f32(t):
+    return ptr(t, F32)
+
+
+def bf16(t):
+    return ptr(t, BF16)
+
+
+def i32(t):
+    return ptr(t, I32)
+
+
+def u8(t):
+    return ptr(t, U8)
 
 
 def stream_of(t):

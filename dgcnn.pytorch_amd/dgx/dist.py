@@ -8,18 +8,22 @@ backward all-reduces sum(dy) and sum(dy * xmu)).
 
 The engine keeps those exact semantics with one collective per BN layer and
 direction: the kernels already produce per-block partial sums, the host sums
-them to one (2, C) vector, and ``allreduce_sums`` adds the vectors of all ranks
-(plus the element count) in a single all-reduce over RCCL (or gloo). Parameter
-gradients stay rank-local (DDP averages them), exactly as SyncBatchNorm does.
+them in fp64 to one (2, C) vector, and ``allreduce_sums`` adds the vectors of
+all ranks (plus the element count) in a single fp64 all-reduce over RCCL (or
+gloo). The global sums stay fp64 into the finalize kernel
+(dgx_bn_finalize_f64), so var = E[y^2] - E[y]^2 sees no fp32 round trip.
+Parameter gradients stay rank-local (DDP averages them), exactly as
+SyncBatchNorm does.
 """
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 
 
-def sync_group(bn, training):
-    """(True, group) when ``bn`` is a SyncBatchNorm that must synchronise now."""
-    if not (training and isinstance(bn, nn.SyncBatchNorm)):
+def sync_group(bn):
+    """(True, group) when ``bn`` is a SyncBatchNorm that must synchronise now
+    (SyncBatchNorm.forward: batch statistics in training mode, world > 1)."""
+    if not (bn.training and isinstance(bn, nn.SyncBatchNorm)):
         return False, None
     if not (dist.is_available() and dist.is_initialized()):
         return False, None
@@ -29,12 +33,13 @@ def sync_group(bn, training):
     return True, group
 
 
-def allreduce_sums(sums, count, group):
-    """sums: (2, C) fp32 local column sums; count: local element count.
-    Returns (global sums (2, C), global count) with ONE all-reduce."""
-    C = sums.shape[-1]
-    buf = torch.empty(2 * C + 1, dtype=torch.float64, device=sums.device)
-    buf[:2 * C] = sums.reshape(-1).double()
+def allreduce_sums(partials, count, group):
+    """partials: (rows, 2, C) fp32 per-block column sums; count: local element
+    count. Returns (global sums (2, C) fp64 contiguous, global count) with ONE
+    all-reduce."""
+    C = partials.shape[-1]
+    buf = torch.empty(2 * C + 1, dtype=torch.float64, device=partials.device)
+    buf[:2 * C] = partials.double().sum(0).reshape(-1)
     buf[2 * C] = float(count)
     dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    return buf[:2 * C].view(2, C).float(), float(buf[2 * C].item())
+    return buf[:2 * C].view(2, C), float(buf[2 * C].item())

@@ -16,33 +16,33 @@ Backward per block (reverse order):
     dz, BN-bwd affine                         HIP
     reverse kNN graph + dPQ                   HIP
     dX += dPQ [W1; W2], dW = dPQ^T X          GEMM (accumulated into xcat's grad)
+
+BatchNorm decisions follow each BN module's own flags (dgx.bn). Under
+torch.autocast the op runs in the engine's own precision on fp32 inputs
+(precision.no_autocast): its GEMMs never return autocast-reduced products.
 """
+import threading
+
 import torch
 
 from . import _native as nat
-from . import dist as dist_
+from . import bn as bn_
 from . import gemm as G
 from . import precision as prec
 from .ops import knn_raw, reduction_order
 
-
-# Optional capture for tests/tools: when a dict, forward stores each block's
-# routing decisions (idx, arg, zpos) under ("fwd", l) and backward stores
-# intermediates under l. Off (None) in normal use.
-_debug = None
+_tls = threading.local()
 
 
-def _bn_factor(bn):
-    """(exponential-average factor nn.BatchNorm uses this step, num_batches_tracked
-    tensor for the finalize kernel to increment or None). With a momentum the
-    counter is bumped on device by dgx_bn_finalize_f32 (no extra launch); the
-    cumulative-average form (momentum None) needs the count on the host."""
-    if bn.momentum is None:
-        if bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
-            return 1.0 / float(bn.num_batches_tracked.item()), None
-        return 0.0, None
-    return float(bn.momentum), bn.num_batches_tracked
+def debug_capture():
+    """Per-thread capture dict for tests/tools (None when off): forward stores each
+    block's routing decisions (idx, arg, zpos) under ("fwd", l), backward stores
+    intermediates under l."""
+    return getattr(_tls, "debug", None)
+
+
+def set_debug_capture(d):
+    _tls.debug = d
 
 
 def _reverse_graph(idx, B, N, k, dev):
@@ -55,7 +55,7 @@ def _reverse_graph(idx, B, N, k, dev):
     rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
     edges = torch.empty(M * k, dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
-        nat.check(nat.lib().dgx_graph_reverse(nat.ptr(idx), B, N, k, nat.ptr(rowptr), nat.ptr(edges),
+        nat.check(nat.lib().dgx_graph_reverse(nat.i32(idx), B, N, k, nat.i32(rowptr), nat.i32(edges),
                                               nat.stream_of(idx)), "reverse graph")
     return rowptr, edges
 
@@ -67,15 +67,35 @@ class _Layer:
         self.cin, self.cout, self.bn, self.slope = cin, cout, bn, slope
 
 
-def _split_weight(w, cin, cout):
+def split_weight(w, cin, cout):
+    """Reference conv weight (Co, 2C[,1,1]) = [W1 | W2] -> stacked [W1; W2] (2Co, C):
+    rows [0,Co) produce P (neighbour half, channels [0,C)), rows [Co,2Co) Q (centre half)."""
     w = w.reshape(cout, 2 * cin)
-    # rows [0,Co) produce P (neighbour half, channels [0,C)), rows [Co,2Co) Q (centre half)
     return torch.cat([w[:, :cin], w[:, cin:]], dim=0)
+
+
+def edge_select(PQ, idx, B, N, k, co, gamma, stream):
+    """dgx_edge_fwd_gather_f32: per (point, channel) the selected pre-BN value,
+    its slot, sum_k P_j and the per-block BN partial sums over all edges."""
+    L = nat.lib()
+    dev = PQ.device
+    M = B * N
+    ysel = torch.empty((M, co), dtype=torch.float32, device=dev)
+    arg = torch.empty((M, co), dtype=torch.uint8, device=dev)
+    sumP = torch.empty((M, co), dtype=torch.float32, device=dev)
+    prow = L.dgx_edge_partials_rows(B, N, co)
+    partials = torch.empty((prow, 2, co), dtype=torch.float32, device=dev)
+    nat.check(L.dgx_edge_fwd_gather_f32(nat.f32(PQ), PQ.stride(0), nat.i32(idx), B, N, k, co, nat.f32(gamma),
+                                        nat.f32(ysel), nat.u8(arg), nat.f32(sumP), nat.f32(partials), prow, stream),
+              "edge gather")
+    return ysel, arg, sumP, partials, prow
 
 
 class _EdgeConvStack(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, layers, training, ctx_preps, *params):
+    @prec.no_autocast
+    def forward(ctx, x, k, layers, ctx_preps, need_grad, *params):
+        x = x.float()
         dev = x.device
         B, C0, N = x.shape
         M = B * N
@@ -94,11 +114,12 @@ class _EdgeConvStack(torch.autograd.Function):
         count = float(M * k)
         have16 = False  # xcat16 holds the previous block's output
         # bf16 [W1;W2] and transposed copies of blocks 2.. in one launch (used when
-        # the block's input is the bf16 twin, i.e. after a batch-statistics block)
+        # the block's input is the bf16 twin, i.e. after a selecting block)
         preps = list(ctx_preps) if ctx_preps is not None else [None] * len(layers)
         if bf16 and len(layers) > 1 and ctx_preps is None:
             jobs = [(params[3 * li], ly.cout, ly.cin, True) for li, ly in enumerate(layers) if li > 0]
             preps[1:] = G.prep_weights(jobs)
+        dbg = debug_capture()
         for li, ly in enumerate(layers):
             w, gamma, beta = params[3 * li: 3 * li + 3]
             cin, co = ly.cin, ly.cout
@@ -112,66 +133,46 @@ class _EdgeConvStack(torch.autograd.Function):
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
                               strides=(N * total, 1, total), shape=(B, cin, N))
             wprep = None
-            if bf16:
+            if cin <= G.SMALLK_MAX:
+                # raw coordinates (block 1, K = 3): exact fp32 in every mode
+                PQ = G.mm_smallk(X, split_weight(w, cin, co))
+            elif bf16:
                 X16 = xcat16[:, off_in:off_in + cin] if li > 0 else None
                 if have16 and G.lds_ok_nt(X16, cin):
                     # bf16 operands by LDS-DMA; the weight's bf16 [W1;W2] and transpose serve fwd and bwd
                     wprep = preps[li]
                     PQ = G.lds_xwt(X16, wprep[0])
                 else:
-                    PQ = G.mm_xwt(X, _split_weight(w, cin, co))  # fp32 operands rounded while staged
+                    PQ = G.mm_xwt(X, split_weight(w, cin, co))  # fp32 operands rounded while staged
             else:
-                PQ = prec.mm(X, _split_weight(w, cin, co).t())
+                PQ = prec.mm(X, split_weight(w, cin, co).t())
             off = sum(widths[:li])
             out = xcat[:, off:off + co]
             bn = ly.bn
-            use_batch = training or bn.running_mean is None
-            scale = torch.empty(co, dtype=torch.float32, device=dev)
-            shift = torch.empty_like(scale)
+            use_batch, _ = bn_.mode(bn)
             with torch.cuda.device(dev):
-                if use_batch:
-                    ysel = torch.empty((M, co), dtype=torch.float32, device=dev)
-                    arg = torch.empty((M, co), dtype=torch.uint8, device=dev)
-                    sumP = torch.empty((M, co), dtype=torch.float32, device=dev)
-                    prow = L.dgx_edge_partials_rows(B, N, co)
-                    partials = torch.empty((prow, 2, co), dtype=torch.float32, device=dev)
-                    mean = torch.empty_like(scale)
-                    invstd = torch.empty_like(scale)
-                    nat.check(L.dgx_edge_fwd_gather_f32(
-                        nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(gamma), nat.ptr(ysel),
-                        nat.ptr(arg), nat.ptr(sumP), nat.ptr(partials), prow, stream), "edge gather")
-                    update = training and bn.running_mean is not None
-                    factor, nbt = _bn_factor(bn) if update else (0.0, None)
-                    fin, frows, fcount = partials, prow, count
-                    sync, group = dist_.sync_group(bn, training)
-                    if sync:  # SyncBatchNorm: statistics of the global batch, one all-reduce
-                        tot, fcount = dist_.allreduce_sums(partials.sum(0), count, group)
-                        fin, frows = tot.unsqueeze(0).contiguous(), 1
-                    nat.check(L.dgx_bn_finalize_f32(
-                        nat.ptr(fin), frows, co, fcount, nat.ptr(gamma), nat.ptr(beta),
-                        nat.ptr(bn.running_mean) if update else None,
-                        nat.ptr(bn.running_var) if update else None, factor, float(bn.eps),
-                        nat.ptr(scale), nat.ptr(shift), nat.ptr(mean), nat.ptr(invstd), nat.ptr(nbt), stream),
-                        "bn finalize")
+                if use_batch or need_grad:
+                    ysel, arg, sumP, partials, prow = edge_select(PQ, idx, B, N, k, co, gamma, stream)
+                    if use_batch:
+                        st = bn_.batch_stats(partials, prow, count, bn, gamma, beta, stream)
+                    else:  # running statistics, output differentiated: keep the selection
+                        st = bn_.running_stats(bn, gamma, beta, stream)
                     out16 = xcat16[:, off:off + co] if bf16 else None
-                    nat.check(L.dgx_bn_lrelu_apply_f32(nat.ptr(ysel), M, co, nat.ptr(scale), nat.ptr(shift),
-                                                       float(ly.slope), nat.ptr(out), total, nat.ptr(out16), stream),
-                              "bn apply")
+                    nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, co, nat.f32(st.scale), nat.f32(st.shift),
+                                                       float(ly.slope), nat.f32(out), total, nat.ptr(out16, nat.BF16),
+                                                       stream), "bn apply")
                     have16 = bf16
-                    saved.append((idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep,
-                                  group if sync else None))
-                    if _debug is not None:
+                    saved.append((idx, PQ, ysel, arg, sumP, st, wprep))
+                    if dbg is not None:
                         # sign of fmaf(scale, ysel, shift) as the kernels evaluate it: the fp64
                         # product of two fp32 values is exact, so this sign is fma's sign
-                        zpos = (scale.double() * ysel.double() + shift.double()) > 0
-                        _debug[("fwd", li)] = (idx.clone(), arg.clone(), zpos)
-                else:
-                    nat.check(L.dgx_bn_eval_affine_f32(
-                        co, nat.ptr(gamma), nat.ptr(beta), nat.ptr(bn.running_mean), nat.ptr(bn.running_var),
-                        float(bn.eps), nat.ptr(scale), nat.ptr(shift), stream), "bn eval affine")
+                        zpos = (st.scale.double() * ysel.double() + st.shift.double()) > 0
+                        dbg[("fwd", li)] = (idx.clone(), arg.clone(), zpos)
+                else:  # inference with running statistics: one fused select + affine + LReLU pass
+                    st = bn_.running_stats(bn, gamma, beta, stream)
                     nat.check(L.dgx_edge_fwd_eval_f32(
-                        nat.ptr(PQ), 2 * co, nat.ptr(idx), B, N, k, co, nat.ptr(scale), nat.ptr(shift),
-                        float(ly.slope), nat.ptr(out), total, stream), "edge eval")
+                        nat.f32(PQ), PQ.stride(0), nat.i32(idx), B, N, k, co, nat.f32(st.scale), nat.f32(st.shift),
+                        float(ly.slope), nat.f32(out), total, stream), "edge eval")
                     have16 = False
                     saved.append(None)
             off_in = off
@@ -179,7 +180,7 @@ class _EdgeConvStack(torch.autograd.Function):
         ctx.layers = layers
         ctx.shape = (B, C0, N)
         ctx.layer_state = saved
-        ctx.x_needs_grad = x.requires_grad
+        ctx.x_needs_grad = ctx.needs_input_grad[0]
         ctx.bf16 = bf16
         ctx.save_for_backward(x_pm, xcat, xcat16, *params)
         if xcat16 is None or not have16:
@@ -189,11 +190,10 @@ class _EdgeConvStack(torch.autograd.Function):
         return xcat, xcat16
 
     @staticmethod
+    @prec.no_autocast
     def backward(ctx, dxcat, _unused):
         if dxcat is None:
             return (None,) * (5 + len(ctx.saved_tensors) - 3)
-        if any(s is None for s in ctx.layer_state):
-            raise RuntimeError("dgx EdgeConv: backward through an eval-mode (running-stats) forward is not supported")
         x_pm, xcat, xcat16, *params = ctx.saved_tensors
         layers, k = ctx.layers, ctx.k
         B, C0, N = ctx.shape
@@ -208,6 +208,9 @@ class _EdgeConvStack(torch.autograd.Function):
         dx_in = None
         count = float(M * k)
         nl = len(layers)
+        dbg = debug_capture()
+        if dxcat.dtype != torch.float32:
+            dxcat = dxcat.float()
         if bf16:
             # The incoming gradient stays read-only: block l's input gradient is written
             # as addend (incoming slice) + dPQ Wcat into a fresh buffer, no clone pass.
@@ -220,7 +223,7 @@ class _EdgeConvStack(torch.autograd.Function):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
             w = params[3 * li]
-            idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd, wprep, group = ctx.layer_state[li]
+            idx, PQ, ysel, arg, sumP, st, wprep = ctx.layer_state[li]
             rowptr, edges = _reverse_graph(idx, B, N, k, dev)
             off = sum(widths[:li])
             prev = off - widths[li - 1] if li > 0 else None
@@ -232,40 +235,25 @@ class _EdgeConvStack(torch.autograd.Function):
             nblk = max(1, min(1024, (M + 63) // 64))
             dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dz with packed slot
             partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
-            dgamma = torch.empty(co, dtype=torch.float32, device=dev)
-            dbeta = torch.empty(co, dtype=torch.float32, device=dev)
-            c0 = torch.empty(co, dtype=torch.float32, device=dev)
-            c1 = torch.empty(co, dtype=torch.float32, device=dev)
             # dPQ only feeds the GEMMs: bf16 (what the GEMM would round it to) in bf16 mode
             dPQ = torch.empty((M, 2 * co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
             with torch.cuda.device(dev):
                 nat.check(L.dgx_edge_bwd_dz_f32(
-                    nat.ptr(dY), ldy, nat.ptr(ysel), nat.ptr(arg), M, co, nat.ptr(scale), nat.ptr(shift),
-                    nat.ptr(mean), nat.ptr(invstd), float(ly.slope), nat.ptr(dz), nat.ptr(partials), nblk, stream),
-                    "edge bwd dz")
-                if group is None:
-                    nat.check(L.dgx_bn_bwd_finalize_f32(
-                        nat.ptr(partials), nblk, co, count, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
-                        nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
-                else:  # SyncBatchNorm: input gradient from global sums, gamma/beta grads rank-local
-                    loc = partials.sum(0)
-                    tot, gcount = dist_.allreduce_sums(loc, count, group)
-                    tot = tot.unsqueeze(0).contiguous()
-                    nat.check(L.dgx_bn_bwd_finalize_f32(
-                        nat.ptr(tot), 1, co, gcount, nat.ptr(scale), nat.ptr(mean), nat.ptr(invstd),
-                        None, None, nat.ptr(c0), nat.ptr(c1), 0, stream), "bn bwd finalize")
-                    dbeta.copy_(loc[0])
-                    dgamma.copy_(loc[1])
+                    nat.f32(dY), ldy, nat.f32(ysel), nat.u8(arg), M, co, nat.f32(st.scale), nat.f32(st.shift),
+                    nat.f32(st.mean), nat.f32(st.invstd), float(ly.slope), nat.f32(dz), nat.f32(partials), nblk,
+                    stream), "edge bwd dz")
+                dgamma, dbeta, c0, c1 = bn_.backward_consts(partials, nblk, count, st, stream)
                 nat.check(L.dgx_edge_bwd_scatter_f32(
-                    nat.ptr(PQ), 2 * co, nat.ptr(rowptr), nat.ptr(edges), nat.ptr(dz), nat.ptr(sumP), B, N, k, co,
-                    nat.ptr(scale), nat.ptr(c0), nat.ptr(c1), nat.ptr(dPQ), int(bf16), stream), "edge bwd scatter")
-            if _debug is not None:
-                _debug[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
-                              "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.float(), "partials": partials.clone(),
-                              "ysel": ysel.clone(), "scale": scale.clone(), "shift": shift.clone(),
-                              "arg": arg.clone(), "idx": idx.clone(), "PQ": PQ.clone(), "sumP": sumP.clone(),
-                              "mean": mean.clone(), "invstd": invstd.clone(), "X": X.clone(),
-                              "rowptr": rowptr.clone(), "edges": edges.clone()}
+                    nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.f32(sumP), B, N, k,
+                    co, nat.f32(st.scale), nat.f32(c0), nat.f32(c1), nat.ptr(dPQ, nat.F32, nat.BF16), int(bf16),
+                    stream), "edge bwd scatter")
+            if dbg is not None:
+                dbg[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
+                           "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.float(), "partials": partials.clone(),
+                           "ysel": ysel.clone(), "scale": st.scale.clone(), "shift": st.shift.clone(),
+                           "arg": arg.clone(), "idx": idx.clone(), "PQ": PQ.clone(), "sumP": sumP.clone(),
+                           "mean": st.mean.clone(), "invstd": st.invstd.clone(), "X": X.clone(),
+                           "rowptr": rowptr.clone(), "edges": edges.clone()}
             grads[3 * li + 1] = dgamma
             grads[3 * li + 2] = dbeta
             if bf16:
@@ -283,11 +271,11 @@ class _EdgeConvStack(torch.autograd.Function):
                         G.lds_xwt(dPQ, wprep[1], out=dst, addend=add)
                     else:
                         dst.copy_(add)
-                        G.mm_xw(dPQ, _split_weight(w, cin, co), out=dst, accumulate=True)
+                        G.mm_xw(dPQ, split_weight(w, cin, co), out=dst, accumulate=True)
                 elif ctx.x_needs_grad:
-                    dx_in = G.mm_xw(dPQ, _split_weight(w, cin, co)).view(B, N, C0).permute(0, 2, 1)
+                    dx_in = G.mm_xw(dPQ, split_weight(w, cin, co)).view(B, N, C0).permute(0, 2, 1)
             else:
-                wcat = _split_weight(w, cin, co)
+                wcat = split_weight(w, cin, co)
                 dwcat = prec.mm(dPQ.t(), X)  # (2Co, C)
                 grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)
                 if li > 0:
@@ -297,26 +285,37 @@ class _EdgeConvStack(torch.autograd.Function):
         return (dx_in, None, None, None, None, *grads)
 
 
-def edgeconv_stack_pair(x, k, convs, training, preps=None):
-    """As edgeconv_stack, also returning the bf16 twin of the concat buffer
-    (empty unless precision "bf16" produced it): conv5's GEMM operand.
-    ``preps``: optional per-block bf16 weight copies (gemm.prep_weights) made
-    by the caller in one launch with other layers' (None for block 1)."""
-    nat.require_device(x)
-    if x.dtype != torch.float32:
-        x = x.float()
+def _layers_and_params(convs):
     layers, params = [], []
     for seq in convs:
         conv, bn, act = seq[0], seq[1], seq[2]
         co, c2 = conv.weight.shape[0], conv.weight.shape[1]
-        if bn.weight is None:
-            raise NotImplementedError("dgx EdgeConv expects affine BatchNorm (as the reference builds it)")
+        if conv.bias is not None or bn.weight is None:
+            raise NotImplementedError("dgx EdgeConv expects Conv2d(bias=False) + affine BatchNorm "
+                                      "(as the reference builds them, dgcnn.py:54-73)")
         layers.append(_Layer(c2 // 2, co, bn, act.negative_slope))
         params += [conv.weight, bn.weight, bn.bias]
-    return _EdgeConvStack.apply(x, k, layers, training, preps, *params)
+    return layers, params
 
 
-def edgeconv_stack(x, k, convs, training):
+def edgeconv_stack_pair(x, k, convs, training=None, preps=None):
+    """As edgeconv_stack, also returning the bf16 twin of the concat buffer
+    (empty unless precision "bf16" produced it): conv5's GEMM operand.
+    ``preps``: optional per-block bf16 weight copies (gemm.prep_weights) made
+    by the caller in one launch with other layers' (None for block 1).
+    ``training`` is accepted for call compatibility only: every BatchNorm
+    decides batch vs running statistics by its own flags, as nn.BatchNorm does."""
+    nat.require_device(x)
+    if x.dtype != torch.float32:
+        x = x.float()
+    layers, params = _layers_and_params(convs)
+    # whether this forward will be differentiated (inside Function.forward grad
+    # mode is always off, so it is decided here)
+    need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+    return _EdgeConvStack.apply(x, k, layers, preps, need_grad, *params)
+
+
+def edgeconv_stack(x, k, convs, training=None):
     """Run the block chain. ``convs``: list of nn.Sequential(Conv2d(2C,Co,1,bias=False),
     BatchNorm2d(Co), LeakyReLU) exactly as the reference builds them (dgcnn.py:54-73).
     Returns the point-major concat buffer (B*N, sum Co)."""

@@ -6,56 +6,56 @@ column i of a row-major (K, ld) buffer). Operands are fp32 or bf16 views of
 existing buffers (column slices of the concat buffer included): nothing is
 copied or converted on the host side.
 """
+import threading
+
 import torch
 
 from . import _native as nat
 
 EPI_STORE, EPI_ACCUM, EPI_STATS, EPI_SLAB, EPI_STATS16 = 0, 1, 2, 3, 4
 
-# Optional instrumentation (bench.py): when a list, every GEMM launch appends
-# (start_event, end_event, flops) recorded on the launch stream.
-_timing = None
+# Optional per-thread instrumentation (tools): when a list, every GEMM launch
+# of this thread appends (start_event, end_event, flops, tag) recorded on the
+# launch stream. Per thread, so nn.DataParallel replicas (one Python thread per
+# device) never record into each other's lists.
+_tls = threading.local()
 
 
 def set_timing(lst):
-    global _timing
-    _timing = lst
+    _tls.timing = lst
 
 
 class _Timed:
     def __init__(self, flops):
         self.flops = flops
+        self.timing = getattr(_tls, "timing", None)
 
     def __enter__(self):
-        if _timing is not None:
+        if self.timing is not None:
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
             self.e0.record()
         return self
 
     def __exit__(self, *exc):
-        if _timing is not None:
+        if self.timing is not None:
             self.e1.record()
-            _timing.append((self.e0, self.e1, self.flops, _tag))
+            self.timing.append((self.e0, self.e1, self.flops, getattr(_tls, "tag", None)))
         return False
 
 
-_tag = None
-
-
 class tag:
-    """Label the GEMM launches issued inside (bench.py's per-class MFMA report)."""
+    """Label the GEMM launches issued inside (this thread only)."""
     def __init__(self, name):
         self.name = name
 
     def __enter__(self):
-        global _tag
-        self.prev, _tag = _tag, self.name
+        self.prev = getattr(_tls, "tag", None)
+        _tls.tag = self.name
         return self
 
     def __exit__(self, *exc):
-        global _tag
-        _tag = self.prev
+        _tls.tag = self.prev
         return False
 
 
@@ -99,6 +99,24 @@ def mm_xwt(x, w, out=None, stats=False):
     return (out, part) if stats else out
 
 
+SMALLK_MAX = 16
+
+
+def mm_smallk(x, w):
+    """Exact fp32 (M,N) = x (M,K) @ w (N,K)^T for K <= 16 (dgx_gemm_smallk_f32):
+    the layer-1 GEMM on raw coordinates, exact in every precision mode."""
+    M, K = x.shape
+    N = w.shape[0]
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    w = w.contiguous()
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device), _Timed(2.0 * M * N * K):
+        nat.check(nat.lib().dgx_gemm_smallk_f32(nat.f32(x), x.stride(0) if M > 1 else K, nat.f32(w), M, N, K,
+                                                nat.f32(out), N, nat.stream_of(x)), "gemm small-k")
+    return out
+
+
 def mm_xw(x, w, out=None, accumulate=False):
     """out (M,N) (+)= x (M,K) @ w (K,N)."""
     M, K = x.shape
@@ -115,6 +133,8 @@ def mm_atb(a, b, out, split_rows=None):
     [W1;W2] result into out = [W1 | W2] (out is (M - Co, 2N))."""
     R, M = a.shape
     N = b.shape[1]
+    if out.dtype != torch.float32 or out.stride(1) != 1:
+        raise RuntimeError("dgx gemm: output must be a row-major fp32 view")
     L = nat.lib()
     S = L.dgx_gemm_splits(M, N, R)
     slab = torch.empty((S, M, N), dtype=torch.float32, device=a.device)
@@ -147,6 +167,10 @@ def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None, out_
     N = w16.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x16.device)
+    if out.dtype != (torch.bfloat16 if out_bf16 else torch.float32) or out.stride(1) != 1:
+        raise RuntimeError("dgx gemm: output view dtype/layout does not match the epilogue")
+    if addend is not None and (addend.dtype != torch.float32 or addend.stride(1) != 1):
+        raise RuntimeError("dgx gemm: addend must be a row-major fp32 view")
     part = None
     if stats:
         part = torch.empty((nat.lib().dgx_gemm_stats_rows(M), 2, N), dtype=torch.float32, device=x16.device)
@@ -167,6 +191,8 @@ def lds_atb(a16, b16, out, split_rows=None):
     split-K slabs summed deterministically); ``split_rows`` as in mm_atb."""
     R, M = a16.shape
     N = b16.shape[1]
+    if out.dtype != torch.float32 or out.stride(1) != 1:
+        raise RuntimeError("dgx gemm: output must be a row-major fp32 view")
     L = nat.lib()
     S = L.dgx_gemm_splits(M, N, R)
     chunk = -(-R // S)
@@ -191,7 +217,7 @@ def prep_weight(w, rows, cols, stacked):
     nt = torch.empty((R, cols), dtype=torch.bfloat16, device=w.device)
     tn = torch.empty((cols, R), dtype=torch.bfloat16, device=w.device)
     with torch.cuda.device(w.device):
-        nat.check(nat.lib().dgx_weight_prep_bf16(nat.ptr(w), rows, cols, int(stacked), nat.ptr(nt), nat.ptr(tn),
+        nat.check(nat.lib().dgx_weight_prep_bf16(nat.f32(w), rows, cols, int(stacked), nat.ptr(nt), nat.ptr(tn),
                                                  nat.stream_of(w)), "weight prep")
     return nt, tn
 
@@ -217,6 +243,8 @@ def prep_weights(jobs):
     P = ctypes.c_void_p * n
     I = ctypes.c_int * n
     # host arrays kept in locals for the duration of the call
+    if any(w.dtype != torch.float32 for (w, _, _, _) in jobs):
+        raise RuntimeError("dgx weight prep: fp32 weights expected")
     W = P(*[w.data_ptr() for (w, _, _, _) in jobs])
     NT = P(*[o[0].data_ptr() for o in out])
     TN = P(*[o[1].data_ptr() for o in out])

@@ -4,9 +4,13 @@
 shapes and dtypes; the work is done by libdgx.so on the tensor's own device
 and current stream.
 """
+import threading
+
 import torch
 
 from . import _native as nat
+
+_tls = threading.local()
 
 
 def reduction_order(x):
@@ -47,31 +51,28 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     stream = nat.stream_of(x)
     with torch.cuda.device(x.device):
         # |x|^2 and the MFMA operand image in one pass over x
-        nat.check(L.dgx_knn_prepare_f32(nat.ptr(x), sB, sC, sN, B, C, N, order, nat.ptr(xx), nat.ptr(img),
+        nat.check(L.dgx_knn_prepare_f32(nat.f32(x), sB, sC, sN, B, C, N, order, nat.f32(xx), nat.f32(img),
                                         img_bytes, stream), "knn prepare")
-        rec = _timing is not None
-        if rec:
+        timing = getattr(_tls, "timing", None)
+        if timing is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        rc = L.dgx_knn_select_f32(nat.ptr(x), sB, sC, sN, nat.ptr(xx), B, C, N, k,
-                                  nat.ptr(idx) if out_dtype == torch.int64 else None,
-                                  nat.ptr(idx) if out_dtype == torch.int32 else None, nat.ptr(vals),
-                                  nat.ptr(img), img_bytes, stream)
-        if rec:
+        rc = L.dgx_knn_select_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
+                                  nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
+                                  nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
+                                  nat.f32(img), img_bytes, stream)
+        if timing is not None:
             ev1.record()
-            _timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
+            timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
     nat.check(rc, "knn")
     return (idx, vals) if return_values else idx
 
 
-# Optional instrumentation (bench.py): when a list, every kNN selection launch
-# appends (start_event, end_event, gram_flops, shape) recorded on the launch stream.
-_timing = None
-
-
 def set_knn_timing(lst):
-    global _timing
-    _timing = lst
+    """Optional per-thread instrumentation (tools): when a list, every kNN
+    selection launch of this thread appends (start_event, end_event,
+    gram_flops, shape) recorded on the launch stream."""
+    _tls.timing = lst
 
 
 def knn(x, k):
@@ -84,6 +85,7 @@ def knn(x, k):
 class _GraphFeature(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, idx32, mode):
+        x = x.float()
         B, C, N = x.shape
         k = idx32.shape[-1]
         if mode == nat.GF_CAT:
@@ -94,8 +96,8 @@ class _GraphFeature(torch.autograd.Function):
             out = torch.empty((B, N, k, C), dtype=torch.float32, device=x.device)
         sB, sC, sN = x.stride()
         with torch.cuda.device(x.device):
-            rc = nat.lib().dgx_graph_feature_f32(nat.ptr(x), sB, sC, sN, B, C, N, nat.ptr(idx32), k, mode,
-                                                 nat.ptr(out), nat.stream_of(x))
+            rc = nat.lib().dgx_graph_feature_f32(nat.f32(x), sB, sC, sN, B, C, N, nat.i32(idx32), k, mode,
+                                                 nat.f32(out), nat.stream_of(x))
         nat.check(rc, "graph_feature")
         ctx.save_for_backward(idx32)
         ctx.mode = mode
@@ -109,8 +111,8 @@ class _GraphFeature(torch.autograd.Function):
         dout = dout.contiguous().float()
         dx = torch.zeros((B, C, N), dtype=torch.float32, device=dout.device)
         with torch.cuda.device(dout.device):
-            rc = nat.lib().dgx_graph_feature_bwd_f32(nat.ptr(dout), B, C, N, nat.ptr(idx32), idx32.shape[-1],
-                                                     ctx.mode, nat.ptr(dx), nat.stream_of(dout))
+            rc = nat.lib().dgx_graph_feature_bwd_f32(nat.f32(dout), B, C, N, nat.i32(idx32), idx32.shape[-1],
+                                                     ctx.mode, nat.f32(dx), nat.stream_of(dout))
         nat.check(rc, "graph_feature backward")
         return dx, None, None
 

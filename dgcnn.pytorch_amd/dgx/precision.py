@@ -9,6 +9,7 @@ distances, BN statistics and every elementwise stage stay fp32 either way.
 Set with ``dgx.precision.set("bf16")`` or the environment variable
 ``DGX_PRECISION=bf16``.
 """
+import functools
 import os
 
 import torch
@@ -39,3 +40,20 @@ def mm(a, b):
     if _mode == "bf16":
         return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
     return torch.mm(a, b)
+
+
+def no_autocast(fn):
+    """Run an autograd.Function's forward/backward with CUDA autocast disabled.
+
+    The reference's DDP script runs the model under torch.cuda.amp.autocast
+    (main_partseg_dist.py:253). Inside the engine's Functions every product
+    must come back in the dtype its consumer kernel is built for, so autocast
+    must not re-type a torch.mm there; the engine computes in its own
+    precision mode instead, on fp32 inputs (each Function casts its input)."""
+    @functools.wraps(fn)
+    def wrapped(*args, **kwargs):
+        if torch.is_autocast_enabled("cuda"):
+            with torch.autocast("cuda", enabled=False):
+                return fn(*args, **kwargs)
+        return fn(*args, **kwargs)
+    return wrapped

@@ -116,6 +116,15 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         double momentum, double eps,
                         float* scale, float* shift, float* mean, float* invstd,
                         int64_t* num_batches_tracked, void* stream);
+/* The same finalize from fp64 column sums (nrows x 2 x Co doubles): the global
+ * sums of a SyncBatchNorm all-reduce (main_partseg_dist.py:189), kept in fp64
+ * into var = E[y^2] - E[y]^2. */
+int dgx_bn_finalize_f64(const double* sums, int nrows, int Co, double count,
+                        const float* gamma, const float* beta,
+                        float* running_mean, float* running_var,
+                        double momentum, double eps,
+                        float* scale, float* shift, float* mean, float* invstd,
+                        int64_t* num_batches_tracked, void* stream);
 int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
                            const float* shift, float slope, float* out, int ldo,
                            void* out_bf16, void* stream);
@@ -146,6 +155,11 @@ int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel,
                         const float* invstd, float slope, float* dzp,
                         float* partials, int nrows, void* stream);
 int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co,
+                            double count, const float* scale, const float* mean,
+                            const float* invstd, float* dgamma, float* dbeta,
+                            float* c0, float* c1, int accumulate, void* stream);
+/* fp64-sums form (SyncBatchNorm backward, after the all-reduce). */
+int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co,
                             double count, const float* scale, const float* mean,
                             const float* invstd, float* dgamma, float* dbeta,
                             float* c0, float* c1, int accumulate, void* stream);
@@ -227,6 +241,13 @@ int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda,
                   const void* B, int b_bf16, int b_ic, int64_t ldb,
                   int M, int N, int K, int epi, int splits,
                   float* C, int64_t ldc, float* partials, void* stream);
+/* Exact fp32 GEMM for a short reduction: C (M x N, row stride ldc) = X W^T,
+ * X (M x K, row stride ldx), W (N x K) dense; each output an fmaf chain over
+ * k = 0..K-1. K <= 16, N % 4 == 0, 16-byte aligned C rows. The layer-1
+ * per-point GEMM on raw xyz (dgcnn.py:55, layers.py:17: K = 3), kept exact in
+ * every precision mode. */
+int dgx_gemm_smallk_f32(const float* X, int64_t ldx, const float* W, int M, int N, int K,
+                        float* C, int64_t ldc, void* stream);
 /* out[orow][ocol] = sum_s slab[s][r][c] (fixed order: deterministic); rows
  * r >= split land at (r - split, c + cols): the [W1;W2] -> [W1 | W2] weight
  * un-stacking (reference conv weight layout (Co, 2C, 1, 1)). */

@@ -92,11 +92,12 @@ def _bn(params, prefix):
 # that each decision is valid (the chosen edge is a max up to rounding; a sign
 # only differs where |z| is at rounding level).
 
-def edgeconv_block_routed(x, weight, bn, idx, arg, zpos, slope=0.2):
-    """x (B,C,N); idx (B,N,k); arg (B*N,Co) chosen k-slot; zpos (B*N,Co) bool."""
+def edgeconv_block_routed(x, weight, bn, idx, arg, zpos, slope=0.2, training=True):
+    """x (B,C,N); idx (B,N,k); arg (B*N,Co) chosen k-slot; zpos (B*N,Co) bool.
+    training=False normalises with the running statistics (BatchNorm eval)."""
     e = graph_feature(x, idx=idx)
     y = F.conv2d(e, weight)
-    z = F.batch_norm(y, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], True,
+    z = F.batch_norm(y, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], training,
                      bn.get("momentum", 0.1), bn.get("eps", 1e-5))
     B, Co, N, _ = z.shape
     a = arg.long().view(B, N, Co).permute(0, 2, 1).unsqueeze(-1)
@@ -105,18 +106,20 @@ def edgeconv_block_routed(x, weight, bn, idx, arg, zpos, slope=0.2):
     return torch.where(m, zsel, slope * zsel), z
 
 
-def dgcnn_routed(x, params, decisions, mask5, slope=0.2):
+def dgcnn_routed(x, params, decisions, mask5, slope=0.2, training=(True,) * 5):
     """DGCNN forward with the engine's decisions: decisions[l] = (idx, arg, zpos)
-    for blocks 1-4, mask5 (B,emb,N) bool = sign of conv5's BN output."""
+    for blocks 1-4, mask5 (B,emb,N) bool = sign of conv5's BN output.
+    training[l]: batch (True) or running (False) statistics for BN l+1."""
     B, _, N = x.shape
     h, feats = x, []
     for i in range(1, 5):
         idx, arg, zpos = decisions[i - 1]
-        h, _ = edgeconv_block_routed(h, params[f"conv{i}.0.weight"], _bn(params, f"conv{i}.1"), idx, arg, zpos, slope)
+        h, _ = edgeconv_block_routed(h, params[f"conv{i}.0.weight"], _bn(params, f"conv{i}.1"), idx, arg, zpos, slope,
+                                     training[i - 1])
         feats.append(h)
     z = torch.cat(feats, dim=1).unsqueeze(-1)
     z = F.conv2d(z, params["conv5.0.weight"])
     bn = _bn(params, "conv5.1")
-    z = F.batch_norm(z, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], True, 0.1, 1e-5)
+    z = F.batch_norm(z, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], training[4], 0.1, 1e-5)
     z = z.view(B, -1, N)
     return torch.where(mask5, z, slope * z)

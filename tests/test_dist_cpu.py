@@ -19,12 +19,14 @@ def _worker(rank, world, port, q):
     try:
         from dgx import dist as D
         import bench
-        sums = torch.arange(6, dtype=torch.float32).view(2, 3) * (rank + 1)
-        tot, cnt = D.allreduce_sums(sums, 10 + rank, dist.group.WORLD)
+        # per-block partials (rows, 2, C): summed in fp64 locally, then across ranks
+        part = torch.arange(12, dtype=torch.float32).view(2, 2, 3) * (rank + 1)
+        tot, cnt = D.allreduce_sums(part, 10 + rank, dist.group.WORLD)
+        assert tot.dtype == torch.float64 and tot.is_contiguous()
         bn = torch.nn.SyncBatchNorm(3)
-        on, grp = D.sync_group(bn, True)
-        off, _ = D.sync_group(bn, False)
-        plain, _ = D.sync_group(torch.nn.BatchNorm2d(3), True)
+        on, grp = D.sync_group(bn.train())
+        off, _ = D.sync_group(bn.eval())
+        plain, _ = D.sync_group(torch.nn.BatchNorm2d(3))
         t = bench.reduce_elapsed(0.5 + rank, world, torch.device("cpu"))
         q.put((rank, tot.tolist(), cnt, on, off, plain, t))
     finally:
@@ -43,7 +45,7 @@ def test_syncbn_stats_allreduce_and_bench_timing_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    exp = (torch.arange(6, dtype=torch.float32).view(2, 3) * 3).tolist()
+    exp = (torch.arange(12, dtype=torch.float64).view(2, 2, 3).sum(0) * 3).tolist()
     for rank, tot, cnt, on, off, plain, t in res:
         assert tot == exp and cnt == 21.0
         assert on and not off and not plain
@@ -53,4 +55,4 @@ def test_syncbn_stats_allreduce_and_bench_timing_gloo():
 def test_sync_group_needs_initialised_world():
     sys.path[:0] = [PKG]
     from dgx import dist as D
-    assert D.sync_group(torch.nn.SyncBatchNorm(4), True) == (False, None)
+    assert D.sync_group(torch.nn.SyncBatchNorm(4)) == (False, None)

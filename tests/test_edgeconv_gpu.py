@@ -40,11 +40,11 @@ class Capture:
     def __enter__(self):
         import dgx.edgeconv as E
         self.E = E
-        E._debug = {}
-        return E._debug
+        E.set_debug_capture({})
+        return E.debug_capture()
 
     def __exit__(self, *exc):
-        self.E._debug = None
+        self.E.set_debug_capture(None)
 
 
 def check_decisions(z64, arg, zpos, B, N):
@@ -145,13 +145,21 @@ def test_dgcnn_train_golden(golden, cuda):
             assert rel_err(b.cpu(), g["after." + n]) < 1e-4, n
 
 
+# Gradient bar of the routed parity test: every parameter of every geometry.
+# Measured engine errors are <= 1e-5 against the fp64 routed oracle (printed by
+# the test; the same routed computation in torch fp32 lands at 1e-6..3e-6), so
+# the bar is held 10x tighter than the 1e-3 contract.
+ROUTED_GRAD_TOL = 1e-4
+
+
 @pytest.mark.parametrize("emb,N,k,B", [(64, 128, 10, 2), (1024, 1024, 20, 4),
                                        (256, 2048, 40, 2),     # cfg3 geometry (N 2048, k 40)
                                        (128, 4096, 20, 1)])    # cfg5 geometry (N 4096, k 20)
 def test_dgcnn_train_routed(golden, cuda, emb, N, k, B):
-    """Strict 1e-3 parity of DGCNN train-mode output and EVERY parameter
-    gradient vs the fp64 oracle following the engine's routing decisions, at
-    the cfg2 / cfg3 / cfg5 cloud sizes (the kernels' LDS slicing changes with N)."""
+    """Strict parity of DGCNN train-mode output and EVERY parameter gradient vs
+    the fp64 oracle following the engine's routing decisions, at the cfg2 /
+    cfg3 / cfg5 cloud sizes (the kernels' LDS slicing changes with N); one
+    fixed bar for every gradient (ROUTED_GRAD_TOL)."""
     from models.dgcnn import DGCNN
     from dgx import synth
     torch.manual_seed(emb + N)
@@ -164,29 +172,29 @@ def test_dgcnn_train_routed(golden, cuda, emb, N, k, B):
         y = m(x)
     gout = torch.from_numpy(synth.uniform(61, tuple(y.shape)) - 0.5)
     y.backward(gout.to(cuda))
-    decisions = [tuple(t.cpu() for t in cap[("fwd", l)]) for l in range(4)]
-    decisions = [(i.long(), a, z) for (i, a, z) in decisions]
-    params = {n: (t.double() if t.is_floating_point() else t) for n, t in init.items()}
-    for n, t in params.items():
-        if t.is_floating_point() and "running" not in n:
-            t.requires_grad_(True)
-    mask5 = (y.detach().cpu() > 0)
-    ref = R.dgcnn_routed(torch.from_numpy(pts).double().permute(0, 2, 1), params, decisions, mask5)
-    ref.backward(gout.double())
-    assert rel_err(y.detach().cpu(), ref.detach()) < TOL
-    # The same routed computation in fp32 (what the reference's fp32 arithmetic
-    # can achieve): gradients that are heavily cancelling sums (conv5's BN
-    # backward makes sum_m dX5 = 0, so e.g. layer 4's beta gradient is a small
-    # difference of large terms) carry fp32 accumulation error well above 1e-3
-    # at large N*k. The engine must be within 1e-3, or no worse than 4x the fp32
-    # restatement, for every parameter.
-    p32 = {n: (t.float().detach().requires_grad_(t.requires_grad) if t.is_floating_point() else t)
-           for n, t in params.items()}
-    ref32 = R.dgcnn_routed(torch.from_numpy(pts).float().permute(0, 2, 1), p32, decisions, mask5)
-    ref32.backward(gout.float())
+    decisions = [tuple(t for t in cap[("fwd", l)]) for l in range(4)]
+    mask5 = y.detach() > 0
+
+    def routed(dtype):
+        params = {n: (t.to(cuda).to(dtype) if t.is_floating_point() else t.to(cuda)) for n, t in init.items()}
+        for n, t in params.items():
+            if t.is_floating_point() and "running" not in n:
+                t.requires_grad_(True)
+        dec = [(i.long(), a, z) for (i, a, z) in decisions]
+        ref = R.dgcnn_routed(torch.from_numpy(pts).to(cuda).to(dtype).permute(0, 2, 1), params, dec, mask5)
+        ref.backward(gout.to(cuda).to(dtype))
+        return ref.detach(), params
+    ref, p64 = routed(torch.float64)
+    _, p32 = routed(torch.float32)
+    assert rel_err(y.detach().cpu(), ref.cpu()) < TOL
+    report = {}
     for n, p in m.named_parameters():
-        e32 = rel_err(p32[n].grad, params[n].grad)
-        assert rel_err(p.grad.cpu(), params[n].grad) < max(TOL, 4 * e32), (n, e32)
+        e = rel_err(p.grad.cpu(), p64[n].grad.cpu())
+        e32 = rel_err(p32[n].grad.cpu(), p64[n].grad.cpu())
+        report[n] = (round(e, 6), round(e32, 6))
+    print("routed grad rel err (engine, torch fp32):", report)
+    for n, (e, _) in report.items():
+        assert e < ROUTED_GRAD_TOL, (n, e)
 
 
 def test_dgcnn_eval_matches_oracle(golden, cuda):
@@ -272,25 +280,67 @@ def test_position_embedding_golden(golden, cuda):
 
 
 def test_dgcnn_full_size_train_step(cuda):
-    """cfg2 shape: finite outputs/grads, BN running stats move, layer-1 kNN
-    equals the oracle at full size (size-independent check)."""
+    """cfg2 shape: finite outputs/grads, BN running stats move, and the chain's
+    layer-1 kNN equals the oracle's at full size."""
+    import oracle as O
     from models.dgcnn import DGCNN
     from dgx import synth
     torch.manual_seed(0)
     m = DGCNN(types.SimpleNamespace(emb_dim=1024, k=20)).to(cuda).train()
-    pts = torch.from_numpy(synth.cube_clouds(32, 1024, 0)).to(cuda)
-    y = m(pts.permute(0, 2, 1))
+    pts = synth.cube_clouds(32, 1024, 0)
+    with Capture() as cap:
+        y = m(torch.from_numpy(pts).to(cuda).permute(0, 2, 1))
     assert tuple(y.shape) == (32, 1024, 1024)
     y.sum().backward()
     assert torch.isfinite(y).all()
     for p in m.parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all()
     assert float(m.conv1[1].running_var.mean()) != 1.0
+    idx1 = cap[("fwd", 0)][0].cpu().numpy()
+    want = O.knn(torch.from_numpy(pts).permute(0, 2, 1), 20)
+    np.testing.assert_array_equal(idx1, want)
+
+
+def test_dgcnn_bf16_headline_cfg2_routed(cuda):
+    """The headline configuration (BASELINE configs[1]: DGCNN(emb 1024), B 32,
+    N 1024, k 20, bf16 GEMMs) at full size: train-mode output and every
+    parameter gradient within SURVEY §8(c)'s bf16 bar (2e-2) of the fp64 oracle
+    routed by the engine's own decisions."""
+    from dgx import precision, synth
+    from models.dgcnn import DGCNN
+    torch.manual_seed(0)
+    B, N, k, emb = 32, 1024, 20, 1024
+    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k))
+    init = {n: t.detach().clone() for n, t in m.state_dict().items()}
+    m = m.to(cuda).train()
+    pts = synth.cube_clouds(B, N, 0)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1)
+    gout = torch.from_numpy(synth.uniform(1234, (B, emb, N)) - 0.5).float()
+    precision.set("bf16")
+    try:
+        with Capture() as cap:
+            y = m(x)
+        y.backward(gout.to(cuda))
+    finally:
+        precision.set("fp32")
+    dec = [(i.long(), a, z) for (i, a, z) in (cap[("fwd", l)] for l in range(4))]
+    params = {n: (t.to(cuda).double() if t.is_floating_point() else t.to(cuda)) for n, t in init.items()}
+    for n, t in params.items():
+        if t.is_floating_point() and "running" not in n:
+            t.requires_grad_(True)
+    ref = R.dgcnn_routed(torch.from_numpy(pts).to(cuda).double().permute(0, 2, 1), params, dec, y.detach() > 0)
+    ref.backward(gout.to(cuda).double())
+    errs = {"out": rel_err(y.detach().cpu(), ref.detach().cpu())}
+    for n, p in m.named_parameters():
+        errs[n] = rel_err(p.grad.cpu(), params[n].grad.cpu())
+    print("bf16 cfg2 rel err:", {n: round(e, 5) for n, e in errs.items()})
+    for n, e in errs.items():
+        assert e < 2e-2, (n, e)
 
 
 def test_dgcnn_bf16_mode_routed(cuda):
-    """bf16 GEMM operands (BASELINE cfg2 precision): output and gradients stay
-    within bf16 operand rounding (3e-2) of the fp64 routed oracle."""
+    """bf16 GEMM operands (BASELINE cfg2 precision), small emb: output and
+    gradients within SURVEY §8(c)'s bf16 bar (2e-2) of the fp64 routed oracle."""
     from dgx import precision, synth
     from models.dgcnn import DGCNN
     torch.manual_seed(7)
@@ -316,6 +366,6 @@ def test_dgcnn_bf16_mode_routed(cuda):
             t.requires_grad_(True)
     ref = R.dgcnn_routed(torch.from_numpy(pts).double().permute(0, 2, 1), params, decisions, y.detach().cpu() > 0)
     ref.backward(gout.double())
-    assert rel_err(y.detach().cpu(), ref.detach()) < 3e-2
+    assert rel_err(y.detach().cpu(), ref.detach()) < 2e-2
     for n, p in m.named_parameters():
-        assert rel_err(p.grad.cpu(), params[n].grad) < 3e-2, n
+        assert rel_err(p.grad.cpu(), params[n].grad) < 2e-2, n
