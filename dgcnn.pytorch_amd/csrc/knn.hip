@@ -24,6 +24,7 @@
 //   knn_fix_kernel    exact recompute of the (rare) rows whose list overflowed.
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "common.h"
 
@@ -680,6 +681,25 @@ int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
 }  // namespace
 
 extern "C" {
+
+const char* dgx_knn_kernel_name(int C, int k) {
+    // the selection kernel dgx_knn_select_f32 launches for (C, k), as profilers print it
+    struct Names {
+        char s[5][5][32];
+        Names() {
+            static const int NS[5] = {1, 3, 8, 16, 32};
+            static const int KBS[5] = {16, 20, 32, 40, 64};
+            for (int a = 0; a < 5; ++a)
+                for (int b = 0; b < 5; ++b) snprintf(s[a][b], sizeof(s[a][b]), "knn_kernel<%d, %d>", NS[a], KBS[b]);
+        }
+    };
+    static const Names names;  // thread-safe one-time initialisation
+    if (C < 1 || C > 128 || k < 1 || k > 64) return "";
+    const int ns = knn_nstep(C);
+    const int a = ns == 1 ? 0 : ns == 3 ? 1 : ns == 8 ? 2 : ns == 16 ? 3 : 4;
+    const int b = k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4;
+    return names.s[a][b];
+}
 
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,
                    void* stream) {

@@ -58,7 +58,10 @@ def _bf16_weight_copies(model):
 class DGCNN(nn.Module):
     """4 EdgeConv blocks (3->64->64->128->256) + conv5 (512->emb); input
     (B,3,N), output (B,emb,N). Reads ``args.emb_dim`` and ``args.k``
-    (reference dgcnn.py:47-78)."""
+    (reference dgcnn.py:47-78). Engine extension: an optional ``args.in_dims``
+    (default 3, the reference's) sets the input channels, e.g. 9 for the S3DIS
+    block layout (prepare_data/indoor3d_util.py:238-261); the default model's
+    parameters and state_dict are the reference's."""
 
     WIDTHS = (64, 64, 128, 256)
 
@@ -66,7 +69,7 @@ class DGCNN(nn.Module):
         super().__init__()
         self.emb_dims = args.emb_dim
         self.k = args.k
-        c_in = 3
+        c_in = getattr(args, "in_dims", 3)
         for i, c_out in enumerate(self.WIDTHS, start=1):
             setattr(self, f"conv{i}", _edge_block(c_in, c_out))
             c_in = c_out
