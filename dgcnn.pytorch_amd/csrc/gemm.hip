@@ -384,7 +384,7 @@ __device__ __forceinline__ bf16x8 frag_tn(const bf16* img, int s, int col0, int 
 template <bool TN, int BM, int BN, int EPI>
 __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
-    int kchunk, float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend,
+    int kchunk, int ka, float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend,
     int64_t ldd) {
     static_assert(BM == G2_BM || (EPI != EPI_STATS && EPI != EPI_STATS16), "stats rows are per 128-row tile");
     constexpr int WN = BN >= 128 ? 2 : 1;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
             stage_tn<BM>(A, lda, i0, M, k0, kend, img, wave, lane);
             stage_tn<BN>(B, ldb, j0, N, k0, kend, img + BM * G2_BK, wave, lane);
         } else {
-            stage_nt<BM>(A, lda, i0, M, k0, img, wave, lane);
+            stage_nt<BM>(A, lda, i0, M, k0 % ka, img, wave, lane);  // ka < K: A reused (split weight)
             stage_nt<BN>(B, ldb, j0, N, k0, img + BM * G2_BK, wave, lane);
         }
     };
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
 }
 
 template <bool TN, int BN, int EPI>
-int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int M, int N, int K, int splits,
+int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int M, int N, int K, int ka, int splits,
                     float* C, int64_t ldc, float* part, const float* addend, int64_t ldd, hipStream_t st) {
     int kchunk = (K + splits - 1) / splits;
     kchunk = (kchunk + G2_BK - 1) / G2_BK * G2_BK;
@@ -595,7 +595,7 @@ int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int 
             const int nI = (M + 63) / 64;
             dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
             hipLaunchKernelGGL((gemm_lds_kernel<TN, 64, BN, EPI>), grid, dim3(GB_THREADS), 0, st, A, lda, B, ldb, M,
-                               N, K, EPI == EPI_SLAB ? kchunk : K, C, ldc, part, addend, ldd);
+                               N, K, EPI == EPI_SLAB ? kchunk : K, ka, C, ldc, part, addend, ldd);
             return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
         }
     }
@@ -603,7 +603,7 @@ int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int 
         const int nI = (M + G2_BM - 1) / G2_BM;
         dim3 grid((unsigned)(nI * nJ), (unsigned)(EPI == EPI_SLAB ? sp : 1));
         hipLaunchKernelGGL((gemm_lds_kernel<TN, G2_BM, BN, EPI>), grid, dim3(GB_THREADS), 0, st, A, lda, B, ldb, M,
-                           N, K, EPI == EPI_SLAB ? kchunk : K, C, ldc, part, addend, ldd);
+                           N, K, EPI == EPI_SLAB ? kchunk : K, ka, C, ldc, part, addend, ldd);
     }
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
@@ -653,9 +653,10 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(WeightPrepJobs j
     __shared__ bf16 tile[WP_T][WP_T + 2];
     int j = 0;
     while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
-    const int Co = jobs.Co[j], C = jobs.C[j], stacked = jobs.stacked[j];
+    const int Co = jobs.Co[j], C = jobs.C[j], stacked = jobs.stacked[j] & 1, split = jobs.stacked[j] & 2;
     const float* __restrict__ W = jobs.W[j];
     const int rows = stacked ? 2 * Co : Co;
+    const int ldn = split ? 2 * C : C;  // split: nt rows are [hi | lo], lo = bf16(w - hi)
     const int ntc = (C + WP_T - 1) / WP_T;
     const int b = blockIdx.x - jobs.first[j];
     const int r0 = (b / ntc) * WP_T, c0 = (b % ntc) * WP_T;
@@ -666,7 +667,8 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(WeightPrepJobs j
         if (r < rows && c < C) {
             const float v = stacked ? W[(int64_t)(r % Co) * 2 * C + (r / Co) * C + c] : W[(int64_t)r * C + c];
             const bf16 h = (bf16)v;
-            jobs.nt[j][(int64_t)r * C + c] = h;
+            jobs.nt[j][(int64_t)r * ldn + c] = h;
+            if (split) jobs.nt[j][(int64_t)r * ldn + C + c] = (bf16)(v - (float)h);
             tile[rr][cc] = h;
         }
     }
@@ -850,9 +852,11 @@ int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda, const void* 
 }
 
 int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int tn, int M, int N, int K,
-                      int epi, int splits, float* C, int64_t ldc, float* partials, const float* addend,
+                      int a_k, int epi, int splits, float* C, int64_t ldc, float* partials, const float* addend,
                       int64_t ldd, void* stream) {
     if (!A || !B || !C || M < 0 || N < 0 || K < 0 || splits < 1) return DGX_EINVAL;
+    if (a_k == 0) a_k = K;
+    if (a_k != K && (tn || a_k < G2_BK || a_k % G2_BK || K % a_k)) return DGX_EUNSUPPORTED;
     if ((epi == EPI_STATS || epi == EPI_STATS16) && !partials) return DGX_EINVAL;
     if (M == 0 || N == 0) return DGX_OK;
     // DMA staging moves 16-B chunks: rows 16-B aligned, whole chunks per row
@@ -865,13 +869,14 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
     const bf16* b = static_cast<const bf16*>(B);
     const bool wide = N > 64;
     if (tn)
-        return wide ? launch_gemm_lds<true, 128, EPI_SLAB>(a, lda, b, ldb, M, N, K, splits, C, ldc, partials, nullptr,
-                                                           0, st)
-                    : launch_gemm_lds<true, 64, EPI_SLAB>(a, lda, b, ldb, M, N, K, splits, C, ldc, partials, nullptr, 0,
-                                                          st);
+        return wide ? launch_gemm_lds<true, 128, EPI_SLAB>(a, lda, b, ldb, M, N, K, K, splits, C, ldc, partials,
+                                                           nullptr, 0, st)
+                    : launch_gemm_lds<true, 64, EPI_SLAB>(a, lda, b, ldb, M, N, K, K, splits, C, ldc, partials, nullptr,
+                                                          0, st);
 #define DGX_G2(E)                                                                                              \
-    return wide ? launch_gemm_lds<false, 128, E>(a, lda, b, ldb, M, N, K, 1, C, ldc, partials, addend, ldd, st) \
-                : launch_gemm_lds<false, 64, E>(a, lda, b, ldb, M, N, K, 1, C, ldc, partials, addend, ldd, st)
+    return wide ? launch_gemm_lds<false, 128, E>(a, lda, b, ldb, M, N, K, a_k, 1, C, ldc, partials, addend, ldd, \
+                                                 st)                                                          \
+                : launch_gemm_lds<false, 64, E>(a, lda, b, ldb, M, N, K, a_k, 1, C, ldc, partials, addend, ldd, st)
     if (epi == EPI_STORE) DGX_G2(EPI_STORE);
     if (epi == EPI_ACCUM) DGX_G2(EPI_ACCUM);
     if (epi == EPI_STATS) DGX_G2(EPI_STATS);
@@ -904,7 +909,7 @@ int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, cons
         jobs.C[j] = C[j];
         jobs.stacked[j] = stacked[j];
         jobs.first[j] = blocks;
-        const int rows = stacked[j] ? 2 * Co[j] : Co[j];
+        const int rows = (stacked[j] & 1) ? 2 * Co[j] : Co[j];
         blocks += ((rows + WP_T - 1) / WP_T) * ((C[j] + WP_T - 1) / WP_T);
     }
     jobs.first[n] = blocks;

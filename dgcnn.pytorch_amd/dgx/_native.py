@@ -62,8 +62,8 @@ _SIGS = {
                       _vp],
     "dgx_gemm_smallk_f32": [_vp, _i64, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_slab_reduce_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp],
-    "dgx_gemm_lds_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _i64,
-                          _vp],
+    "dgx_gemm_lds_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp,
+                          _i64, _vp],
     "dgx_weight_prep_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_weight_prep_multi_bf16": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_pointconv_bf16_rows": [_i32, _i32],

@@ -117,7 +117,7 @@ class _EdgeConvStack(torch.autograd.Function):
         # the block's input is the bf16 twin, i.e. after a selecting block)
         preps = list(ctx_preps) if ctx_preps is not None else [None] * len(layers)
         if bf16 and len(layers) > 1 and ctx_preps is None:
-            jobs = [(params[3 * li], ly.cout, ly.cin, True) for li, ly in enumerate(layers) if li > 0]
+            jobs = [(params[3 * li], ly.cout, ly.cin, True, True) for li, ly in enumerate(layers) if li > 0]
             preps[1:] = G.prep_weights(jobs)
         dbg = debug_capture()
         for li, ly in enumerate(layers):

@@ -160,11 +160,16 @@ def _bf16_2d(t):
 
 def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None, out_bf16=False):
     """out (M,N) = x16 (M,K) @ w16 (N,K)^T (bf16 operands, K % 64 == 0).
+    A split weight w16 (N, 2K) = [W_hi | W_lo] (prep_weights(..., split=True))
+    gives x16 (W_hi + W_lo)^T: the weight with 16 significant bits.
     ``stats``: also returns the BatchNorm column partials (rows, 2, N);
     with ``out_bf16`` the product is stored bf16 (stats from the fp32 sums).
     ``accumulate``: out += ...; with ``addend``: out = addend + ... ."""
     M, K = x16.shape
     N = w16.shape[0]
+    Kw = w16.shape[1]
+    if Kw not in (K, 2 * K):
+        raise RuntimeError(f"dgx gemm: weight k extent {Kw} does not match the operand's {K}")
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x16.device)
     if out.dtype != (torch.bfloat16 if out_bf16 else torch.float32) or out.stride(1) != 1:
@@ -178,9 +183,9 @@ def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None, out_
         raise RuntimeError("dgx gemm: a bf16 product is only stored together with its statistics")
     epi = (EPI_STATS16 if out_bf16 else EPI_STATS) if stats else (
         EPI_ACCUM if (accumulate or addend is not None) else EPI_STORE)
-    with torch.cuda.device(out.device), _Timed(2.0 * M * N * K):
+    with torch.cuda.device(out.device), _Timed(2.0 * M * N * Kw):
         nat.check(nat.lib().dgx_gemm_lds_bf16(
-            nat.ptr(x16), _bf16_2d(x16), nat.ptr(w16), _bf16_2d(w16), 0, M, N, K, epi, 1, nat.ptr(out),
+            nat.ptr(x16), _bf16_2d(x16), nat.ptr(w16), _bf16_2d(w16), 0, M, N, Kw, K, epi, 1, nat.ptr(out),
             out.stride(0), nat.ptr(part), nat.ptr(addend), addend.stride(0) if addend is not None else 0,
             nat.stream_of(out)), "gemm lds nt")
     return (out, part) if stats else out
@@ -202,7 +207,7 @@ def lds_atb(a16, b16, out, split_rows=None):
     with torch.cuda.device(out.device):
         st = nat.stream_of(out)
         with _Timed(2.0 * M * N * R):
-            nat.check(L.dgx_gemm_lds_bf16(nat.ptr(a16), _bf16_2d(a16), nat.ptr(b16), _bf16_2d(b16), 1, M, N, R,
+            nat.check(L.dgx_gemm_lds_bf16(nat.ptr(a16), _bf16_2d(a16), nat.ptr(b16), _bf16_2d(b16), 1, M, N, R, R,
                                           EPI_SLAB, S, nat.ptr(slab), N, None, None, 0, st), "gemm lds tn")
         split = M if split_rows is None else split_rows
         nat.check(L.dgx_slab_reduce_f32(nat.ptr(slab), used, M, N, split, nat.ptr(out), out.stride(0), st),
@@ -223,34 +228,37 @@ def prep_weight(w, rows, cols, stacked):
 
 
 def prep_weights(jobs):
-    """prep_weight for several (w, rows, cols, stacked) jobs in one launch; the
-    bf16 copies share one allocation. Returns [(nt, tn), ...]."""
+    """prep_weight for several (w, rows, cols, stacked[, split]) jobs in one
+    launch; the bf16 copies share one allocation. Returns [(nt, tn), ...].
+    ``split``: nt is (R, 2*cols) = [W_hi | W_lo] for lds_xwt's split-weight
+    form; tn (the backward's operand) is W_hi^T either way."""
     import ctypes
     if not jobs:
         return []
+    jobs = [tuple(j) + (False,) * (5 - len(j)) for j in jobs]
     dev = jobs[0][0].device
-    sizes = [(2 * r if st else r) * c for (_, r, c, st) in jobs]
-    pad = [-(-n // 8) * 8 for n in sizes]  # 16-byte aligned views
-    buf = torch.empty(2 * sum(pad), dtype=torch.bfloat16, device=dev)
+    sizes = [((2 * r if st else r) * c, (2 if sp else 1) * (2 * r if st else r) * c) for (_, r, c, st, sp) in jobs]
+    pads = [(-(-a // 8) * 8, -(-b // 8) * 8) for (a, b) in sizes]  # 16-byte aligned views
+    buf = torch.empty(sum(a + b for a, b in pads), dtype=torch.bfloat16, device=dev)
     out, off = [], 0
-    for (w, r, c, st), n, p_ in zip(jobs, sizes, pad):
+    for (w, r, c, st, sp), (n_tn, n_nt), (p_tn, p_nt) in zip(jobs, sizes, pads):
         R = 2 * r if st else r
-        nt = buf[off:off + n].view(R, c)
-        tn = buf[off + p_:off + p_ + n].view(c, R)
-        off += 2 * p_
+        nt = buf[off:off + n_nt].view(R, 2 * c if sp else c)
+        tn = buf[off + p_nt:off + p_nt + n_tn].view(c, R)
+        off += p_nt + p_tn
         out.append((nt, tn))
     n = len(jobs)
     P = ctypes.c_void_p * n
     I = ctypes.c_int * n
     # host arrays kept in locals for the duration of the call
-    if any(w.dtype != torch.float32 for (w, _, _, _) in jobs):
+    if any(w.dtype != torch.float32 for (w, _, _, _, _) in jobs):
         raise RuntimeError("dgx weight prep: fp32 weights expected")
-    W = P(*[w.data_ptr() for (w, _, _, _) in jobs])
+    W = P(*[w.data_ptr() for (w, _, _, _, _) in jobs])
     NT = P(*[o[0].data_ptr() for o in out])
     TN = P(*[o[1].data_ptr() for o in out])
-    CO = I(*[r for (_, r, _, _) in jobs])
-    CI = I(*[c for (_, _, c, _) in jobs])
-    ST = I(*[int(st) for (_, _, _, st) in jobs])
+    CO = I(*[r for (_, r, _, _, _) in jobs])
+    CI = I(*[c for (_, _, c, _, _) in jobs])
+    ST = I(*[int(st) | (2 * int(sp)) for (_, _, _, st, sp) in jobs])
     with torch.cuda.device(dev):
         nat.check(nat.lib().dgx_weight_prep_multi_bf16(
             n, ctypes.addressof(W), ctypes.addressof(CO), ctypes.addressof(CI), ctypes.addressof(ST),

@@ -47,8 +47,11 @@ def _bf16_weight_copies(model):
         return None
     jobs = []
     for conv in (model.conv2, model.conv3, model.conv4):
+        # EdgeConv weights in the split (hi + lo) form: BN normalises edge values
+        # y = P_j + Q_i whose batch spread is small next to their size, so the
+        # weights' bf16 rounding is the largest error term the blocks can shed cheaply
         w = conv[0].weight
-        jobs.append((w, w.shape[0], w.shape[1] // 2, True))
+        jobs.append((w, w.shape[0], w.shape[1] // 2, True, True))
     w5 = model.conv5[0].weight
     jobs.append((w5, w5.shape[0], w5.shape[1], False))
     out = _gemm.prep_weights(jobs)

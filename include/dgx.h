@@ -263,9 +263,12 @@ int dgx_slab_reduce_f32(const float* slab, int S, int rows, int cols, int split,
  * (K,M), B (K,N) row-major (the weight gradients), M, N multiples of 8, epi 3
  * (split-K slabs). lda, ldb multiples of 8, 16-byte aligned bases; anything
  * else returns DGX_EUNSUPPORTED (callers then use dgx_gemm_bf16). With epi 1
- * and addend != NULL: C = addend (row stride ldd) + A B^T (C need not hold data). */
+ * and addend != NULL: C = addend (row stride ldd) + A B^T (C need not hold data).
+ * a_k (tn = 0): A's k extent; 0 or K for a plain GEMM, K/2 for a split weight
+ * B = [W_hi | W_lo] (N x K, W_lo = bf16(W - W_hi)): C = A W_hi^T + A W_lo^T,
+ * i.e. the weight operand carries 16 significant bits (a_k % 64 == 0). */
 int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int tn,
-                      int M, int N, int K, int epi, int splits, float* C,
+                      int M, int N, int K, int a_k, int epi, int splits, float* C,
                       int64_t ldc, float* partials, const float* addend,
                       int64_t ldd, void* stream);
 /* bf16 weight operands per step: nt = [rows][C], tn = its transpose. stacked
@@ -274,7 +277,9 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
 int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt,
                          void* tn, void* stream);
 /* dgx_weight_prep_bf16 for n <= 8 weights in one launch (host arrays of
- * length n: one job per EdgeConv block of a forward). */
+ * length n: one job per EdgeConv block of a forward). stacked[j] bit 0: an
+ * EdgeConv weight as above; bit 1: nt is the split form [rows][2C] = [hi | lo]
+ * (lo = bf16(w - hi)) for dgx_gemm_lds_bf16's a_k = C; tn stays hi only. */
 int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, const int* C, const int* stacked,
                                void* const* nt, void* const* tn, void* stream);
 

@@ -199,3 +199,41 @@ def test_weight_prep_multi(cuda):
     for w, (co, c, st), (nt, tn) in zip(ws, shapes, got):
         ent, etn = G.prep_weight(w, co, c, st)
         assert torch.equal(nt, ent) and torch.equal(tn, etn)
+
+
+def test_weight_prep_split(cuda):
+    """Split form: nt = [W_hi | W_lo] with W_hi = bf16(W), W_lo = bf16(W - W_hi);
+    tn stays W_hi^T (the backward operand)."""
+    from dgx import gemm as G
+    torch.manual_seed(6)
+    shapes = [(64, 64, True), (256, 128, True), (1024, 512, False)]
+    ws = [torch.randn(co, 2 * c if st else c, 1, 1, device=cuda) for (co, c, st) in shapes]
+    got = G.prep_weights([(w, co, c, st, True) for w, (co, c, st) in zip(ws, shapes)])
+    for w, (co, c, st), (nt, tn) in zip(ws, shapes, got):
+        w2 = w.reshape(co, -1)
+        exp = torch.cat([w2[:, :c], w2[:, c:]], dim=0) if st else w2
+        hi = exp.to(torch.bfloat16)
+        lo = (exp - hi.float()).to(torch.bfloat16)
+        assert nt.shape == (exp.shape[0], 2 * c)
+        assert torch.equal(nt[:, :c], hi) and torch.equal(nt[:, c:], lo)
+        assert torch.equal(tn, hi.t().contiguous())
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 128, 64), (3000, 512, 128), (32768, 1024, 512)])
+def test_lds_xwt_split_weight(cuda, M, N, K):
+    """x16 [W_hi | W_lo]^T with the A tile reused for both halves equals the fp64
+    product of the bf16 operand with the 16-significant-bit weight."""
+    from dgx import gemm as G
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = torch.randn(N, K, 1, 1, device=cuda) / K ** 0.5
+    (nt, _), = G.prep_weights([(w, N, K, False, True)])
+    z = G.lds_xwt(x, nt)
+    wsplit = nt[:, :K].double() + nt[:, K:].double()
+    ref = x.double() @ wsplit.t()
+    assert rel_err(z.cpu().numpy(), ref.cpu().numpy()) < TOL
+    # and it is closer to the fp32 weight than the hi part alone
+    exact = x.double() @ w.reshape(N, K).double().t()
+    e_split = float((z.double() - exact).abs().max())
+    e_hi = float((G.lds_xwt(x, nt[:, :K].contiguous()).double() - exact).abs().max())
+    assert e_split < 0.25 * e_hi

@@ -33,32 +33,49 @@ def main():
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--emb", type=int, default=1024)
     ap.add_argument("--z32", action="store_true", help="store conv5's Z in fp32 instead of bf16")
-    ap.add_argument("--l1exact", action="store_true", help="block 1 PQ GEMM (K=3) in exact fp32")
-    ap.add_argument("--edgefwd32", action="store_true", help="every EdgeConv forward GEMM in fp32")
+    ap.add_argument("--wexact", choices=["none", "edge", "conv5", "both"], default="none",
+                    help="forward GEMMs with the fp32 (unrounded) weight: emulates a hi+lo bf16 weight split")
     a = ap.parse_args()
     from dgx import gemm as G0
-    if a.l1exact or a.edgefwd32:
-        orig_mm, orig_lds = G0.mm_xwt, G0.lds_xwt
+    if a.wexact != "none":
+        orig_prep_many, orig_prep_one, orig_lds = G0.prep_weights, G0.prep_weight, G0.lds_xwt
+        from dgx.edgeconv import split_weight
+
+        def tag(nt, w, rows, cols, stacked):
+            nt.w32 = split_weight(w, cols, rows) if stacked else w.reshape(rows, cols)
+            return nt
+
+        def prep_weights(jobs):
+            out = orig_prep_many(jobs)
+            res = []
+            for (w, r, c, st), (nt, tn) in zip(jobs, out):
+                want = (st and a.wexact in ("edge", "both")) or (not st and a.wexact in ("conv5", "both"))
+                res.append((tag(nt, w, r, c, st) if want else nt, tn))
+            return res
+
+        def lds_xwt(x16, w16, *args, **kw):
+            if hasattr(w16, "w32") and not args and not kw.get("accumulate") and kw.get("addend") is None:
+                z = torch.mm(x16.float(), w16.w32.t())
+                if kw.get("stats"):
+                    part = torch.stack([z.sum(0), (z * z).sum(0)]).unsqueeze(0).contiguous()
+                    return (z.to(torch.bfloat16) if kw.get("out_bf16") else z), part
+                return z
+            return orig_lds(x16, w16, *args, **kw)
 
         class _GE:
             def __getattr__(self, n):
                 return getattr(G0, n)
-
-            @staticmethod
-            def mm_xwt(x, w, *args, **kw):
-                if x.shape[1] <= 8 or a.edgefwd32:
-                    return torch.mm(x.float(), w.float().t())
-                return orig_mm(x, w, *args, **kw)
-
-            @staticmethod
-            def lds_xwt(x16, w16, *args, **kw):
-                if a.edgefwd32 and not kw and not args:
-                    return torch.mm(x16.float(), w16.float().t())
-                return orig_lds(x16, w16, *args, **kw)
-        E.G = _GE()
+        ge = _GE()
+        ge.prep_weights = prep_weights
+        ge.lds_xwt = lds_xwt
+        import dgx.pointconv as P0
+        import models.dgcnn as MD
+        E.G = ge
+        P0.G = ge
+        MD._gemm = ge
     if a.z32:
-        from dgx import gemm as G
         from dgx import pointconv as P
+        G = P.G
         orig = G.lds_xwt
 
         class _G:
