@@ -579,6 +579,235 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 NT tile for the large GEMMs (conv5 forward Z = Xcat W5^T, K = 512,
+// and its input gradient dX = dZ W5, K = emb; models/dgcnn.py:74-78, 100-102).
+// 8 waves (2 along M x 4 along N), each owning a 128 x 64 sub-tile = 8 x 4
+// blocks of v_mfma_f32_16x16x32_bf16 (128 accumulator registers), K-steps of 64.
+// Operands move by LDS-DMA (global_load_lds_dwordx4) into rings sized by where
+// they come from: A (the activation stream, read once from HBM) has 3 slots and
+// is fetched two K-steps ahead; B (the weight, L2-resident) has 2 slots and is
+// fetched one K-step ahead. 3 x 32 + 2 x 32 KiB = the whole 160 KiB of LDS. Each
+// K-step is four MFMA phases (one C quadrant x K = 64 = 16 MFMAs, fragments read
+// where they change); the next K-steps' DMA is issued in pieces across the
+// phases, B(t+1) before A(t+2), so the K-step ends on a COUNTED vmcnt (A(t+2)
+// stays in flight) and a raw s_barrier: no drain of the DMA queue in the loop.
+// LDS image per operand: [row][64 k] bf16, 128-B rows; 16-B chunk c of row r at
+// position c ^ ((r >> 1) & 7): a ds_read_b128 lane group (16 rows, one chunk)
+// then covers the 16 (row parity, position) slots of a 256-B bank row once —
+// conflict-free (the swizzle is applied to each lane's SOURCE address, the DMA
+// destination being lane-linear).
+constexpr int G3_BM = 256, G3_BN = 256, G3_BK = 64, G3_THREADS = 512;
+constexpr int G3_TILE = G3_BM * G3_BK;  // bf16 elements of one operand's K-step image (32 KiB)
+constexpr int G3_ASLOTS = 3, G3_BSLOTS = 2;
+
+__device__ __forceinline__ int g3_pos(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+// Half h (rows [128h, 128h + 128)) of one operand's K-step image: 16 KiB = 16
+// wave-instructions; wave w issues instructions 2w, 2w + 1.
+__device__ __forceinline__ void g3_stage_half(const bf16* __restrict__ src, int64_t ld, int r0, int rows, int kc,
+                                              bf16* img, int h, int wave, int lane) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int inst = h * 16 + wave * 2 + u;  // 1 KiB = 8 rows per instruction
+        const int row = inst * 8 + (lane >> 3);
+        const int pos = lane & 7;
+        const int c = pos ^ ((row >> 1) & 7);   // the chunk this lane's DMA lands at `pos`
+        const int gr = min(r0 + row, rows - 1);
+        dma16(src + (int64_t)gr * ld + kc + 8 * c, img + inst * 512);
+    }
+}
+
+__device__ __forceinline__ bf16x8 g3_frag(const bf16* img, int row, int chunk) {
+    return *reinterpret_cast<const bf16x8*>(img + row * 64 + (g3_pos(row, chunk) << 3));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(G3_THREADS, 1) void gemm256_nt_kernel(
+    const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K, int ka,
+    float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend, int64_t ldd) {
+    // A ring (3 slots) | B ring (2 slots): one array (a second __shared__ object
+    // can make hipcc wait for the DMA queue before every ds_read)
+    __shared__ __attribute__((aligned(16))) bf16 lds[(G3_ASLOTS + G3_BSLOTS) * G3_TILE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int nJ = (N + G3_BN - 1) / G3_BN;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ti = L / nJ, tj = L - ti * nJ;
+    const int i0 = ti * G3_BM, j0 = tj * G3_BN;
+    const int nk = K / G3_BK;
+    bf16* const aring = lds;
+    bf16* const bring = lds + G3_ASLOTS * G3_TILE;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto stageA = [&](int t, int h) {
+        if (t < nk) g3_stage_half(A, lda, i0, M, (t * G3_BK) % ka, aring + (t % G3_ASLOTS) * G3_TILE, h, wave, lane);
+    };
+    auto stageB = [&](int t, int h) {
+        if (t < nk) g3_stage_half(B, ldb, j0, N, t * G3_BK, bring + (t % G3_BSLOTS) * G3_TILE, h, wave, lane);
+    };
+    // prologue: A(0), B(0), then A(1) left in flight (4 DMA per thread per operand K-step)
+    stageA(0, 0); stageA(0, 1);
+    stageB(0, 0); stageB(0, 1);
+    stageA(1, 0); stageA(1, 1);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int t = 0; t < nk; ++t) {
+        const bf16* As = aring + (t % G3_ASLOTS) * G3_TILE;
+        const bf16* Bs = bring + (t % G3_BSLOTS) * G3_TILE;
+        bf16x8 bfr[2][2][2];  // [col half][col block][k sub-step]
+        bf16x8 afr[4][2];     // [row block of the row half][k sub-step]
+        // quadrant order (row half, col half): (0,0) (0,1) (1,1) (1,0): A read twice, B once
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rh = q >> 1;
+            const int ch = (q == 1 || q == 2) ? 1 : 0;
+            if (q == 0) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+#pragma unroll
+                        for (int s = 0; s < 2; ++s)
+                            bfr[h][b][s] = g3_frag(Bs, wc * 64 + h * 32 + b * 16 + fr, s * 4 + fq);
+            }
+            if (q == 0 || q == 2) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+                        afr[a][s] = g3_frag(As, wr * 128 + rh * 64 + a * 16 + fr, s * 4 + fq);
+            }
+            // next K-steps' DMA: B(t+1) in phases 0-1, then A(t+2) in phases 2-3
+            if (q < 2) stageB(t + 1, q);
+            else stageA(t + 2, q - 2);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[rh * 4 + a][ch * 2 + b] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[a][s], bfr[ch][b][s], acc[rh * 4 + a][ch * 2 + b],
+                                                                    0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        // A(t+1) and B(t+1) landed (A(t+2) may stay in flight), and every wave is
+        // done reading the slots the next K-step's DMA overwrites
+        if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+
+    // ---- epilogue
+    // accumulator (a, b)[r]: row wr*128 + a*16 + fq*4 + r, column wc*64 + b*16 + fr
+    if (EPI == EPI_STATS || EPI == EPI_STATS16) {
+        // BatchNorm column partials of this wave's 128 rows from the fp32 sums:
+        // partial row 2*ti + wr (128-row granularity, dgx_gemm_stats_rows)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            float s1 = 0.f, s2 = 0.f;
+            const int col = j0 + wc * 64 + b * 16 + fr;
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool ok = i0 + wr * 128 + a * 16 + fq * 4 + r < M && col < N;
+                    const float v = ok ? acc[a][b][r] : 0.f;
+                    s1 += v;
+                    s2 = fmaf(v, v, s2);
+                }
+            s1 += __shfl_xor(s1, 16);
+            s2 += __shfl_xor(s2, 16);
+            s1 += __shfl_xor(s1, 32);
+            s2 += __shfl_xor(s2, 32);
+            const int prow = 2 * ti + wr;
+            if (fq == 0 && col < N && i0 + wr * 128 < M) {
+                part[(int64_t)prow * 2 * N + col] = s1;
+                part[(int64_t)prow * 2 * N + N + col] = s2;
+            }
+        }
+    }
+    // Output through LDS in 4 rounds of 64 rows x 256 columns (fp32, padded
+    // rows): waves holding those rows write their accumulators, then every
+    // thread moves 16-byte row pieces (4 fp32 / 8 bf16 outputs per store).
+    constexpr int LDT = G3_BN + 4;
+    constexpr int VO = EPI == EPI_STATS16 ? 8 : 4;
+    constexpr int CPR = G3_BN / VO;
+    float* tile = reinterpret_cast<float*>(lds);
+    const bool vec_out = (ldc % VO) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0 &&
+                         (EPI != EPI_ACCUM || !addend ||
+                          ((ldd % 4) == 0 && (reinterpret_cast<uintptr_t>(addend) & 15) == 0));
+#pragma unroll
+    for (int rnd = 0; rnd < 4; ++rnd) {
+        // round rnd holds rows [64 rnd, 64 rnd + 64): wave half wr = rnd >> 1, row blocks 4*(rnd&1) .. +4
+        if (wr == (rnd >> 1)) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        tile[(a * 16 + fq * 4 + r) * LDT + wc * 64 + b * 16 + fr] = acc[(rnd & 1) * 4 + a][b][r];
+        }
+        __syncthreads();
+        for (int e = tid; e < 64 * CPR; e += G3_THREADS) {
+            const int rr = e / CPR, c = (e - rr * CPR) * VO;
+            const int i = i0 + rnd * 64 + rr, j = j0 + c;
+            if (i >= M || j >= N) continue;
+            const float* src = tile + rr * LDT + c;
+            if (vec_out && j + VO <= N) {
+                if constexpr (EPI == EPI_STATS16) {
+                    const float4 u = *reinterpret_cast<const float4*>(src);
+                    const float4 w = *reinterpret_cast<const float4*>(src + 4);
+                    bf16x8 h = {(bf16)u.x, (bf16)u.y, (bf16)u.z, (bf16)u.w, (bf16)w.x, (bf16)w.y, (bf16)w.z, (bf16)w.w};
+                    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(C) + (int64_t)i * ldc + j) = h;
+                } else {
+                    float4 v = *reinterpret_cast<const float4*>(src);
+                    float4* dst = reinterpret_cast<float4*>(C + (int64_t)i * ldc + j);
+                    if (EPI == EPI_ACCUM) {
+                        const float4 o = addend ? *reinterpret_cast<const float4*>(addend + (int64_t)i * ldd + j) : *dst;
+                        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+                    }
+                    *dst = v;
+                }
+            } else {
+                for (int u = 0; u < VO && j + u < N; ++u) {
+                    const float v = src[u];
+                    if (EPI == EPI_STATS16) {
+                        reinterpret_cast<bf16*>(C)[(int64_t)i * ldc + j + u] = (bf16)v;
+                    } else {
+                        float* dst = C + (int64_t)i * ldc + j + u;
+                        if (EPI == EPI_ACCUM) *dst = (addend ? addend[(int64_t)i * ldd + j + u] : *dst) + v;
+                        else *dst = v;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int EPI>
+int launch_gemm256(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int M, int N, int K, int ka, float* C,
+                   int64_t ldc, float* part, const float* addend, int64_t ldd, hipStream_t st) {
+    const int nI = (M + G3_BM - 1) / G3_BM, nJ = (N + G3_BN - 1) / G3_BN;
+    hipLaunchKernelGGL((gemm256_nt_kernel<EPI>), dim3((unsigned)(nI * nJ)), dim3(G3_THREADS), 0, st, A, lda, B, ldb,
+                       M, N, K, ka, C, ldc, part, addend, ldd);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
 template <bool TN, int BN, int EPI>
 int launch_gemm_lds(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int M, int N, int K, int ka, int splits,
                     float* C, int64_t ldc, float* part, const float* addend, int64_t ldd, hipStream_t st) {
@@ -873,6 +1102,20 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
                                                            nullptr, 0, st)
                     : launch_gemm_lds<true, 64, EPI_SLAB>(a, lda, b, ldb, M, N, K, K, splits, C, ldc, partials, nullptr,
                                                           0, st);
+    // large NT GEMMs (conv5 forward and input gradient): 256 x 256 tiles when
+    // they fill the chip (>= 256 tiles) and every tile is whole along N and K
+    const bool big = (int64_t)((M + G3_BM - 1) / G3_BM) * ((N + G3_BN - 1) / G3_BN) >= 256 && N % G3_BN == 0 &&
+                     K % G3_BK == 0 && a_k % G3_BK == 0;
+    if (big) {
+        if (epi == EPI_STORE) return launch_gemm256<EPI_STORE>(a, lda, b, ldb, M, N, K, a_k, C, ldc, partials, addend,
+                                                              ldd, st);
+        if (epi == EPI_ACCUM) return launch_gemm256<EPI_ACCUM>(a, lda, b, ldb, M, N, K, a_k, C, ldc, partials, addend,
+                                                              ldd, st);
+        if (epi == EPI_STATS) return launch_gemm256<EPI_STATS>(a, lda, b, ldb, M, N, K, a_k, C, ldc, partials, addend,
+                                                              ldd, st);
+        if (epi == EPI_STATS16)
+            return launch_gemm256<EPI_STATS16>(a, lda, b, ldb, M, N, K, a_k, C, ldc, partials, addend, ldd, st);
+    }
 #define DGX_G2(E)                                                                                              \
     return wide ? launch_gemm_lds<false, 128, E>(a, lda, b, ldb, M, N, K, a_k, 1, C, ldc, partials, addend, ldd, \
                                                  st)                                                          \

@@ -116,8 +116,8 @@ def test_gemm_rejects_unsupported(cuda):
 
 # ---- bf16-operand path: LDS-DMA staging (global_load_lds), transposed reads ----
 
-@pytest.mark.parametrize("M,N,K", [(32768, 1024, 512), (1000, 128, 64), (777, 64, 128), (3000, 512, 1024),
-                                   (129, 200, 192)])
+@pytest.mark.parametrize("M,N,K", [(32768, 1024, 512), (32768, 512, 1024), (65536 + 300, 256, 64), (1000, 128, 64),
+                                   (777, 64, 128), (3000, 512, 1024), (129, 200, 192)])
 def test_lds_xwt_store_stats_addend(cuda, M, N, K):
     from dgx import gemm as G
     torch.manual_seed(M + 3 * N + K)
@@ -128,6 +128,8 @@ def test_lds_xwt_store_stats_addend(cuda, M, N, K):
     assert rel_err(z.cpu().numpy(), ref.numpy()) < TOL
     z2, part = G.lds_xwt(x, w, stats=True)
     assert torch.equal(z, z2)
+    z16, part16 = G.lds_xwt(x, w, stats=True, out_bf16=True)
+    assert torch.equal(z16, z.to(torch.bfloat16)) and torch.equal(part16, part)
     ps = part.double().sum(0).cpu()
     zd = z.double().cpu()
     assert rel_err(ps[0].numpy(), zd.sum(0).numpy()) < 1e-4
