@@ -29,7 +29,7 @@ from .ops import knn_raw, reduction_order
 class _EdgeMLP2(torch.autograd.Function):
     @staticmethod
     @prec.no_autocast
-    def forward(ctx, x, k, bn1, bn2, slope1, slope2, need_grad, w1, g1, b1, w2, g2, b2):
+    def forward(ctx, x, k, bn1, bn2, slope1, slope2, need_grad, knn_src, w1, g1, b1, w2, g2, b2):
         x = x.float()
         dev = x.device
         B, C, N = x.shape
@@ -39,7 +39,8 @@ class _EdgeMLP2(torch.autograd.Function):
         stream = nat.stream_of(x)
         bf16 = prec.get() == "bf16"
         X = x.permute(0, 2, 1).reshape(M, C)
-        idx = knn_raw(x, k, order=reduction_order(x), out_dtype=torch.int32)      # layers.py:45 -> dgcnn.py:21
+        kx = x if knn_src is None else knn_src.float()                            # neighbours found on kx
+        idx = knn_raw(kx, k, order=reduction_order(kx), out_dtype=torch.int32)   # layers.py:45 -> dgcnn.py:21
         w1s = split_weight(w1, C, C1)
         if C <= G.SMALLK_MAX:  # raw coordinates (K = 3): exact fp32 in every mode
             PQ = G.mm_smallk(X, w1s)                                              # (M, 2C1)
@@ -166,16 +167,18 @@ class _EdgeMLP2(torch.autograd.Function):
             gw1 = torch.cat([dwcat[:C1], dwcat[C1:]], dim=1).reshape(w1.shape)
             if ctx.needs_input_grad[0]:
                 dx = prec.mm(dPQ, split_weight(w1, C, C1)).view(B, N, C).permute(0, 2, 1)
-        return (dx, None, None, None, None, None, None, gw1, dg1, db1, gw2.view(w2.shape), dg2, db2)
+        return (dx, None, None, None, None, None, None, None, gw1, dg1, db1, gw2.view(w2.shape), dg2, db2)
 
 
-def edge_mlp2(x, k, conv1, conv2, training=None):
+def edge_mlp2(x, k, conv1, conv2, training=None, knn_src=None):
     """max_k conv2(conv1(get_graph_feature(x, k))) for conv1/conv2 =
     nn.Sequential(Conv2d(1x1, bias=False), BatchNorm2d, LeakyReLU) as
     PositionEmbedding builds them (reference models/layers.py:17-20, 45-52).
     Returns (B, C2, N) (a permuted view of a point-major buffer).
     ``training`` is accepted for call compatibility only (dgx.bn: each BN
-    module's own flags decide batch vs running statistics)."""
+    module's own flags decide batch vs running statistics). ``knn_src``:
+    optional (B, C', N) tensor the neighbours are searched on instead of x
+    (upstream's dim9 semseg graph: kNN on the normalised xyz channels)."""
     nat.require_device(x)
     if x.dtype != torch.float32:
         x = x.float()
@@ -190,4 +193,9 @@ def edge_mlp2(x, k, conv1, conv2, training=None):
         raise RuntimeError(f"dgx edge MLP: conv1 expects {cv1.weight.shape[1]} edge channels, input has C={x.shape[1]}")
     params = (cv1.weight, bn1.weight, bn1.bias, cv2.weight, bn2.weight, bn2.bias)
     need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
-    return _EdgeMLP2.apply(x, k, bn1, bn2, act1.negative_slope, act2.negative_slope, need_grad, *params)
+    if knn_src is not None:
+        nat.require_device(knn_src)
+        knn_src = knn_src.detach()
+        if knn_src.shape[0] != x.shape[0] or knn_src.shape[2] != x.shape[2]:
+            raise RuntimeError("dgx edge MLP: knn_src must be (B, C', N) with the input's B and N")
+    return _EdgeMLP2.apply(x, k, bn1, bn2, act1.negative_slope, act2.negative_slope, need_grad, knn_src, *params)

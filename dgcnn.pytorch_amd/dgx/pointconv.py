@@ -73,6 +73,7 @@ class _PointConvBNLReLU(torch.autograd.Function):
         ctx.meta = (B, N, float(slope), bf16)
         ctx.st = st
         ctx.wprep = wprep
+        ctx.wshape = weight.shape
         ctx.save_for_backward(Xop, W, Z)
         return out
 
@@ -122,13 +123,13 @@ class _PointConvBNLReLU(torch.autograd.Function):
         else:
             dW = torch.mm(dZ.t(), Xop)
             dX = torch.mm(dZ, W)
-        return dX, None, None, None, None, None, None, dW.view(Co, -1, 1, 1), dgamma, dbeta
+        return dX, None, None, None, None, None, None, dW.view(ctx.wshape), dgamma, dbeta
 
 
 def pointconv_bn_lrelu(X, B, N, seq, training=None, X16=None, wprep=None):
     """X (B*N, K) point-major -> (B, Co, N) = LeakyReLU(BN(Conv1x1(X))) with the
-    modules of ``seq`` = nn.Sequential(Conv2d(K,Co,1,bias=False), BatchNorm2d,
-    LeakyReLU) (reference dgcnn.py:74-78). ``X16``: optional bf16 twin of X
+    modules of ``seq`` = nn.Sequential(Conv2d(K,Co,1,bias=False) or Conv1d,
+    BatchNorm2d/1d, LeakyReLU) (reference dgcnn.py:74-78). ``X16``: optional bf16 twin of X
     (precision "bf16"), the GEMM operand. ``wprep``: optional bf16 (W, W^T) of
     the conv weight already made for this step (gemm.prep_weights).
     ``training`` is accepted for call compatibility only (dgx.bn: each BN
