@@ -76,6 +76,7 @@ _SIGS = {
     "dgx_edge_mlp_h1_bwd_f32": [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i32,
                                 _vp],
     "dgx_edge_mlp_scatter_f32": [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "dgx_hog_1x1_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
 }
 _RESTYPES = {
     "dgx_version": ctypes.c_char_p,

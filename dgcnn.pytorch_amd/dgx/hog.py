@@ -1,0 +1,26 @@
+"""compute_hog_1x1's work after the kNN call, on the device (SURVEY §8 row f1;
+reference models/model_partseg.py:28-92): one C-ABI call (dgx_hog_1x1_f32,
+csrc/hog.hip) replaces the D2H copy, np.linalg.svd over B*N neighbourhoods,
+the H2D copy and the histogram votes. No host round trip, no CPU fallback."""
+import torch
+
+from . import _native as N
+
+
+def hog_1x1(x, idx):
+    """x (B, 3, N) fp32 on the device, idx (B, N, k) int64 local kNN ids ->
+    (B, N, 18) histograms, as the reference computes them from the same idx."""
+    N.require_device(x, idx)
+    B, C, P = x.shape
+    if C != 3:
+        raise RuntimeError(f"dgx: compute_hog_1x1 takes (B, 3, N) clouds, got {tuple(x.shape)}")
+    k = idx.shape[-1]
+    if tuple(idx.shape) != (B, P, k):
+        raise RuntimeError(f"dgx: kNN ids of shape {tuple(idx.shape)} do not match the cloud {tuple(x.shape)}")
+    x = x.contiguous()
+    idx = idx.contiguous()
+    axis = torch.empty((P, 4), device=x.device, dtype=torch.float32)
+    out = torch.empty((B, P, 18), device=x.device, dtype=torch.float32)
+    N.check(N.lib().dgx_hog_1x1_f32(N.f32(x), N.ptr(idx, N.I64), B, P, k, N.f32(axis), N.f32(out),
+                                    N.stream_of(x)), "hog_1x1")
+    return out

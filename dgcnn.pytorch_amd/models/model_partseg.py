@@ -1,44 +1,33 @@
 """Drop-in for reference ``models/model_partseg.py``: ``compute_hog_1x1``,
-``MLPHead``, ``Net`` (SURVEY §8 rows a7, a9).
+``MLPHead``, ``Net`` (SURVEY §8 rows a7, a9, f1).
 
-Engine work on this path is the kNN: ``Net.forward`` reaches it three times on
+Engine work on this path: the kNN, which ``Net.forward`` reaches three times on
 the same cloud — the four EdgeConv blocks of ``emb_nn`` (model_partseg.py:177),
 the HOG neighbourhoods (model_partseg.py:179 -> :26) and ``pos_mlp``'s
-PositionEmbedding (model_partseg.py:183). All three bind to the engine through
-``models.dgcnn`` exactly as the reference binds by name (model_partseg.py:11-12).
+PositionEmbedding (model_partseg.py:183), all bound through ``models.dgcnn``
+as the reference binds them (model_partseg.py:11-12) — and the rest of
+``compute_hog_1x1`` (row f1): the reference's D2H copy, np.linalg.svd over B*N
+neighbourhoods, H2D copy and histogram votes (model_partseg.py:28-92) are one
+device call (dgx.hog, csrc/hog.hip) with LAPACK's singular-vector signs.
 
-Everything else here is the reference's own PyTorch composition, kept as-is
-because it is out of the engine's scope:
-the HOG's host-side SVD round trip, its histogram votes, and the transformer /
-attention / MLP head, which run as stock PyTorch-ROCm modules. Two reference
-behaviours are reproduced on purpose, because checkpoints and downstream
-numbers depend on them:
+The transformer / attention / MLP head stay the reference's own PyTorch
+composition (stock PyTorch-ROCm modules; out of the engine's scope). Two
+reference behaviours are reproduced on purpose, because checkpoints and
+downstream numbers depend on them:
   * the HOG gathers rows of ``x.contiguous().view(B*N, -1)`` with LOCAL ids
     (no per-cloud offset), i.e. a (B,3,N) buffer reinterpreted as rows of 3
     and only the first cloud's rows addressed;
-  * device placement follows ``LOCAL_RANK`` / ``use_cpu`` as the reference
-    does (model_partseg.py:42-47, 66-73).
+  * the histogram's device follows ``use_cpu`` / ``LOCAL_RANK`` as the
+    reference's does (model_partseg.py:66-73); the work runs on x's device.
 """
 import os
 
-import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
+from dgx.hog import hog_1x1
 from models.dgcnn import DGCNN, knn
 from models.layers import PositionEmbedding
-
-_DEG = 180 / np.pi
-_BIN_WIDTH = 20.0
-_N_BINS = 9
-
-
-def _svd_device(use_cpu):
-    # model_partseg.py:42-47: LOCAL_RANK wins over use_cpu for the SVD outputs
-    if "LOCAL_RANK" in os.environ:
-        return torch.device("cuda", int(os.environ["LOCAL_RANK"]))
-    return torch.device("cpu") if use_cpu else torch.device("cuda")
 
 
 def _hist_device(use_cpu):
@@ -50,41 +39,12 @@ def _hist_device(use_cpu):
     return torch.device("cuda")
 
 
-def _rows(t, flat, shape):
-    """Row gather with LOCAL ids over the (B*N, -1) view (reference semantics)."""
-    return t.reshape(shape[0] * shape[1], -1)[flat, :].view(*shape)
-
-
 def compute_hog_1x1(x, k, use_cpu=False):
     """(B,3,N) -> (B,N,18) per-point 9-bin x 2-angle histogram of the dominant
-    direction of each point's k-neighbourhood (reference model_partseg.py:15-92)."""
-    B, N = x.size(0), x.size(2)
-    flat = knn(x, k).view(-1)                                       # engine kNN, :26
-    nbrs = _rows(x.contiguous(), flat, (B, N, k, 3))                # :28-30
-    centred = nbrs - nbrs.mean(dim=2, keepdim=True)                 # :32-33
-    _, sv, vh = np.linalg.svd(centred.detach().cpu().numpy(), full_matrices=False)  # :36-37
-    dev = _svd_device(use_cpu)
-    axis = torch.from_numpy(vh).to(dev)[:, :, 0]                    # first right-singular vector
-    mag = torch.from_numpy(np.sqrt(sv)).to(dev)[:, :, 0].unsqueeze(-1)
-
-    g = _rows(axis, flat, (B, N, k, 3))
-    m = _rows(mag, flat, (B, N, k, 1))
-    zenith = torch.acos(g[:, :, :, 2]).unsqueeze(-1) * _DEG
-    azimuth = torch.atan(g[:, :, :, 1] / g[:, :, :, 0]).unsqueeze(-1) * _DEG
-    cells = torch.cat((zenith.int(), azimuth.int(), m), dim=-1)     # (zenith, azimuth, magnitude)
-    cells[cells < 0] += 180                                         # unsigned orientation
-
-    hist = torch.zeros((B, N, _N_BINS, 2), device=_hist_device(use_cpu))
-    angles, weight = cells[:, :, :, :2], cells[:, :, :, 2].unsqueeze(-1)
-    bins = torch.floor(angles / _BIN_WIDTH - 0.5) % _N_BINS
-    # linear interpolation between the two nearest bin centres (:77-84)
-    upper = weight * ((_BIN_WIDTH * ((bins + 1) % _N_BINS + 0.5) - angles) % 180) / _BIN_WIDTH
-    lower = weight * ((angles - _BIN_WIDTH * (bins + 0.5)) % 180) / _BIN_WIDTH
-    for c in range(_N_BINS):
-        hit = bins == c
-        hist[:, :, c] += (upper * hit).sum(dim=2)
-        hist[:, :, (c + 1) % _N_BINS] += (lower * hit).sum(dim=2)
-    return F.normalize(hist, p=2.0, dim=2).view(B, N, -1)
+    direction of each point's k-neighbourhood (reference model_partseg.py:15-92).
+    Engine kNN (:26), then one device call for :28-92."""
+    hist = hog_1x1(x, knn(x, k))
+    return hist.to(_hist_device(use_cpu))
 
 
 def _conv_bn_lrelu(c_in, c_out, inplace=True):

@@ -320,6 +320,18 @@ int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const fl
                              const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
                              const float* c1, float* dPQ, void* stream);
 
+/* ---- f1: compute_hog_1x1 on the device, replaces models/model_partseg.py:26-92
+ * after the kNN call (the D2H copy, np.linalg.svd on B*N k x 3 matrices, the H2D
+ * copy and the histogram votes). x: contiguous (B, 3, N) fp32; idx: (B, N, k)
+ * int64 LOCAL ids (the engine kNN's output, as knn() returns it). Reproduces the
+ * reference's local-id gather: neighbourhoods are rows of the
+ * (B*N, 3) view of x, so only cloud 0's N SVDs are used; axis (N x 4 fp32
+ * scratch) receives (v0 v1 v2 sqrt(sigma0)) of the dominant right singular
+ * vector (LAPACK dgesdd's sign, csrc/svd3.h); out: (B, N, 18) = (B, N, 9 bins,
+ * 2 angles) L2-normalised histograms. 5 <= k <= 64 (DGX_EUNSUPPORTED else). */
+int dgx_hog_1x1_f32(const float* x, const int64_t* idx, int B, int N, int k, float* axis, float* out,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,8 @@ Contents
   * ``graph_feature`` — numpy restatement of ``models/dgcnn.py:15-44``.
   * ``reference.py`` — torch-CPU restatement of the float path (EdgeConv blocks,
     DGCNN, PositionEmbedding) used for 1e-3 parity and as the CPU baseline.
+  * ``hog.hog_1x1`` — torch/numpy-CPU restatement of compute_hog_1x1 after its
+    kNN call (models/model_partseg.py:28-92).
 
 Pinned by ``tests/golden/`` fixtures that ``tests/golden/make_goldens.py``
 produced by running the reference itself in the build container.
