@@ -41,19 +41,5 @@ __device__ __forceinline__ bool dgx_xcd_slice_map(int block, int B, int parts, i
     return true;
 }
 
-// LeakyReLU and the packed (dz, slot) word shared by the EdgeConv (edgeconv.hip)
-// and edge-MLP (edgemlp.hip) backward kernels.
+// LeakyReLU shared by the EdgeConv (edgeconv.hip) and edge-MLP (edgemlp.hip) kernels.
 __device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.f ? v : v * slope; }
-
-// dz with the selected k-slot packed into the 6 low mantissa bits (k <= 64):
-// one 4-byte word per (point, channel) in the backward's LDS image. The value
-// is ROUNDED to the remaining 17 mantissa bits (+32 on the magnitude bits, the
-// carry propagates correctly into the exponent): truncation would bias every
-// dz toward zero and the bias accumulates linearly through the BN backward's
-// cancelling sums (sum over the batch of the gradient is ~0), which showed as
-// 1e-3..1e-2 gradient error at N*k = 81920; rounding keeps it unbiased.
-__device__ __forceinline__ float pack_dz(float dz, int slot) {
-    return __uint_as_float(((__float_as_uint(dz) + 32u) & ~63u) | (unsigned)slot);
-}
-__device__ __forceinline__ float unpack_dz(float p) { return __uint_as_float(__float_as_uint(p) & ~63u); }
-__device__ __forceinline__ int unpack_slot(float p) { return (int)(__float_as_uint(p) & 63u); }

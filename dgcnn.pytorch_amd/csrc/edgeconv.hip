@@ -35,8 +35,6 @@ constexpr int EC_THREADS = 512;
 constexpr int EC_LDS_BYTES = 64 * 1024;   // operand slices per workgroup (2 workgroups per CU)
 constexpr int GF_IPT = 8;                    // idx ints per thread per pass
 constexpr int GF_ICAP = GF_IPT * EC_THREADS;
-constexpr int GB_EPT = 6;                    // CSR edges per thread per pass (LDS total <= 80 KB)
-constexpr int GB_ECAP = GB_EPT * EC_THREADS;  // edges staged per pass (else read from HBM)
 
 // V consecutive floats from LDS in one ds_read (b32 / b64 / b128).
 template <int V>
@@ -133,32 +131,42 @@ struct SliceSplit {
 // grid (B * nparts, ceil(Co / CS)); partial-stat row = blockIdx.x.
 // Stage rows [0,N) x columns [col0, col0+CS) of a row-major matrix (row stride
 // ld floats) into LDS [N][CS]; 16-byte loads when the slice is 16-byte aligned.
+// With `dir` each column is multiplied by the sign of dir[col] (+-1, exact),
+// so the forward gather's per-channel max-or-min becomes a plain max.
 template <int CS, int THREADS>
 __device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float* __restrict__ src, int64_t ld,
-                                            int N, int col0, int ncols, bool vec4) {
+                                            int N, int col0, int ncols, bool vec4,
+                                            const float* __restrict__ dir = nullptr) {
     const int t = threadIdx.x;
+    auto sgn = [&](int c) { return (dir && col0 + c < ncols && dir[col0 + c] < 0.f) ? -1.f : 1.f; };
+    constexpr int Q = CS >= 4 ? CS / 4 : 1;
+    static_assert(THREADS % Q == 0, "a thread stages one column group");
     if (CS % 4 == 0 && vec4 && col0 + CS <= ncols) {
-        constexpr int Q = CS / 4;
+        const int qt = t % Q;  // this thread's column group, the same on every trip
+        const float4 sg = make_float4(sgn(4 * qt), sgn(4 * qt + 1), sgn(4 * qt + 2), sgn(4 * qt + 3));
         const int total = N * Q;
         int e = t;
         for (; e + 3 * THREADS < total; e += 4 * THREADS) {  // 4 independent 16-byte loads in flight
             float4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int ee = e + u * THREADS, n = ee / Q, q = ee - n * Q;
-                v[u] = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * q);
+                const int ee = e + u * THREADS, n = ee / Q;
+                v[u] = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * qt);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) reinterpret_cast<float4*>(dst)[e + u * THREADS] = v[u];
+            for (int u = 0; u < 4; ++u)
+                reinterpret_cast<float4*>(dst)[e + u * THREADS] =
+                    make_float4(v[u].x * sg.x, v[u].y * sg.y, v[u].z * sg.z, v[u].w * sg.w);
         }
         for (; e < total; e += THREADS) {
-            const int n = e / Q, q = e - n * Q;
-            reinterpret_cast<float4*>(dst)[e] = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * q);
+            const int n = e / Q;
+            const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * qt);
+            reinterpret_cast<float4*>(dst)[e] = make_float4(v.x * sg.x, v.y * sg.y, v.z * sg.z, v.w * sg.w);
         }
     } else {
         for (int e = t; e < N * CS; e += THREADS) {
             const int n = e / CS, c = e - n * CS;
-            dst[e] = (col0 + c < ncols) ? src[(int64_t)n * ld + col0 + c] : 0.f;
+            dst[e] = (col0 + c < ncols) ? src[(int64_t)n * ld + col0 + c] * sgn(c) : 0.f;
         }
     }
 }
@@ -179,7 +187,9 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     const int64_t base = (int64_t)b * N;
     const int per = (N + nparts - 1) / nparts;
     const int n_beg = part * per, n_end = min(N, n_beg + per);
-    stage_slice<CS, EC_THREADS>(lds, PQ + base * ldpq, ldpq, N, o0, Co, (ldpq % 4) == 0 && (o0 % 4) == 0);
+    // P slice with each channel's sign of the BN scale folded in: max over k of
+    // dir*P is max_k P (dir = +1) or -min_k P (dir = -1), one compare per value
+    stage_slice<CS, EC_THREADS>(lds, PQ + base * ldpq, ldpq, N, o0, Co, (ldpq % 4) == 0 && (o0 % 4) == 0, sel_sign);
 
     // Pass = PP consecutive points; their idx rows (PP*k ints, contiguous in
     // HBM) are staged in LDS, the next pass's rows prefetched into registers
@@ -208,12 +218,13 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
 
     const int tp = t % TPP, pl = t / TPP;
     const int c0 = tp * V;          // first channel of this thread within the slice
-    float sgn[V], shv[V];
+    float sgn[V], dir[V], shv[V];  // sel value (scale in EVAL), its sign +-1, shift
     bool okc[V];
 #pragma unroll
     for (int u = 0; u < V; ++u) {
         okc[u] = o0 + c0 + u < Co;
         sgn[u] = okc[u] ? sel_sign[o0 + c0 + u] : 1.f;
+        dir[u] = sgn[u] < 0.f ? -1.f : 1.f;
         shv[u] = (EVAL && okc[u]) ? shift[o0 + c0 + u] : 0.f;
     }
     // whole-vector HBM accesses when all V channels exist and rows stay aligned
@@ -242,17 +253,18 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
             int barg[V];
 #pragma unroll
             for (int u = 0; u < V; ++u) {
-                best[u] = sgn[u] < 0.f ? INFINITY : -INFINITY;
+                best[u] = -INFINITY;
                 s[u] = 0.f;
                 s2[u] = 0.f;
                 barg[u] = 0;
             }
+            // values are dir*P: strict '>' keeps the first extremal slot
             auto take = [&](int j, int kk) {
                 float v[V];
                 lds_vec<V>(lds + j * CS + c0, v);
 #pragma unroll
                 for (int u = 0; u < V; ++u) {
-                    const bool better = sgn[u] < 0.f ? v[u] < best[u] : v[u] > best[u];
+                    const bool better = v[u] > best[u];
                     best[u] = better ? v[u] : best[u];
                     barg[u] = better ? kk : barg[u];
                     s[u] += v[u];
@@ -272,6 +284,8 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
 #pragma unroll
             for (int u = 0; u < V; ++u) {
                 const float q = qv[u];
+                best[u] *= dir[u];  // back to P: the selected P_j (exact sign flips)
+                s[u] *= dir[u];
                 yv[u] = best[u] + q;
                 if (EVAL) {
                     yv[u] = lrelu(fmaf(sgn[u], yv[u], shv[u]), slope);
@@ -421,13 +435,13 @@ __global__ void bn_lrelu_apply4_kernel(const float* __restrict__ ysel, int M, in
 }
 
 // ------------------------------------------------------------ backward -----
-// dz at the selected edge (packed with its slot) and per-row-block partial
-// (sum dz, sum dz*yhat). grid (nrows, ceil(Co/64)).
+// dz = dL/dz at the selected edge (z = BN(y)), fp32, and per-row-block
+// partials (sum dz, sum dz*yhat). grid (nrows, ceil(Co/64)).
 __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
-    const float* __restrict__ dY, int lddy, const float* __restrict__ ysel, const uint8_t* __restrict__ arg,
-    int M, int Co, const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ mean, const float* __restrict__ invstd, float slope, float* __restrict__ dzp,
-    float* __restrict__ partials, int rows_per_blk) {
+    const float* __restrict__ dY, int lddy, const float* __restrict__ ysel, int M, int Co,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float slope, float* __restrict__ dz, float* __restrict__ partials,
+    int rows_per_blk) {
     __shared__ float red[2][4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int o = blockIdx.y * 64 + lane;
@@ -441,13 +455,11 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
         constexpr int DZ_U = 4;
         for (int r0 = wave; r0 < rows_per_blk; r0 += 4 * DZ_U) {
             float yv[DZ_U], gv[DZ_U];
-            int av[DZ_U];
 #pragma unroll
             for (int u = 0; u < DZ_U; ++u) {
                 const int64_t i = min(i0 + r0 + 4 * u, (int64_t)M - 1);
                 yv[u] = ysel[i * Co + o];
                 gv[u] = dY[i * lddy + o];
-                av[u] = arg[i * Co + o];
             }
 #pragma unroll
             for (int u = 0; u < DZ_U; ++u) {
@@ -455,7 +467,7 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
                 if (r0 + 4 * u >= rows_per_blk || i >= M) break;
                 const float z = fmaf(a, yv[u], sh);
                 const float d = gv[u] * (z > 0.f ? 1.f : slope);
-                dzp[i * Co + o] = pack_dz(d, av[u]);
+                dz[i * Co + o] = d;
                 acc1 += d;
                 acc2 = fmaf(d, (yv[u] - mu) * is, acc2);
             }
@@ -640,181 +652,58 @@ __global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(const int32_t
     }
 }
 
-// dPQ for every point: grid (B * nparts, ceil(Co / CS)). The cloud's Q slice
-// and packed dz|slot slice live in LDS; each (point, channel) thread walks
-// the point's in-edges.
-template <int CS, bool OUT16>
-__global__ __launch_bounds__(EC_THREADS) void edge_bwd_lds_kernel(
-    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
-    const float* __restrict__ dzp, const float* __restrict__ sumP, int B, int N, int k, int Co, int nparts,
-    const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
-    void* __restrict__ dPQv) {
-    // dPQ fp32, or bf16 when it only feeds the bf16 GEMMs (dX, dW)
-    float* __restrict__ dPQ = static_cast<float*>(dPQv);
-    __bf16* __restrict__ dPQh = static_cast<__bf16*>(dPQv);
-    constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V, PP = SliceSplit<CS>::PP_MAX;
-    extern __shared__ float lds[];  // [N][CS] Q slice | [N][CS] packed dz | edges [GB_ECAP] | rowptr [PP+1]
-    float* qs = lds;
-    float* ds = lds + N * CS;
-    int* ebuf = reinterpret_cast<int*>(ds + N * CS);
-    int* rps = ebuf + GB_ECAP;
-    int b, part, slice;
-    if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
-    const int o0 = slice * CS;
-    const int t = threadIdx.x;
-    const int64_t base = (int64_t)b * N;
-    const int per = (N + nparts - 1) / nparts;
-    const int n_beg = part * per, n_end = min(N, n_beg + per);
-    const int npass = n_end > n_beg ? (n_end - n_beg + PP - 1) / PP : 0;
+// dPQ for every point: grid (B * nparts, ceil(Co / CS)), CS <= 8 channels per
+// slice, one point per thread with all CS channels, so the per-edge work
+// (edge-id decode, LDS addresses) is shared by CS channels. LDS holds the
+// cloud's Q slice and dz slice (fp32, exact) and the selected slots (u8, the
+// forward's arg) — 9 bytes per (point, channel) — plus the block's points in
+// descending in-degree order: the in-degree of feature-space kNN graphs is
+// skewed (hubs), and a wave's trip count is its largest in-degree, so waves
+// take points of similar degree. Every point still sums its in-edges in its
+// CSR (ascending edge id) order: results do not depend on the schedule.
+//   dP_j = a * sum_{in-edges (i,s) of j, s = slot_i} dz_i
+//          + deg_j c0 + c1 (deg_j P_j + sum_in Q_i)
+//   dQ_i = a dz_i + k c0 + c1 (k Q_i + sum_k P_j)
+constexpr int BW_EB = 16;         // in-edge ids loaded per batch
+constexpr int BW_BUCKETS = 64;    // degree buckets of the in-block order
+constexpr int BW_LDS_BYTES = 72 * 1024;  // Q | dz | slot slices (two workgroups per CU)
 
-    // The pass's in-edge lists (a contiguous CSR range) and row pointers are
-    // staged in LDS; the next pass's are prefetched into registers while the
-    // current pass computes. A pass with more than GB_ECAP in-edges (hubs)
-    // reads its lists from HBM instead.
-    int pe[GB_EPT], prp = 0, pre_lo = 0, pre_hi = 0;
-    auto load_pass = [&](int p) {
-        const int n0 = n_beg + p * PP, n1 = min(n_end, n0 + PP);
-        pre_lo = rowptr[base + n0];
-        pre_hi = rowptr[base + n1];
-        if (t <= PP) prp = rowptr[base + min(n0 + t, n1)];
-#pragma unroll
-        for (int u = 0; u < GB_EPT; ++u) {
-            const int e = pre_lo + t + u * EC_THREADS;
-            pe[u] = e < pre_hi ? edges[e] : 0;
-        }
-    };
-    auto store_pass = [&]() {
-#pragma unroll
-        for (int u = 0; u < GB_EPT; ++u) ebuf[t + u * EC_THREADS] = pe[u];
-        if (t <= PP) rps[t] = prp;
-    };
-
-    if (npass > 0) load_pass(0);
-    stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
-    stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
-    if (npass > 0) store_pass();
-    __syncthreads();
-    const int tp = t % TPP, pl = t / TPP;
-    const int cc = tp * V;
-    float a[V], k0[V], k1[V];
-    bool okc[V];
-#pragma unroll
-    for (int u = 0; u < V; ++u) {
-        const int o = o0 + cc + u;
-        okc[u] = o < Co;
-        a[u] = okc[u] ? scale[o] : 0.f;
-        k0[u] = okc[u] ? c0[o] : 0.f;
-        k1[u] = okc[u] ? c1[o] : 0.f;
-    }
-    const bool vec = okc[V - 1] && (Co % 4) == 0 && (ldpq % 4) == 0;
-    const float kf = (float)k;
-    const int32_t ibase = (int32_t)base;
-    for (int p = 0; p < npass; ++p) {
-        const int lo = pre_lo, hi = pre_hi;
-        if (p + 1 < npass) load_pass(p + 1);
-        const int n = n_beg + p * PP + pl;
-        if (okc[0] && n < n_end) {
-            const int64_t j = base + n;
-            const int32_t beg = rps[pl] - lo, end = rps[pl + 1] - lo;
-            const int* __restrict__ el = (hi - lo <= GB_ECAP) ? ebuf : edges + lo;
-            float pjv[V], spv[V];  // HBM reads issued before the edge loop hides their latency
-            if (vec) {
-                gld_vec<V>(PQ + j * ldpq + o0 + cc, pjv);
-                gld_vec<V>(sumP + j * Co + o0 + cc, spv);
-            } else {
-#pragma unroll
-                for (int u = 0; u < V; ++u) {
-                    pjv[u] = okc[u] ? PQ[j * ldpq + o0 + cc + u] : 0.f;
-                    spv[u] = okc[u] ? sumP[j * Co + o0 + cc + u] : 0.f;
-                }
-            }
-            float sq[V], sd[V];
-#pragma unroll
-            for (int u = 0; u < V; ++u) { sq[u] = 0.f; sd[u] = 0.f; }
-            auto edge = [&](int32_t e) {
-                const int il = (e >> 6) - ibase, slot = e & 63;
-                float q[V], d[V];
-                lds_vec<V>(qs + il * CS + cc, q);
-                lds_vec<V>(ds + il * CS + cc, d);
-#pragma unroll
-                for (int u = 0; u < V; ++u) {
-                    sq[u] += q[u];
-                    sd[u] += unpack_slot(d[u]) == slot ? unpack_dz(d[u]) : 0.f;
-                }
-            };
-            int32_t u0 = beg;
-            for (; u0 + 8 <= end; u0 += 8) {
-                int32_t e[8];
-#pragma unroll
-                for (int w = 0; w < 8; ++w) e[w] = el[u0 + w];
-#pragma unroll
-                for (int w = 0; w < 8; ++w) edge(e[w]);
-            }
-            for (; u0 + 4 <= end; u0 += 4) {
-                const int32_t e0 = el[u0], e1 = el[u0 + 1], e2 = el[u0 + 2], e3 = el[u0 + 3];
-                edge(e0);
-                edge(e1);
-                edge(e2);
-                edge(e3);
-            }
-            for (; u0 < end; ++u0) edge(el[u0]);
-            const float deg = (float)(end - beg);
-            float qn[V], dn[V];
-            lds_vec<V>(qs + n * CS + cc, qn);
-            lds_vec<V>(ds + n * CS + cc, dn);
-            float dp[V], dq[V];
-#pragma unroll
-            for (int u = 0; u < V; ++u) {
-                dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
-                dq[u] = fmaf(a[u], unpack_dz(dn[u]), fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
-            }
-            if (OUT16 && vec) {
-                gst_bf16<V>(dPQh + j * 2 * Co + o0 + cc, dp);
-                gst_bf16<V>(dPQh + j * 2 * Co + Co + o0 + cc, dq);
-            } else if (OUT16) {
-#pragma unroll
-                for (int u = 0; u < V; ++u) {
-                    if (!okc[u]) continue;
-                    dPQh[j * 2 * Co + o0 + cc + u] = (__bf16)dp[u];
-                    dPQh[j * 2 * Co + Co + o0 + cc + u] = (__bf16)dq[u];
-                }
-            } else if (vec) {
-                gst_vec<V>(dPQ + j * 2 * Co + o0 + cc, dp);
-                gst_vec<V>(dPQ + j * 2 * Co + Co + o0 + cc, dq);
-            } else {
-#pragma unroll
-                for (int u = 0; u < V; ++u) {
-                    if (!okc[u]) continue;
-                    dPQ[j * 2 * Co + o0 + cc + u] = dp[u];
-                    dPQ[j * 2 * Co + Co + o0 + cc + u] = dq[u];
-                }
-            }
-        }
-        __syncthreads();
-        if (p + 1 < npass) {
-            store_pass();
-            __syncthreads();
-        }
+template <int CS>
+__device__ __forceinline__ void lds_slots(const uint8_t* __restrict__ p, uint32_t (&w)[(CS + 3) / 4]) {
+    if constexpr (CS == 16) {
+        const uint4 t = *reinterpret_cast<const uint4*>(p);
+        w[0] = t.x;
+        w[1] = t.y;
+        w[2] = t.z;
+        w[3] = t.w;
+    } else if constexpr (CS == 8) {
+        const uint2 t = *reinterpret_cast<const uint2*>(p);
+        w[0] = t.x;
+        w[1] = t.y;
+    } else if constexpr (CS == 4) {
+        w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (CS == 2) {
+        w[0] = *reinterpret_cast<const uint16_t*>(p);
+    } else {
+        w[0] = p[0];
     }
 }
 
-// Wide form of the dP/dQ scatter (the slice holds CS <= 8 channels): one
-// point per thread, all CS channels of the slice per thread, so the per-edge
-// work (edge-id decode, addresses, 16-B LDS reads of Q_i and dz_i) is shared
-// by CS channels. In-edge lists and row pointers are read from HBM/L2 directly
-// (contiguous per point, consecutive points -> consecutive ranges).
-constexpr int BW_EB = 16;  // in-edge ids loaded per batch (edge_bwd_wide_kernel)
 template <int CS, bool OUT16>
-__global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
+__global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
-    const float* __restrict__ dzp, const float* __restrict__ sumP, int B, int N, int k, int Co, int nparts,
-    const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
-    void* __restrict__ dPQv) {
+    const float* __restrict__ dz, const uint8_t* __restrict__ arg, const float* __restrict__ sumP, int B, int N,
+    int k, int Co, int nparts, const float* __restrict__ scale, const float* __restrict__ c0,
+    const float* __restrict__ c1, void* __restrict__ dPQv) {
+    static_assert(CS == 1 || CS == 2 || CS == 4 || CS == 8 || CS == 16, "slice width");
+    constexpr int SW = (CS + 3) / 4;  // slot words per row
     float* __restrict__ dPQ = static_cast<float*>(dPQv);
     __bf16* __restrict__ dPQh = static_cast<__bf16*>(dPQv);
-    extern __shared__ float lds[];  // [N][CS] Q slice | [N][CS] packed dz slice
+    extern __shared__ float lds[];  // [N][CS] Q | [N][CS] dz | [N][CS] u8 slot | order u16 [per] | buckets
     float* qs = lds;
     float* ds = lds + N * CS;
+    uint8_t* ss = reinterpret_cast<uint8_t*>(ds + N * CS);
+    uint16_t* order = reinterpret_cast<uint16_t*>(ss + ((N * CS + 15) & ~15));
     int b, part, slice;
     if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
     const int o0 = slice * CS;
@@ -822,8 +711,62 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
     const int64_t base = (int64_t)b * N;
     const int per = (N + nparts - 1) / nparts;
     const int n_beg = part * per, n_end = min(N, n_beg + per);
+    const int np = max(0, n_end - n_beg);
+    int* bucket = reinterpret_cast<int*>(order + ((per + 7) & ~7));
+    const bool full = o0 + CS <= Co;
+    if (t < BW_BUCKETS) bucket[t] = 0;
     stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
-    stage_slice<CS, EC_THREADS>(ds, dzp + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+    stage_slice<CS, EC_THREADS>(ds, dz + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+    const uint8_t* __restrict__ ab = arg + base * Co + o0;
+    if (full && (Co % CS) == 0) {
+        for (int n = t; n < N; n += EC_THREADS) {
+            uint32_t w[SW];
+            if constexpr (CS == 16) {
+                *reinterpret_cast<uint4*>(ss + n * CS) = *reinterpret_cast<const uint4*>(ab + (int64_t)n * Co);
+            } else if constexpr (CS == 8) {
+                const uint2 v = *reinterpret_cast<const uint2*>(ab + (int64_t)n * Co);
+                w[0] = v.x;
+                w[1] = v.y;
+                *reinterpret_cast<uint2*>(ss + n * CS) = make_uint2(w[0], w[1]);
+            } else if constexpr (CS == 4) {
+                *reinterpret_cast<uint32_t*>(ss + n * CS) = *reinterpret_cast<const uint32_t*>(ab + (int64_t)n * Co);
+            } else if constexpr (CS == 2) {
+                *reinterpret_cast<uint16_t*>(ss + n * CS) = *reinterpret_cast<const uint16_t*>(ab + (int64_t)n * Co);
+            } else {
+                ss[n] = ab[(int64_t)n * Co];
+            }
+            (void)w;
+        }
+    } else {
+        for (int e = t; e < N * CS; e += EC_THREADS) {
+            const int n = e / CS, c = e - n * CS;
+            ss[e] = o0 + c < Co ? ab[(int64_t)n * Co + c] : (uint8_t)255;
+        }
+    }
+    __syncthreads();  // buckets zeroed
+    // in-block order: counting sort of the block's points by in-degree, descending
+    for (int r = t; r < np; r += EC_THREADS) {
+        const int64_t j = base + n_beg + r;
+        const int deg = rowptr[j + 1] - rowptr[j];
+        atomicAdd(&bucket[BW_BUCKETS - 1 - min(deg, BW_BUCKETS - 1)], 1);
+    }
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the 64 bucket counts (one wave)
+        const int c = bucket[t];
+        int inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o);
+            if (t >= o) inc += v;
+        }
+        bucket[t] = inc - c;
+    }
+    __syncthreads();
+    for (int r = t; r < np; r += EC_THREADS) {
+        const int64_t j = base + n_beg + r;
+        const int deg = rowptr[j + 1] - rowptr[j];
+        order[atomicAdd(&bucket[BW_BUCKETS - 1 - min(deg, BW_BUCKETS - 1)], 1)] = (uint16_t)r;
+    }
     float a[CS], k0[CS], k1[CS];
 #pragma unroll
     for (int u = 0; u < CS; ++u) {
@@ -832,12 +775,12 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
         k0[u] = c0[o];
         k1[u] = c1[o];
     }
-    const bool full = o0 + CS <= Co;
     const bool vec = full && (CS % 4) == 0 && (Co % 4) == 0 && (ldpq % 4) == 0;
     const float kf = (float)k;
     const int32_t ibase = (int32_t)base;
     __syncthreads();
-    for (int n = n_beg + t; n < n_end; n += EC_THREADS) {
+    for (int r = t; r < np; r += EC_THREADS) {
+        const int n = n_beg + order[r];
         const int64_t j = base + n;
         const int32_t beg = rowptr[j], end = rowptr[j + 1];
         float pjv[CS], spv[CS];  // HBM reads issued before the edge loop hides their latency
@@ -857,17 +800,19 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
         auto edge = [&](int32_t e) {
             const int il = (e >> 6) - ibase;
             const uint32_t slot = (uint32_t)(e & 63);
-            float q[CS], d[CS];
+            float q[CS];
+            uint32_t w[SW];
             lds_vec<CS>(qs + il * CS, q);
+            lds_slots<CS>(ss + il * CS, w);
+#pragma unroll
+            for (int u = 0; u < CS; ++u) sq[u] += q[u];
+            float d[CS];
             lds_vec<CS>(ds + il * CS, d);
 #pragma unroll
-            for (int u = 0; u < CS; ++u) {
-                sq[u] += q[u];
-                sd[u] += (__float_as_uint(d[u]) & 63u) == slot ? unpack_dz(d[u]) : 0.f;
-            }
+            for (int u = 0; u < CS; ++u) sd[u] += ((w[u >> 2] >> (8 * (u & 3))) & 0xffu) == slot ? d[u] : 0.f;
         };
-        // in-edge ids EB at a time, all loads issued before the first is used:
-        // one memory latency per EB edges instead of one per 4
+        // in-edge ids EB at a time, all loads issued before the first is used
+        // (prefetching the next batch as well measured slower)
         for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
             int32_t ids[BW_EB];
 #pragma unroll
@@ -884,7 +829,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
 #pragma unroll
         for (int u = 0; u < CS; ++u) {
             dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
-            dq[u] = fmaf(a[u], unpack_dz(dn[u]), fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
+            dq[u] = fmaf(a[u], dn[u], fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
         }
         if (OUT16 && vec) {
             gst_bf16<CS>(dPQh + j * 2 * Co + o0, dp);
@@ -906,6 +851,13 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_wide_kernel(
             }
         }
     }
+}
+
+// scatter LDS bytes for N points at CS channels (Q | dz | slot | order | buckets)
+inline size_t scatter_lds_bytes(int N, int cs, int parts) {
+    const int per = (N + parts - 1) / parts;
+    return (size_t)2 * N * cs * sizeof(float) + (((size_t)N * cs + 15) & ~(size_t)15) +
+           (size_t)((per + 7) & ~7) * sizeof(uint16_t) + BW_BUCKETS * sizeof(int);
 }
 
 inline int grid_for(int64_t total, int block) {
@@ -1048,14 +1000,14 @@ int dgx_bn_lrelu_apply_f32(const float* ysel, int M, int Co, const float* scale,
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, const uint8_t* arg, int M, int Co,
-                        const float* scale, const float* shift, const float* mean, const float* invstd, float slope,
-                        float* dzp, float* partials, int nrows, void* stream) {
-    if (!dY || !ysel || !arg || !scale || !shift || !mean || !invstd || !dzp || !partials) return DGX_EINVAL;
+int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, int M, int Co, const float* scale,
+                        const float* shift, const float* mean, const float* invstd, float slope, float* dz,
+                        float* partials, int nrows, void* stream) {
+    if (!dY || !ysel || !scale || !shift || !mean || !invstd || !dz || !partials) return DGX_EINVAL;
     if (M < 1 || Co < 1 || lddy < Co || nrows < 1) return DGX_EINVAL;
     const int rows = (M + nrows - 1) / nrows;
     hipLaunchKernelGGL(edge_bwd_dz_kernel, dim3(nrows, (Co + 63) / 64), dim3(256), 0, dgx_stream(stream), dY, lddy,
-                       ysel, arg, M, Co, scale, shift, mean, invstd, slope, dzp, partials, rows);
+                       ysel, M, Co, scale, shift, mean, invstd, slope, dz, partials, rows);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -1096,57 +1048,39 @@ int dgx_graph_reverse(const int32_t* idx, int B, int N, int k, int32_t* rowptr, 
 }
 
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
-                             const float* dzp, const float* sumP, int B, int N, int k, int Co, const float* scale,
-                             const float* c0, const float* c1, void* dPQ, int out_bf16, void* stream) {
-    if (!PQ || !rowptr || !edges || !dzp || !sumP || !scale || !c0 || !c1 || !dPQ) return DGX_EINVAL;
+                             const float* dz, const uint8_t* arg, const float* sumP, int B, int N, int k, int Co,
+                             const float* scale, const float* c0, const float* c1, void* dPQ, int out_bf16,
+                             void* stream) {
+    if (!PQ || !rowptr || !edges || !dz || !arg || !sumP || !scale || !c0 || !c1 || !dPQ) return DGX_EINVAL;
     if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
-    const int cs = slice_channels(N, 2);
-    if ((size_t)2 * N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
+    if (N > 65535) return DGX_EUNSUPPORTED;
+    int cs = 8;  // slice channels: 9 bytes per (point, channel) within BW_LDS_BYTES
+    // (16 measured slower: one workgroup per CU; 4 slower: per-edge work over fewer channels)
+    while (cs > 1 && (size_t)9 * N * cs > (size_t)BW_LDS_BYTES) cs >>= 1;
+    if ((size_t)9 * N * cs > (size_t)BW_LDS_BYTES) return DGX_EUNSUPPORTED;
     const int slices = (Co + cs - 1) / cs;
     const int parts = point_parts(B, slices, N);
     const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
-    const size_t lds = (size_t)2 * N * cs * sizeof(float) + (GB_ECAP + EC_THREADS + 1) * sizeof(int);
+    const size_t lds = scatter_lds_bytes(N, cs, parts);
     hipStream_t st = dgx_stream(stream);
-#define DGX_BWD_CASE(CSV)                                                                                    \
-    case CSV:                                                                                               \
-        if (out_bf16)                                                                                       \
-            hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, true>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                               edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                    \
-        else                                                                                                \
-            hipLaunchKernelGGL((edge_bwd_lds_kernel<CSV, false>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                               edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                    \
+#define DGX_SCATTER_CASE(CSV)                                                                                  \
+    case CSV:                                                                                                 \
+        if (out_bf16)                                                                                         \
+            hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, true>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq,   \
+                               rowptr, edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);          \
+        else                                                                                                  \
+            hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, false>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq,  \
+                               rowptr, edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);          \
         break;
-    if (cs <= 8) {  // wide form: one point per thread, all slice channels
-        const size_t wl = (size_t)2 * N * cs * sizeof(float);
-#define DGX_WIDE_CASE(CSV)                                                                                    \
-    case CSV:                                                                                                \
-        if (out_bf16)                                                                                        \
-            hipLaunchKernelGGL((edge_bwd_wide_kernel<CSV, true>), grid, dim3(EC_THREADS), wl, st, PQ, ldpq, rowptr, \
-                               edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);                     \
-        else                                                                                                 \
-            hipLaunchKernelGGL((edge_bwd_wide_kernel<CSV, false>), grid, dim3(EC_THREADS), wl, st, PQ, ldpq,      \
-                               rowptr, edges, dzp, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);             \
-        break;
-        switch (cs) {
-            DGX_WIDE_CASE(8)
-            DGX_WIDE_CASE(4)
-            DGX_WIDE_CASE(2)
-            DGX_WIDE_CASE(1)
-            default: return DGX_EUNSUPPORTED;
-        }
-#undef DGX_WIDE_CASE
-        return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
-    }
     switch (cs) {
-        DGX_BWD_CASE(32)
-        DGX_BWD_CASE(16)
-        DGX_BWD_CASE(8)
-        DGX_BWD_CASE(4)
-        DGX_BWD_CASE(2)
-        DGX_BWD_CASE(1)
+        DGX_SCATTER_CASE(16)
+        DGX_SCATTER_CASE(8)
+        DGX_SCATTER_CASE(4)
+        DGX_SCATTER_CASE(2)
+        DGX_SCATTER_CASE(1)
         default: return DGX_EUNSUPPORTED;
     }
-#undef DGX_BWD_CASE
+#undef DGX_SCATTER_CASE
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

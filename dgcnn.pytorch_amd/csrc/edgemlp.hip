@@ -155,11 +155,12 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_max_kernel(const void* __restr
 }
 
 // BN2 backward, dense over edges: dZ2[e][c] = a_c dz_i[c] [s == slot_i[c]] + c0_c + c1_c z2[e][c].
-// A thread owns 8 channels of one point: the point's packed dz and the
-// per-channel constants are loaded once, then its k edge rows stream through
+// A thread owns 8 channels of one point: the point's dz, selected slots and
+// the per-channel constants are loaded once, then its k edge rows stream through
 // (16-byte bf16 rows, or two float4).
 template <bool IO16>
-__global__ __launch_bounds__(EM_THREADS) void mlp_dz2_kernel(const float* __restrict__ dzp, const void* __restrict__ Z,
+__global__ __launch_bounds__(EM_THREADS) void mlp_dz2_kernel(const float* __restrict__ dz,
+                                                             const uint8_t* __restrict__ arg, const void* __restrict__ Z,
                                                              int64_t M, int k, int C2, const float* __restrict__ scale,
                                                              const float* __restrict__ c0,
                                                              const float* __restrict__ c1, void* __restrict__ dZ) {
@@ -170,15 +171,16 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_dz2_kernel(const float* __rest
         const int c = (int)(t % co) * 8;
         const int64_t i = t / co;
         float d[8], a[8], k0[8], k1[8];
-        ld8(dzp + i * C2 + c, d);
+        ld8(dz + i * C2 + c, d);
+        const uint2 sw = *reinterpret_cast<const uint2*>(arg + i * C2 + c);
         ld8(scale + c, a);
         ld8(c0 + c, k0);
         ld8(c1 + c, k1);
         int slot[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            slot[u] = unpack_slot(d[u]);
-            d[u] = a[u] * unpack_dz(d[u]);
+            slot[u] = (int)(((u < 4 ? sw.x : sw.y) >> (8 * (u & 3))) & 0xffu);
+            d[u] = a[u] * d[u];
         }
 #pragma unroll 2
         for (int s = 0; s < k; ++s) {
@@ -365,18 +367,20 @@ int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2,
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-int dgx_edge_mlp_dz_f32(const float* dzp, const void* Z, int bf16, int B, int N, int k, int C2, const float* scale,
-                        const float* c0, const float* c1, void* dZ, void* stream) {
-    if (!dzp || !Z || !scale || !c0 || !c1 || !dZ || B < 1 || N < 1 || k < 1 || k > 64 || C2 < 4) return DGX_EINVAL;
-    if (C2 % 8 || !al16(dzp) || !al16(Z) || !al16(dZ) || !al16(scale) || !al16(c0) || !al16(c1))
+int dgx_edge_mlp_dz_f32(const float* dz, const uint8_t* arg, const void* Z, int bf16, int B, int N, int k, int C2,
+                        const float* scale, const float* c0, const float* c1, void* dZ, void* stream) {
+    if (!dz || !arg || !Z || !scale || !c0 || !c1 || !dZ || B < 1 || N < 1 || k < 1 || k > 255 || C2 < 4)
+        return DGX_EINVAL;
+    if (C2 % 8 || !al16(dz) || !al16(Z) || !al16(dZ) || !al16(scale) || !al16(c0) || !al16(c1) ||
+        reinterpret_cast<uintptr_t>(arg) % 8)
         return DGX_EUNSUPPORTED;
     const int64_t M = (int64_t)B * N;
     const int grid = grid_of(M * (C2 / 8), EM_THREADS);
     if (bf16)
-        hipLaunchKernelGGL(mlp_dz2_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dzp, Z, M, k, C2,
-                           scale, c0, c1, dZ);
+        hipLaunchKernelGGL(mlp_dz2_kernel<true>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dz, arg, Z, M, k,
+                           C2, scale, c0, c1, dZ);
     else
-        hipLaunchKernelGGL(mlp_dz2_kernel<false>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dzp, Z, M, k,
+        hipLaunchKernelGGL(mlp_dz2_kernel<false>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), dz, arg, Z, M, k,
                            C2, scale, c0, c1, dZ);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }

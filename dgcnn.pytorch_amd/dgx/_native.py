@@ -44,11 +44,11 @@ _SIGS = {
     "dgx_bn_bwd_finalize_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
     "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp],
-    "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
+    "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
-    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32,
-                                 _vp],
+    "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
+                                 _i32, _vp],
     "dgx_colstats_rows": [_i64],
     "dgx_colstats_f32": [_vp, _i32, _i64, _i32, _vp, _i32, _vp],
     "dgx_pointconv_apply_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],
@@ -71,7 +71,7 @@ _SIGS = {
     "dgx_pointconv_bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_edge_mlp_h1_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_edge_mlp_max_f32": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
-    "dgx_edge_mlp_dz_f32": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "dgx_edge_mlp_dz_f32": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
     "dgx_edge_mlp_h1_bwd_rows": [_i32, _i32, _i32, _i32],
     "dgx_edge_mlp_h1_bwd_f32": [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i32,
                                 _vp],

@@ -233,18 +233,18 @@ class _EdgeConvStack(torch.autograd.Function):
             else:
                 dY, ldy = dxcat[:, off:off + co], dxcat.stride(0)
             nblk = max(1, min(1024, (M + 63) // 64))
-            dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dz with packed slot
+            dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dL/dz at the selected edge
             partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
             # dPQ only feeds the GEMMs: bf16 (what the GEMM would round it to) in bf16 mode
             dPQ = torch.empty((M, 2 * co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
             with torch.cuda.device(dev):
                 nat.check(L.dgx_edge_bwd_dz_f32(
-                    nat.f32(dY), ldy, nat.f32(ysel), nat.u8(arg), M, co, nat.f32(st.scale), nat.f32(st.shift),
+                    nat.f32(dY), ldy, nat.f32(ysel), M, co, nat.f32(st.scale), nat.f32(st.shift),
                     nat.f32(st.mean), nat.f32(st.invstd), float(ly.slope), nat.f32(dz), nat.f32(partials), nblk,
                     stream), "edge bwd dz")
                 dgamma, dbeta, c0, c1 = bn_.backward_consts(partials, nblk, count, st, stream)
                 nat.check(L.dgx_edge_bwd_scatter_f32(
-                    nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.f32(sumP), B, N, k,
+                    nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.u8(arg), nat.f32(sumP), B, N, k,
                     co, nat.f32(st.scale), nat.f32(c0), nat.f32(c1), nat.ptr(dPQ, nat.F32, nat.BF16), int(bf16),
                     stream), "edge bwd scatter")
             if dbg is not None:

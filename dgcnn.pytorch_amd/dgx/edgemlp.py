@@ -121,12 +121,12 @@ class _EdgeMLP2(torch.autograd.Function):
             nblk = max(1, min(1024, (M + 63) // 64))
             dz = torch.empty((M, C2), dtype=torch.float32, device=dev)
             part = torch.empty((nblk, 2, C2), dtype=torch.float32, device=dev)
-            nat.check(L.dgx_edge_bwd_dz_f32(nat.f32(dY), C2, nat.f32(ysel), nat.u8(arg), M, C2, nat.f32(st2.scale),
+            nat.check(L.dgx_edge_bwd_dz_f32(nat.f32(dY), C2, nat.f32(ysel), M, C2, nat.f32(st2.scale),
                                             nat.f32(st2.shift), nat.f32(st2.mean), nat.f32(st2.invstd), slope2,
                                             nat.f32(dz), nat.f32(part), nblk, stream), "edge bwd dz")
             dg2, db2, c0, c1 = bn_.backward_consts(part, nblk, float(E), st2, stream)
             dZ2 = torch.empty((E, C2), dtype=Z2.dtype, device=dev)
-            nat.check(L.dgx_edge_mlp_dz_f32(nat.f32(dz), nat.ptr(Z2, nat.F32, nat.BF16), int(z16), B, N, k, C2,
+            nat.check(L.dgx_edge_mlp_dz_f32(nat.f32(dz), nat.u8(arg), nat.ptr(Z2, nat.F32, nat.BF16), int(z16), B, N, k, C2,
                                             nat.f32(st2.scale), nat.f32(c0), nat.f32(c1),
                                             nat.ptr(dZ2, nat.F32, nat.BF16), stream), "edge dz2")
             # ---- conv2 GEMMs: dH1 = dZ2 W2, dW2 = dZ2^T H1

@@ -143,9 +143,8 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx,
                           void* stream);
 
 /* Backward of the block (autograd of dgcnn.py:84-98 through BN train mode):
- *   dgx_edge_bwd_dz: dz = dY * LeakyReLU'(z) at the selected edge, stored in
- *     dzp (M x Co) with the selected slot packed into its 6 low mantissa bits
- *     (relative perturbation <= 2^-17), and per-row partials (sum dz,
+ *   dgx_edge_bwd_dz: dz = dY * LeakyReLU'(z) at the selected edge (M x Co
+ *     fp32; the edge is the forward's arg slot), and per-row partials (sum dz,
  *     sum dz*yhat) -> dgx_bn_bwd_finalize: dgamma, dbeta (accumulate != 0
  *     adds to them) and the per-channel affine c0 + c1*y of BN's input grad.
  *   dgx_graph_reverse: reverse kNN graph: rowptr (M+1), edges (M*k), edge id
@@ -154,9 +153,9 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx,
  *     sum_{edges->j}(c0 + c1*y_e),  dQ_i = a*dz_i + k*c0 + c1*sum_k y_ik.
  * The caller's GEMMs then form dX += dPQ [W1;W2] and dW = dPQ^T X. */
 int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel,
-                        const uint8_t* arg, int M, int Co, const float* scale,
+                        int M, int Co, const float* scale,
                         const float* shift, const float* mean,
-                        const float* invstd, float slope, float* dzp,
+                        const float* invstd, float slope, float* dz,
                         float* partials, int nrows, void* stream);
 int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co,
                             double count, const float* scale, const float* mean,
@@ -170,9 +169,9 @@ int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co,
 int dgx_graph_reverse(const int32_t* idx, int B, int N, int k,
                       int32_t* rowptr, int32_t* edges, void* stream);
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
-                             const int32_t* edges, const float* dzp,
-                             const float* sumP, int B, int N, int k, int Co,
-                             const float* scale, const float* c0,
+                             const int32_t* edges, const float* dz,
+                             const uint8_t* arg, const float* sumP, int B, int N,
+                             int k, int Co, const float* scale, const float* c0,
                              const float* c1, void* dPQ, int out_bf16,
                              void* stream);
 
@@ -310,8 +309,8 @@ int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, in
                         const float* scale, const float* shift, float slope, void* H1, int out_bf16, void* stream);
 int dgx_edge_mlp_max_f32(const void* Z, int z_bf16, int B, int N, int k, int C2, const float* scale, float* ysel,
                          uint8_t* arg, void* stream);
-int dgx_edge_mlp_dz_f32(const float* dzp, const void* Z, int bf16, int B, int N, int k, int C2, const float* scale,
-                        const float* c0, const float* c1, void* dZ, void* stream);
+int dgx_edge_mlp_dz_f32(const float* dz, const uint8_t* arg, const void* Z, int bf16, int B, int N, int k, int C2,
+                        const float* scale, const float* c0, const float* c1, void* dZ, void* stream);
 int dgx_edge_mlp_h1_bwd_rows(int B, int N, int k, int C1);
 int dgx_edge_mlp_h1_bwd_f32(float* dH, const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
                             const float* scale, const float* shift, const float* mean, const float* invstd,

@@ -179,18 +179,16 @@ def test_edge_mlp_bf16_kernels_equal_fp32_kernels(cuda):
     assert torch.equal(sel[0], want)
     assert torch.equal(torch.gather(zf, 1, arg[0].long().unsqueeze(1)).squeeze(1), want)
     # dense BN2 backward: bf16 in/out == fp32 in/out rounded
-    dzp = torch.randn(M, C2, generator=g).to(cuda)
-    dzp = (dzp.view(torch.int32) & ~63 | torch.randint(0, k, (M, C2), generator=g).to(cuda).int()).view(torch.float32)
+    dzv = torch.randn(M, C2, generator=g).to(cuda)
+    sarg = torch.randint(0, k, (M, C2), generator=g).to(cuda).to(torch.uint8)
     c0, c1 = torch.randn(C2, generator=g).to(cuda), torch.randn(C2, generator=g).to(cuda)
     d32 = torch.empty(E, C2, device=cuda)
     d16 = torch.empty(E, C2, device=cuda, dtype=torch.bfloat16)
     for zz, out, flag in ((z16.float().contiguous(), d32, 0), (z16, d16, 1)):
-        nat.check(L.dgx_edge_mlp_dz_f32(nat.ptr(dzp), nat.ptr(zz), flag, B, N, k, C2, nat.ptr(sc2), nat.ptr(c0),
-                                        nat.ptr(c1), nat.ptr(out), st), "dz2")
+        nat.check(L.dgx_edge_mlp_dz_f32(nat.ptr(dzv), nat.ptr(sarg), nat.ptr(zz), flag, B, N, k, C2, nat.ptr(sc2),
+                                        nat.ptr(c0), nat.ptr(c1), nat.ptr(out), st), "dz2")
     assert torch.equal(d32.to(torch.bfloat16), d16)
-    slot = (dzp.view(torch.int32) & 63).long()
-    dzv = (dzp.view(torch.int32) & ~63).view(torch.float32)
-    hit = slot.unsqueeze(1) == torch.arange(k, device=cuda).view(1, k, 1)
+    hit = sarg.long().unsqueeze(1) == torch.arange(k, device=cuda).view(1, k, 1)
     ref = torch.addcmul(c0, c1, zf) + torch.where(hit, sc2 * dzv.unsqueeze(1), torch.zeros((), device=cuda))
     assert rel_err(d32.view(M, k, C2).cpu(), ref.cpu()) < 1e-6
 
