@@ -541,17 +541,30 @@ __device__ __forceinline__ int32_t block_sum_rg(int32_t v, int32_t* red) {
     return t;
 }
 
-__global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(const int32_t* __restrict__ idx, int N, int k,
-                                                                   int P, int cap, int32_t* __restrict__ rowptr,
-                                                                   int32_t* __restrict__ edges) {
+// Several graphs (the kNN graphs of a DGCNN's blocks, same B, N, k) in one
+// launch: blockIdx.x = graph * (B * P) + cloud * P + range.
+constexpr int RG_MAX_GRAPHS = 8;
+struct RevGraphJobs {
+    const int32_t* idx[RG_MAX_GRAPHS];
+    int32_t* rowptr[RG_MAX_GRAPHS];
+    int32_t* edges[RG_MAX_GRAPHS];
+};
+
+__global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(RevGraphJobs jobs, int B, int N, int k, int P,
+                                                                   int cap) {
     extern __shared__ int32_t rg[];
+    const int gi = blockIdx.x / (B * P);
+    const int32_t* __restrict__ idx = jobs.idx[gi];
+    int32_t* __restrict__ rowptr = jobs.rowptr[gi];
+    int32_t* __restrict__ edges = jobs.edges[gi];
+    const int blk = blockIdx.x - gi * (B * P);
     const int R = (N + P - 1) / P;
     int32_t* cnt = rg;                 // [R] in-degree -> fill cursor
     int32_t* start = cnt + R;          // [R] local list starts
     int32_t* red = start + R;          // [RG_THREADS / 64 + 2]
     int32_t* list = red + RG_THREADS / 64 + 2;   // [cap] edge ids
     int32_t* ltg = list + cap;                    // [cap] local target of each slot
-    const int b = blockIdx.x / P, p = blockIdx.x - b * P;
+    const int b = blk / P, p = blk - b * P;
     const int t = threadIdx.x;
     const int j0 = p * R, j1 = min(N, j0 + R), nr = max(0, j1 - j0);
     const int64_t base = (int64_t)b * N;
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(const int32_t
         cnt[r] = run;  // fill cursor
         run += c;
     }
-    if (b == (int)(gridDim.x / P) - 1 && p == P - 1 && t == 0) rowptr[base + N] = (int32_t)((base + N) * k);
+    if (b == B - 1 && p == P - 1 && t == 0) rowptr[base + N] = (int32_t)((base + N) * k);
     __syncthreads();
     const bool in_lds = total <= cap;
     int32_t* out = in_lds ? list : edges + ebase + before;
@@ -1031,20 +1044,37 @@ int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co, double count,
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-int dgx_graph_reverse(const int32_t* idx, int B, int N, int k, int32_t* rowptr, int32_t* edges, void* stream) {
-    if (!idx || !rowptr || !edges || B < 1 || N < 1 || k < 1 || k > 64) return DGX_EINVAL;
+int dgx_graph_reverse_multi(int n, const int32_t* const* idx, int B, int N, int k, int32_t* const* rowptr,
+                            int32_t* const* edges, void* stream) {
+    if (n < 1 || n > RG_MAX_GRAPHS || !idx || !rowptr || !edges || B < 1 || N < 1 || k < 1 || k > 64)
+        return DGX_EINVAL;
     if ((int64_t)B * N >= (1LL << 25)) return DGX_EUNSUPPORTED;
-    // workgroups per cloud: enough to fill the chip and to keep a range's
-    // edges (about N*k/P) well inside the LDS list capacity
+    RevGraphJobs jobs{};
+    for (int g = 0; g < n; ++g) {
+        if (!idx[g] || !rowptr[g] || !edges[g]) return DGX_EINVAL;
+        jobs.idx[g] = idx[g];
+        jobs.rowptr[g] = rowptr[g];
+        jobs.edges[g] = edges[g];
+    }
+    // workgroups per cloud: enough (over all graphs) to fill the chip, and few
+    // enough that the cloud's index list is not re-scanned more than needed
+    // (every workgroup of a cloud scans it twice); a range's edges (about
+    // N*k/P) stay well inside the LDS list capacity
     int P = 1;
-    while (P < N && ((int64_t)B * P < 512 || (int64_t)N * k / P > RG_CAP / 2)) P *= 2;
+    while (P < N && ((int64_t)n * B * P < 512 || (int64_t)N * k / P > RG_CAP / 2)) P *= 2;
     const int R = (N + P - 1) / P;
-    const int cap = (int)std::min<int64_t>(RG_CAP, std::max<int64_t>(1024, 4 * ((int64_t)N * k / P)));
+    // list capacity 1.75x a range's mean edge count (two workgroups per CU at
+    // cfg2); a range beyond it (degenerate clouds) sorts its lists in HBM
+    const int cap = (int)std::min<int64_t>(RG_CAP, std::max<int64_t>(1024, 7 * ((int64_t)N * k / P) / 4));
     const size_t lds = ((size_t)2 * R + RG_THREADS / 64 + 2 + 2 * (size_t)cap) * sizeof(int32_t);
     if (lds > 160 * 1024) return DGX_EUNSUPPORTED;
-    hipLaunchKernelGGL(rev_graph_par_kernel, dim3((unsigned)(B * P)), dim3(RG_THREADS), lds, dgx_stream(stream), idx,
-                       N, k, P, cap, rowptr, edges);
+    hipLaunchKernelGGL(rev_graph_par_kernel, dim3((unsigned)(n * B * P)), dim3(RG_THREADS), lds, dgx_stream(stream),
+                       jobs, B, N, k, P, cap);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_graph_reverse(const int32_t* idx, int B, int N, int k, int32_t* rowptr, int32_t* edges, void* stream) {
+    return dgx_graph_reverse_multi(1, &idx, B, N, k, &rowptr, &edges, stream);
 }
 
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,

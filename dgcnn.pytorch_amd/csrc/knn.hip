@@ -127,11 +127,13 @@ __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[
     // compare uses the NEW value against the original list, so elements of
     // equal value keep their relative order (a carried-element bubble would
     // swap equal neighbours). One lane mask live per step.
+    // For a sorted list the new slot q value is median(v[q-1], v[q], nv): one
+    // v_med3_f32 per slot (ties keep the value, the ids follow the compares).
     bool gt_cur = nv > v[KMAX - 1];
 #pragma unroll
     for (int q = KMAX - 1; q > 0; --q) {
         const bool gt_prev = nv > v[q - 1];
-        v[q] = gt_prev ? v[q - 1] : (gt_cur ? nv : v[q]);
+        v[q] = __builtin_amdgcn_fmed3f(v[q - 1], v[q], nv);
         id[q] = gt_prev ? id[q - 1] : (gt_cur ? nj : id[q]);
         gt_cur = gt_prev;
     }
@@ -146,6 +148,8 @@ __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[
 // its row, which is recomputed exactly (knn_fix_kernel).
 template <int KB>
 struct KnnList {
+    // (KL 10 / 9 at KB 20 measured: fewer insertion VALU, but the rows they flag
+    // cost more in knn_fix_kernel than the lists save)
     static constexpr int KL = KB <= 16 ? 10 : (KB <= 20 ? 12 : (KB <= 32 ? 15 : (KB <= 40 ? 17 : 23)));
     static constexpr int RPL = (KB + 3) / 4;   // ranks per lane of a wave's 4-list merge
 };
@@ -294,6 +298,10 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     {
         const int qs = min(q, N - 1);
         ld_vec<NSTEP>(ib + ((int64_t)(qs >> 4) * 64 + g * 16 + knn_row(qs & 15)) * NSTEP, bq);
+        // 2 x the query operand: every product and partial sum of the fmaf chain
+        // doubles exactly, so the MFMA returns fl(2 * dot) (dgcnn.py:7) directly
+#pragma unroll
+        for (int t = 0; t < NSTEP; ++t) bq[t] *= 2.0f;
     }
     const float xxq = q < N ? xx[(int64_t)b * N + q] : 0.f;
 
@@ -358,8 +366,7 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     };
 
     auto consider = [&](float dot, float xc, int j) {
-        const float two_dot = 2.0f * dot;
-        const float tq = two_dot - xc;
+        const float tq = dot - xc;  // dot is already 2 x (query operand doubled)
         const float v = tq - xxq;
         const bool pass = j < N && v >= thr;
         // unconditional store: a rejected candidate's slot is reused by the

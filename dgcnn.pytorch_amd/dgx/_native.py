@@ -47,6 +47,7 @@ _SIGS = {
     "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    "dgx_graph_reverse_multi": [_i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
                                  _i32, _vp],
     "dgx_colstats_rows": [_i64],

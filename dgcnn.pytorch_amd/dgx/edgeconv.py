@@ -21,6 +21,7 @@ BatchNorm decisions follow each BN module's own flags (dgx.bn). Under
 torch.autocast the op runs in the engine's own precision on fp32 inputs
 (precision.no_autocast): its GEMMs never return autocast-reduced products.
 """
+import ctypes
 import threading
 
 import torch
@@ -45,19 +46,24 @@ def set_debug_capture(d):
     _tls.debug = d
 
 
-def _reverse_graph(idx, B, N, k, dev):
-    """Reverse kNN graph (CSR of in-edges, dgx_graph_reverse) of one block, on
-    the current stream. Built in the backward, right before its consumer: a
-    build on a side stream overlapping the forward measured slower (1.63 vs
-    1.56 ms/step at cfg2; the concurrent kernels contend for the L2 the kNN
-    operand images live in)."""
+def _reverse_graphs(idxs, B, N, k, dev):
+    """Reverse kNN graphs (CSR of in-edges) of all blocks in one launch
+    (dgx_graph_reverse_multi), on the current stream at the start of the
+    backward: the blocks' workgroups share the chip, and each cloud's index
+    list is re-scanned by fewer workgroups than per-block launches need. (A
+    build on a side stream overlapping the forward measured slower: 1.63 vs
+    1.56 ms/step at cfg2, the concurrent kernels contend for the L2 the kNN
+    operand images live in.)"""
     M = B * N
-    rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
-    edges = torch.empty(M * k, dtype=torch.int32, device=dev)
+    n = len(idxs)
+    rowptrs = [torch.empty(M + 1, dtype=torch.int32, device=dev) for _ in range(n)]
+    edges = [torch.empty(M * k, dtype=torch.int32, device=dev) for _ in range(n)]
+    arr = ctypes.c_void_p * n
     with torch.cuda.device(dev):
-        nat.check(nat.lib().dgx_graph_reverse(nat.i32(idx), B, N, k, nat.i32(rowptr), nat.i32(edges),
-                                              nat.stream_of(idx)), "reverse graph")
-    return rowptr, edges
+        nat.check(nat.lib().dgx_graph_reverse_multi(
+            n, arr(*[i.data_ptr() for i in idxs]), B, N, k, arr(*[r.data_ptr() for r in rowptrs]),
+            arr(*[e.data_ptr() for e in edges]), nat.stream_of(idxs[0])), "reverse graphs")
+    return list(zip(rowptrs, edges))
 
 
 class _Layer:
@@ -219,12 +225,15 @@ class _EdgeConvStack(torch.autograd.Function):
             dnew = torch.empty((M, max(lead, 1)), dtype=torch.float32, device=dev)
         else:
             dxcat = dxcat.contiguous().clone()
+        for idx in (st[0] for st in ctx.layer_state):
+            assert idx.dtype == torch.int32 and idx.is_contiguous()
+        rev = _reverse_graphs([st[0] for st in ctx.layer_state], B, N, k, dev)
         for li in reversed(range(nl)):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
             w = params[3 * li]
             idx, PQ, ysel, arg, sumP, st, wprep = ctx.layer_state[li]
-            rowptr, edges = _reverse_graph(idx, B, N, k, dev)
+            rowptr, edges = rev[li]
             off = sum(widths[:li])
             prev = off - widths[li - 1] if li > 0 else None
             X = x_pm if li == 0 else xcat[:, prev: prev + cin]

@@ -168,6 +168,10 @@ int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co,
                             float* c0, float* c1, int accumulate, void* stream);
 int dgx_graph_reverse(const int32_t* idx, int B, int N, int k,
                       int32_t* rowptr, int32_t* edges, void* stream);
+/* The reverse graphs of n <= 8 kNN graphs of the same (B, N, k) — a
+ * DGCNN's blocks — in one launch (the graphs' workgroups share the chip). */
+int dgx_graph_reverse_multi(int n, const int32_t* const* idx, int B, int N, int k,
+                            int32_t* const* rowptr, int32_t* const* edges, void* stream);
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
                              const int32_t* edges, const float* dz,
                              const uint8_t* arg, const float* sumP, int B, int N,
