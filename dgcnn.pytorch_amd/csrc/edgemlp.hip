@@ -329,6 +329,193 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
     }
 }
 
+// ---- fused forward (bf16 mode): h1 -> conv2 on the MFMA -> max over k + BN2
+// statistics, without writing z2. A pair of waves takes one point at a time,
+// each wave half of the C2 output channels: the point's k edge rows, padded to
+// KT tiles of 16, are the MFMA row tiles. Per row tile a lane builds its A
+// fragment (row = lane & 15, channels 32 ks + 8 g .. +7, g = lane >> 4)
+// straight from the gathered P_j and the point's Q_i (h1 = LReLU(a1 (P_j + Q_i)
+// + b1), rounded to bf16 as the unfused path stores it), multiplies by its half
+// of W2 (B fragments in registers for the whole kernel) and folds the 16 x C2/2
+// result into the point's running max (and first slot) and the per-column sums
+// of z2 and z2^2. W2's rows come pre-multiplied by dir = sign(gamma2) (exact),
+// so the max of dir * z2 is the max (or min) the BN2 + LReLU ordering needs;
+// outputs are multiplied back. Optionally writes h1 (bf16, the backward's
+// operand; the half-0 wave of a pair stores it). Block = 2 pairs x EMF_PPW
+// points; blocks of a cloud stay on one XCD (its P rows are L2-resident);
+// partial-stat row = block.
+constexpr int EMF_PPW = 4;
+constexpr int EMF_PPB = 2 * EMF_PPW;
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+template <int KT, int NTW>
+__global__ __launch_bounds__(256) void emlp_fwd_kernel(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int B, int N, int k, int tiles,
+    const float* __restrict__ scale1, const float* __restrict__ shift1, float slope1, const __bf16* __restrict__ W2d,
+    const float* __restrict__ dir2, float* __restrict__ ysel, uint8_t* __restrict__ arg, float* __restrict__ part,
+    __bf16* __restrict__ H1) {
+    constexpr int C1 = 64, C2 = 32 * NTW;
+    __shared__ float red[2][2][C2];
+    int b, tile;
+    if (!dgx_xcd_cloud_map(blockIdx.x, B, tiles, b, tile)) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pair = wave >> 1, half = wave & 1;
+    const int g = lane >> 4, r16 = lane & 15;
+    const int cb = half * NTW;  // first channel tile of this wave
+    bf16x8_t wf[NTW][2];
+#pragma unroll
+    for (int ct = 0; ct < NTW; ++ct)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+            wf[ct][ks] = *reinterpret_cast<const bf16x8_t*>(W2d + ((cb + ct) * 16 + r16) * C1 + ks * 32 + 8 * g);
+    float a1[2][8];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) ld8(scale1 + ks * 32 + 8 * g, a1[ks]);
+    float2 s1[NTW], s2[NTW];
+#pragma unroll
+    for (int ct = 0; ct < NTW; ++ct) { s1[ct] = make_float2(0.f, 0.f); s2[ct] = make_float2(0.f, 0.f); }
+    const int64_t cbase = (int64_t)b * N;
+    const int n0 = tile * EMF_PPB + pair * EMF_PPW;
+    const int np = max(0, min(EMF_PPW, N - n0));
+    // Per point its KT row tiles are unrolled with the P_j loads one tile
+    // ahead (ids of all tiles up front); the next point's Q_i and ids are issued
+    // during the current point. The point loop is not unrolled (I-cache).
+    int jv[KT];
+    float qv[2][8];
+    auto load_ids = [&](int pp) {
+        const int64_t i = cbase + n0 + pp;
+#pragma unroll
+        for (int rt = 0; rt < KT; ++rt) jv[rt] = idx[i * k + min(rt * 16 + r16, k - 1)];
+    };
+    if (np > 0) {
+        load_ids(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) ld8(PQ + (cbase + n0) * ldpq + C1 + ks * 32 + 8 * g, qv[ks]);
+    }
+#pragma unroll 1
+    for (int pp = 0; pp < np; ++pp) {
+        const int64_t i = cbase + n0 + pp;
+        float pb[2][2][8];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) ld8(PQ + (cbase + jv[0]) * ldpq + ks * 32 + 8 * g, pb[0][ks]);
+        // h1 = LReLU(a1 (P_j + Q_i) + b1) as LReLU(a1 P_j + qb), qb = a1 Q_i + b1 per point
+        float qb[2][8];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            float b1[8];
+            ld8(shift1 + ks * 32 + 8 * g, b1);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) qb[ks][u] = fmaf(a1[ks][u], qv[ks][u], b1[u]);
+        }
+        if (pp + 1 < np) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) ld8(PQ + (i + 1) * ldpq + C1 + ks * 32 + 8 * g, qv[ks]);
+        }
+        float best[NTW];
+        int barg[NTW];
+#pragma unroll
+        for (int ct = 0; ct < NTW; ++ct) { best[ct] = -INFINITY; barg[ct] = 0; }
+#pragma unroll
+        for (int rt = 0; rt < KT; ++rt) {
+            if (rt + 1 < KT) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    ld8(PQ + (cbase + jv[rt + 1]) * ldpq + ks * 32 + 8 * g, pb[(rt + 1) & 1][ks]);
+            } else if (pp + 1 < np) {
+                load_ids(pp + 1);
+            }
+            const int s = rt * 16 + r16;
+            bf16x8_t af[2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    af[ks][u] = (__bf16)lrelu(fmaf(a1[ks][u], pb[rt & 1][ks][u], qb[ks][u]), slope1);
+            if (H1 && half == 0 && s < k) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    *reinterpret_cast<bf16x8_t*>(H1 + (i * k + s) * C1 + ks * 32 + 8 * g) = af[ks];
+            }
+            f32x4_t acc[NTW];
+#pragma unroll
+            for (int ct = 0; ct < NTW; ++ct) {
+                acc[ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], wf[ct][ks], acc[ct], 0, 0, 0);
+            }
+            // acc[ct][r]: edge row rt*16 + 4g + r, channel (cb + ct)*16 + r16. Tiles
+            // before the last are full; the last masks rows >= k by value.
+            const int sb = rt * 16 + 4 * g;
+#pragma unroll
+            for (int ct = 0; ct < NTW; ++ct) {
+                const f32x4_t v = acc[ct];
+                float w[4], x[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool ok = rt + 1 < KT || sb + r < k;
+                    w[r] = ok ? v[r] : 0.f;
+                    x[r] = ok ? v[r] : -INFINITY;
+                }
+                s1[ct].x += w[0] + w[2];
+                s1[ct].y += w[1] + w[3];
+                s2[ct].x = fmaf(w[0], w[0], fmaf(w[2], w[2], s2[ct].x));
+                s2[ct].y = fmaf(w[1], w[1], fmaf(w[3], w[3], s2[ct].y));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool better = x[r] > best[ct];
+                    best[ct] = better ? x[r] : best[ct];
+                    barg[ct] = better ? sb + r : barg[ct];
+                }
+            }
+        }
+        // the four lane groups hold rows 4g.. of the same channel: canonical
+        // (larger value, then smaller slot) reduction; group g then writes tile g
+#pragma unroll
+        for (int ct = 0; ct < NTW; ++ct) {
+#pragma unroll
+            for (int o = 16; o <= 32; o <<= 1) {
+                const float ov = __shfl_xor(best[ct], o);
+                const int oa = __shfl_xor(barg[ct], o);
+                const bool take = ov > best[ct] || (ov == best[ct] && oa < barg[ct]);
+                best[ct] = take ? ov : best[ct];
+                barg[ct] = take ? oa : barg[ct];
+            }
+        }
+        if (g < NTW) {
+            float bv = best[0];
+            int ba = barg[0];
+#pragma unroll
+            for (int u = 1; u < NTW; ++u) {
+                bv = g == u ? best[u] : bv;
+                ba = g == u ? barg[u] : ba;
+            }
+            const int c2 = (cb + g) * 16 + r16;
+            ysel[i * C2 + c2] = dir2[c2] * bv;
+            arg[i * C2 + c2] = (uint8_t)ba;
+        }
+    }
+    // BN2 partials of this block: lane sums -> over the lane groups -> over pairs
+#pragma unroll
+    for (int ct = 0; ct < NTW; ++ct) {
+        float t1 = s1[ct].x + s1[ct].y, t2 = s2[ct].x + s2[ct].y;
+        t1 += __shfl_xor(t1, 16);
+        t2 += __shfl_xor(t2, 16);
+        t1 += __shfl_xor(t1, 32);
+        t2 += __shfl_xor(t2, 32);
+        if (g == 0) {
+            red[pair][0][(cb + ct) * 16 + r16] = t1;
+            red[pair][1][(cb + ct) * 16 + r16] = t2;
+        }
+    }
+    __syncthreads();
+    const int prow = b * tiles + tile;
+    for (int c = threadIdx.x; c < C2; c += 256) {
+        part[(int64_t)prow * 2 * C2 + c] = dir2[c] * (red[0][0][c] + red[1][0][c]);
+        part[(int64_t)prow * 2 * C2 + C2 + c] = red[0][1][c] + red[1][1][c];
+    }
+}
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
@@ -348,6 +535,49 @@ int dgx_edge_mlp_h1_f32(const float* PQ, int ldpq, const int32_t* idx, int B, in
     else
         hipLaunchKernelGGL(mlp_h1_kernel<false>, dim3(grid), dim3(EM_THREADS), 0, dgx_stream(stream), PQ, ldpq, idx,
                            N, k, C1, E, scale, shift, slope, H1);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_mlp_fused_rows(int B, int N) {
+    if (B < 1 || N < 1) return DGX_EINVAL;
+    return B * ((N + EMF_PPB - 1) / EMF_PPB);
+}
+
+int dgx_edge_mlp_fused_fwd_bf16(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1, int C2,
+                                const float* scale1, const float* shift1, float slope1, const void* W2d,
+                                const float* dir2, float* ysel, uint8_t* arg, float* partials, int nrows, void* H1,
+                                void* stream) {
+    if (!PQ || !idx || !scale1 || !shift1 || !W2d || !dir2 || !ysel || !arg || !partials) return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || ldpq < 2 * C1) return DGX_EINVAL;
+    if (C1 != 64 || (C2 != 64 && C2 != 128) || k > 64 || ldpq % 4 || !al16(PQ) || !al16(scale1) || !al16(shift1) ||
+        !al16(W2d) || (H1 && !al16(H1)))
+        return DGX_EUNSUPPORTED;
+    const int tiles = (N + EMF_PPB - 1) / EMF_PPB;
+    if (nrows != B * tiles) return DGX_EINVAL;
+    const dim3 grid(dgx_xcd_cloud_grid(B, tiles));
+    const __bf16* w = static_cast<const __bf16*>(W2d);
+    __bf16* h = static_cast<__bf16*>(H1);
+    hipStream_t st = dgx_stream(stream);
+    const int kt = (k + 15) / 16;
+#define DGX_EMF(KTV, NTV)                                                                                        \
+    hipLaunchKernelGGL((emlp_fwd_kernel<KTV, NTV / 2>), grid, dim3(256), 0, st, PQ, ldpq, idx, B, N, k, tiles, scale1, \
+                       shift1, slope1, w, dir2, ysel, arg, partials, h)
+    if (C2 == 128) {
+        switch (kt) {
+            case 1: DGX_EMF(1, 8); break;
+            case 2: DGX_EMF(2, 8); break;
+            case 3: DGX_EMF(3, 8); break;
+            default: DGX_EMF(4, 8); break;
+        }
+    } else {
+        switch (kt) {
+            case 1: DGX_EMF(1, 4); break;
+            case 2: DGX_EMF(2, 4); break;
+            case 3: DGX_EMF(3, 4); break;
+            default: DGX_EMF(4, 4); break;
+        }
+    }
+#undef DGX_EMF
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -36,7 +36,7 @@ constexpr int GB_BM = 128;
 constexpr int GB_BK = 32;
 constexpr int GB_LDK = GB_BK + 8;  // bf16 per LDS row (80 B)
 
-enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4 };
+enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4, EPI_DZ2 = 5 };
 
 template <typename T> struct VecOf;
 template <> struct VecOf<float> { static constexpr int V = 4; typedef float4 type; };
@@ -385,7 +385,7 @@ template <bool TN, int BM, int BN, int EPI>
 __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
     int kchunk, int ka, float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend,
-    int64_t ldd) {
+    int64_t ldd, const uint8_t* __restrict__ aux8 = nullptr) {
     static_assert(BM == G2_BM || (EPI != EPI_STATS && EPI != EPI_STATS16), "stats rows are per 128-row tile");
     constexpr int WN = BN >= 128 ? 2 : 1;
     constexpr int WM = 4 / WN;
@@ -523,12 +523,28 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     constexpr int NR = BM * LDT * 4 <= LDSB ? 1 : 2;
     constexpr int RR = BM / NR;
     static_assert(RR * LDT * 4 <= LDSB && WM % NR == 0, "epilogue tile must fit the stage buffers");
-    constexpr int VO = EPI == EPI_STATS16 ? 8 : 4;  // outputs per 16-byte store
+    constexpr int VO = (EPI == EPI_STATS16 || EPI == EPI_DZ2) ? 8 : 4;  // outputs per 16-byte store
     constexpr int CPR = BN / VO;
     float* tile = reinterpret_cast<float*>(lds);
     const bool vec_out = (ldc % VO) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
                          (EPI != EPI_ACCUM || !addend ||
                           ((ldd % 4) == 0 && (reinterpret_cast<uintptr_t>(addend) & 15) == 0));
+    // EPI_DZ2 (BN2 backward of the PositionEmbedding edge MLP, dense over edge
+    // rows i = p*k + s): dZ2 = c1 z + c0 + [arg[p] == s] a2 dz[p], bf16 out;
+    // part = [c0 | c1 | a2] (3 N), addend = dz (M/k x N), ldd = k, aux8 = arg.
+    // A thread's output columns are fixed (GB_THREADS % CPR == 0), so its
+    // constants are loaded once
+    float k0[8], k1[8], a2[8];
+    if constexpr (EPI == EPI_DZ2) {
+        static_assert(GB_THREADS % CPR == 0, "fixed columns per thread");
+        const int jc = min(j0 + (tid % CPR) * VO, N - 8);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            *reinterpret_cast<float4*>(k0 + 4 * h) = *reinterpret_cast<const float4*>(part + jc + 4 * h);
+            *reinterpret_cast<float4*>(k1 + 4 * h) = *reinterpret_cast<const float4*>(part + N + jc + 4 * h);
+            *reinterpret_cast<float4*>(a2 + 4 * h) = *reinterpret_cast<const float4*>(part + 2 * N + jc + 4 * h);
+        }
+    }
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
         __syncthreads();  // K loop / stats / previous round done with the buffers
@@ -541,6 +557,46 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
                     for (int b = 0; b < TN_; ++b)
                         tile[(wm * TM * 16 - q * RR + a * 16 + (lane >> 4) * 4 + r) * LDT + wn * TN_ * 16 + b * 16 +
                              (lane & 15)] = acc[a][b][r];
+        }
+        if constexpr (EPI == EPI_DZ2) {
+            // the rows' dz / slot pieces are loaded for all of this round's
+            // iterations at once, before the tile is ready (latency overlap)
+            constexpr int IT = RR * CPR / GB_THREADS;
+            static_assert(RR * CPR % GB_THREADS == 0, "whole iterations");
+            float dd[IT][8];
+            uint2 aw[IT];
+            const int64_t kk = ldd;
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int e = tid + it * GB_THREADS;
+                const int rr = e / CPR, c = (e - rr * CPR) * VO;
+                const int64_t i = min(i0 + q * RR + rr, M - 1);
+                const int j = min(j0 + c, N - 8);
+                const int64_t pnt = i / kk;
+                *reinterpret_cast<float4*>(dd[it]) = *reinterpret_cast<const float4*>(addend + pnt * N + j);
+                *reinterpret_cast<float4*>(dd[it] + 4) = *reinterpret_cast<const float4*>(addend + pnt * N + j + 4);
+                aw[it] = *reinterpret_cast<const uint2*>(aux8 + pnt * N + j);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int e = tid + it * GB_THREADS;
+                const int rr = e / CPR, c = (e - rr * CPR) * VO;
+                const int64_t i = i0 + q * RR + rr;
+                const int j = j0 + c;
+                if (i >= M || j + 8 > N) continue;
+                const int sl = (int)(i - (i / kk) * kk);
+                const float* src = tile + rr * LDT + c;
+                bf16x8 h;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int slot = (int)(((u < 4 ? aw[it].x : aw[it].y) >> (8 * (u & 3))) & 0xffu);
+                    const float v = fmaf(k1[u], src[u], k0[u]);
+                    h[u] = (bf16)(slot == sl ? v + a2[u] * dd[it][u] : v);
+                }
+                *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(out) + i * ldc + j) = h;
+            }
+            continue;
         }
         __syncthreads();
         for (int e = tid; e < RR * CPR; e += GB_THREADS) {
@@ -1078,6 +1134,31 @@ int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda, const void* 
     }
 #undef DGX_GEMM
     return DGX_EUNSUPPORTED;
+}
+
+int dgx_gemm_dz2_bf16(const void* H1, const void* W2, int M, int N, int K, const float* dz, const uint8_t* arg,
+                      const float* consts, int k, void* dZ2, void* stream) {
+    if (!H1 || !W2 || !dz || !arg || !consts || !dZ2 || M < 1 || N < 1 || K < 1 || k < 1 || M % k) return DGX_EINVAL;
+    if (!aligned_to(H1, 16) || !aligned_to(W2, 16) || !aligned_to(dz, 16) || !aligned_to(consts, 16) ||
+        !aligned_to(dZ2, 16) || reinterpret_cast<uintptr_t>(arg) % 8 || K % G2_BK || N % 8)
+        return DGX_EUNSUPPORTED;
+    const bf16* a = static_cast<const bf16*>(H1);
+    const bf16* b = static_cast<const bf16*>(W2);
+    float* out = static_cast<float*>(dZ2);
+    hipStream_t st = dgx_stream(stream);
+    const int nI = (M + G2_BM - 1) / G2_BM;
+    if (N > 64) {
+        const int nJ = (N + 127) / 128;
+        hipLaunchKernelGGL((gemm_lds_kernel<false, G2_BM, 128, EPI_DZ2>), dim3((unsigned)(nI * nJ)), dim3(GB_THREADS),
+                           0, st, a, (int64_t)K, b, (int64_t)K, M, N, K, K, K, out, (int64_t)N, const_cast<float*>(consts),
+                           dz, (int64_t)k, arg);
+    } else {
+        const int nJ = (N + 63) / 64;
+        hipLaunchKernelGGL((gemm_lds_kernel<false, G2_BM, 64, EPI_DZ2>), dim3((unsigned)(nI * nJ)), dim3(GB_THREADS),
+                           0, st, a, (int64_t)K, b, (int64_t)K, M, N, K, K, K, out, (int64_t)N, const_cast<float*>(consts),
+                           dz, (int64_t)k, arg);
+    }
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int tn, int M, int N, int K,

@@ -78,6 +78,10 @@ _SIGS = {
                                 _vp],
     "dgx_edge_mlp_scatter_f32": [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
     "dgx_hog_1x1_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    "dgx_edge_mlp_fused_rows": [_i32, _i32],
+    "dgx_gemm_dz2_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp],
+    "dgx_edge_mlp_fused_fwd_bf16": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp,
+                                    _vp, _i32, _vp, _vp],
 }
 _RESTYPES = {
     "dgx_version": ctypes.c_char_p,

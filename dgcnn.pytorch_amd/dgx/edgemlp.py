@@ -58,6 +58,35 @@ class _EdgeMLP2(torch.autograd.Function):
                 st1 = bn_.running_stats(bn1, g1, b1, stream)
                 # sum_k P_j only enters the train-mode BN1 backward (c1 = 0 here)
                 sumP1 = torch.zeros((M, C1), dtype=torch.float32, device=dev) if need_grad else None
+            fused = bf16 and C1 == 64 and C2 in (64, 128) and k <= 64
+            if fused:
+                # h1 -> conv2 (MFMA) -> max over k + BN2 statistics in one kernel: z2 never
+                # reaches HBM; h1 (bf16) is written only when the backward needs it
+                wprep = G.prep_weight(w2, C2, C1, False)
+                dir2 = torch.where(g2 < 0, -1.0, 1.0).to(torch.float32).contiguous()
+                W2d = (W2 * dir2.view(C2, 1)).to(torch.bfloat16).contiguous()
+                H1 = torch.empty((E, C1), dtype=torch.bfloat16, device=dev) if need_grad else None
+                rows2 = L.dgx_edge_mlp_fused_rows(B, N)
+                part2 = torch.empty((rows2, 2, C2), dtype=torch.float32, device=dev)
+                ysel = torch.empty((M, C2), dtype=torch.float32, device=dev)
+                arg = torch.empty((M, C2), dtype=torch.uint8, device=dev)
+                nat.check(L.dgx_edge_mlp_fused_fwd_bf16(
+                    nat.f32(PQ), 2 * C1, nat.i32(idx), B, N, k, C1, C2, nat.f32(st1.scale), nat.f32(st1.shift),
+                    float(slope1), nat.bf16(W2d), nat.f32(dir2), nat.f32(ysel), nat.u8(arg), nat.f32(part2), rows2,
+                    nat.ptr(H1, nat.BF16), stream), "edge mlp fused forward")
+                st2 = (bn_.batch_stats(part2, rows2, float(E), bn2, g2, b2, stream) if use2
+                       else bn_.running_stats(bn2, g2, b2, stream))
+                out = torch.empty((M, C2), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, C2, nat.f32(st2.scale), nat.f32(st2.shift),
+                                                   float(slope2), nat.f32(out), C2, None, stream), "bn apply")
+                ctx.dims = (B, C, N, k, C1, C2)
+                ctx.slopes = (float(slope1), float(slope2))
+                ctx.st = (st1, st2)
+                ctx.wprep = wprep
+                ctx.bf16 = bf16
+                if need_grad:
+                    ctx.save_for_backward(X, idx, PQ, sumP1, H1, None, ysel, arg, w1, w2)
+                return out.view(B, N, C2).permute(0, 2, 1)
             h16 = bf16 and C1 % 64 == 0
             H1 = torch.empty((E, C1), dtype=torch.bfloat16 if h16 else torch.float32, device=dev)
             nat.check(L.dgx_edge_mlp_h1_f32(nat.f32(PQ), 2 * C1, nat.i32(idx), B, N, k, C1, nat.f32(st1.scale),
@@ -114,7 +143,8 @@ class _EdgeMLP2(torch.autograd.Function):
         dev = X.device
         L = nat.lib()
         stream = nat.stream_of(X)
-        z16 = Z2.dtype == torch.bfloat16
+        fused = Z2 is None  # fused forward: z2 was never stored
+        z16 = fused or Z2.dtype == torch.bfloat16
         dY = dout.float().permute(0, 2, 1).reshape(M, C2).contiguous()
         with torch.cuda.device(dev):
             # ---- BN2 + LReLU backward at the selected edges, then dense over all edges
@@ -125,10 +155,18 @@ class _EdgeMLP2(torch.autograd.Function):
                                             nat.f32(st2.shift), nat.f32(st2.mean), nat.f32(st2.invstd), slope2,
                                             nat.f32(dz), nat.f32(part), nblk, stream), "edge bwd dz")
             dg2, db2, c0, c1 = bn_.backward_consts(part, nblk, float(E), st2, stream)
-            dZ2 = torch.empty((E, C2), dtype=Z2.dtype, device=dev)
-            nat.check(L.dgx_edge_mlp_dz_f32(nat.f32(dz), nat.u8(arg), nat.ptr(Z2, nat.F32, nat.BF16), int(z16), B, N, k, C2,
-                                            nat.f32(st2.scale), nat.f32(c0), nat.f32(c1),
-                                            nat.ptr(dZ2, nat.F32, nat.BF16), stream), "edge dz2")
+            if fused:
+                # z2 recomputed from h1 on the MFMA, BN2 backward in the GEMM's epilogue:
+                # dZ2 = c1 z2 + c0 + [slot] a2 dz, stored bf16 (z2 never reaches HBM)
+                dZ2 = torch.empty((E, C2), dtype=torch.bfloat16, device=dev)
+                consts = torch.cat([c0, c1, st2.scale]).contiguous()
+                nat.check(L.dgx_gemm_dz2_bf16(nat.bf16(H1), nat.bf16(ctx.wprep[0]), E, C2, C1, nat.f32(dz),
+                                              nat.u8(arg), nat.f32(consts), k, nat.bf16(dZ2), stream), "edge dz2 gemm")
+            else:
+                dZ2 = torch.empty((E, C2), dtype=Z2.dtype, device=dev)
+                nat.check(L.dgx_edge_mlp_dz_f32(nat.f32(dz), nat.u8(arg), nat.ptr(Z2, nat.F32, nat.BF16), int(z16), B, N,
+                                                k, C2, nat.f32(st2.scale), nat.f32(c0), nat.f32(c1),
+                                                nat.ptr(dZ2, nat.F32, nat.BF16), stream), "edge dz2")
             # ---- conv2 GEMMs: dH1 = dZ2 W2, dW2 = dZ2^T H1
             gw2 = torch.empty((C2, C1), dtype=torch.float32, device=dev)
             if ctx.wprep is not None and z16:

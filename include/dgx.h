@@ -319,6 +319,24 @@ int dgx_edge_mlp_h1_bwd_rows(int B, int N, int k, int C1);
 int dgx_edge_mlp_h1_bwd_f32(float* dH, const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1,
                             const float* scale, const float* shift, const float* mean, const float* invstd,
                             float slope, float* partials, int nrows, void* stream);
+/* Fused bf16 forward of the edge MLP (h1, conv2, max over k and BN2 statistics
+ * in one kernel; z2 is never stored): W2d = bf16(dir2[c] * W2[c][:]) with
+ * dir2 = sign(gamma2) (+-1), so the kernel maximises dir2*z2; ysel/arg as the
+ * unfused max-over-k entry writes them (ysel in z2's sign), partials [nrows][2][C2] (sum z2,
+ * sum z2^2) with nrows = dgx_edge_mlp_fused_rows(B, N) for BN2; h1 (E x C1
+ * bf16) is written when H1 != NULL (the backward's operand). C1 = 64,
+ * C2 in {64, 128}, k <= 64, 16-byte aligned operands. */
+int dgx_edge_mlp_fused_rows(int B, int N);
+/* Its backward partner: dZ2 (E x C2 bf16) = c1 (H1 W2^T) + c0 + [arg == s] a2 dz
+ * for edge rows e = p*k + s, z2 recomputed on the MFMA from h1 (E x C1 bf16,
+ * K = C1 % 64 == 0) and W2 (C2 x C1 bf16) with the BN2 backward in the
+ * epilogue; consts = [c0 | c1 | a2] (3 x C2 fp32), dz / arg (E/k x C2). */
+int dgx_gemm_dz2_bf16(const void* H1, const void* W2, int M, int N, int K, const float* dz, const uint8_t* arg,
+                      const float* consts, int k, void* dZ2, void* stream);
+int dgx_edge_mlp_fused_fwd_bf16(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1, int C2,
+                                const float* scale1, const float* shift1, float slope1, const void* W2d,
+                                const float* dir2, float* ysel, uint8_t* arg, float* partials, int nrows, void* H1,
+                                void* stream);
 int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const float* sumP, const int32_t* rowptr,
                              const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
                              const float* c1, float* dPQ, void* stream);

@@ -101,19 +101,21 @@ def test_edge_mlp_eval_matches_reference(cuda):
     assert rel_err(y.cpu(), ref) < TOL
 
 
-def test_edge_mlp_bf16_mode(cuda):
-    """bf16 GEMM operands (h1, dZ2 rounded to bf16, z2 stored bf16): within
-    bf16 operand rounding (3e-2) of the fp64 reference."""
+@pytest.mark.parametrize("B,N,k,c2", [(2, 512, 20, 128), (2, 1024, 40, 128), (3, 256, 10, 64), (1, 300, 33, 64)])
+def test_edge_mlp_bf16_mode(cuda, B, N, k, c2):
+    """bf16 mode (the fused forward: h1 -> conv2 on the MFMA -> max over k and
+    BN2 statistics in one kernel, z2 recomputed from h1 in the backward): within
+    bf16 operand rounding (3e-2) of the fp64 reference. k = 20/40/10/33 cover
+    2, 3, 1 and 3 (partial) 16-row tiles per point; C2 = 64 is the semseg width."""
     from dgx import precision, synth
     from dgx.edgemlp import edge_mlp2
-    B, N, k = 2, 512, 20
-    conv1, conv2 = _convs(21)
-    ref1, ref2 = _convs(21)
+    conv1, conv2 = _convs(21, c2=c2)
+    ref1, ref2 = _convs(21, c2=c2)
     ref1, ref2 = ref1.double().train(), ref2.double().train()
     conv1, conv2 = conv1.to(cuda).train(), conv2.to(cuda).train()
     pts = synth.cube_clouds(B, N, 8)
     x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1).requires_grad_(True)
-    gout = torch.from_numpy(synth.uniform(10, (B, 128, N)) - 0.5).float()
+    gout = torch.from_numpy(synth.uniform(10, (B, c2, N)) - 0.5).float()
     precision.set("bf16")
     try:
         y = edge_mlp2(x, k, conv1, conv2, True)
