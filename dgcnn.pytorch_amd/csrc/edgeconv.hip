@@ -133,10 +133,15 @@ struct SliceSplit {
 // ld floats) into LDS [N][CS]; 16-byte loads when the slice is 16-byte aligned.
 // With `dir` each column is multiplied by the sign of dir[col] (+-1, exact),
 // so the forward gather's per-channel max-or-min becomes a plain max.
-template <int CS, int THREADS>
+// SWZ (CS = 8 only): the two 16-byte halves of row n are stored swapped when
+// bit 2 of n is set, so 16-byte reads of one half from random rows spread over
+// all eight 16-byte bank groups instead of the four that 32-byte rows map one
+// half to (fewer LDS bank conflicts in the backward scatter's gathers).
+template <int CS, int THREADS, bool SWZ = false>
 __device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float* __restrict__ src, int64_t ld,
                                             int N, int col0, int ncols, bool vec4,
                                             const float* __restrict__ dir = nullptr) {
+    static_assert(!SWZ || CS == 8, "swizzled rows are 2 x 16 bytes");
     const int t = threadIdx.x;
     auto sgn = [&](int c) { return (dir && col0 + c < ncols && dir[col0 + c] < 0.f) ? -1.f : 1.f; };
     constexpr int Q = CS >= 4 ? CS / 4 : 1;
@@ -154,19 +159,24 @@ __device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float
                 v[u] = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * qt);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                reinterpret_cast<float4*>(dst)[e + u * THREADS] =
+            for (int u = 0; u < 4; ++u) {
+                const int ee = e + u * THREADS;
+                const int pos = SWZ ? (ee ^ ((ee >> 3) & 1)) : ee;  // ee = 2n + q: q ^ bit 2 of n
+                reinterpret_cast<float4*>(dst)[pos] =
                     make_float4(v[u].x * sg.x, v[u].y * sg.y, v[u].z * sg.z, v[u].w * sg.w);
+            }
         }
         for (; e < total; e += THREADS) {
             const int n = e / Q;
             const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)n * ld + col0 + 4 * qt);
-            reinterpret_cast<float4*>(dst)[e] = make_float4(v.x * sg.x, v.y * sg.y, v.z * sg.z, v.w * sg.w);
+            const int pos = SWZ ? (e ^ ((e >> 3) & 1)) : e;
+            reinterpret_cast<float4*>(dst)[pos] = make_float4(v.x * sg.x, v.y * sg.y, v.z * sg.z, v.w * sg.w);
         }
     } else {
         for (int e = t; e < N * CS; e += THREADS) {
             const int n = e / CS, c = e - n * CS;
-            dst[e] = (col0 + c < ncols) ? src[(int64_t)n * ld + col0 + c] * sgn(c) : 0.f;
+            const int pos = SWZ ? n * CS + (c ^ (((n >> 2) & 1) << 2)) : e;
+            dst[pos] = (col0 + c < ncols) ? src[(int64_t)n * ld + col0 + c] * sgn(c) : 0.f;
         }
     }
 }
@@ -728,8 +738,21 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     int* bucket = reinterpret_cast<int*>(order + ((per + 7) & ~7));
     const bool full = o0 + CS <= Co;
     if (t < BW_BUCKETS) bucket[t] = 0;
-    stage_slice<CS, EC_THREADS>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
-    stage_slice<CS, EC_THREADS>(ds, dz + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+    constexpr bool SWZ = CS == 8;
+    stage_slice<CS, EC_THREADS, SWZ>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
+    stage_slice<CS, EC_THREADS, SWZ>(ds, dz + base * Co, Co, N, o0, Co, (Co % 4) == 0);
+    // row n of a swizzled slice: halves at 4 * (h ^ bit 2 of n)
+    auto lds_row = [&](const float* __restrict__ arr, int n, float (&r)[CS]) {
+        if constexpr (SWZ) {
+            const int sw = ((n >> 2) & 1) << 2;
+            const float4 a = *reinterpret_cast<const float4*>(arr + n * CS + sw);
+            const float4 b = *reinterpret_cast<const float4*>(arr + n * CS + (4 ^ sw));
+            r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+            r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+        } else {
+            lds_vec<CS>(arr + n * CS, r);
+        }
+    };
     const uint8_t* __restrict__ ab = arg + base * Co + o0;
     if (full && (Co % CS) == 0) {
         for (int n = t; n < N; n += EC_THREADS) {
@@ -815,12 +838,12 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             const uint32_t slot = (uint32_t)(e & 63);
             float q[CS];
             uint32_t w[SW];
-            lds_vec<CS>(qs + il * CS, q);
+            lds_row(qs, il, q);
             lds_slots<CS>(ss + il * CS, w);
 #pragma unroll
             for (int u = 0; u < CS; ++u) sq[u] += q[u];
             float d[CS];
-            lds_vec<CS>(ds + il * CS, d);
+            lds_row(ds, il, d);
 #pragma unroll
             for (int u = 0; u < CS; ++u) sd[u] += ((w[u >> 2] >> (8 * (u & 3))) & 0xffu) == slot ? d[u] : 0.f;
         };
@@ -836,8 +859,8 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
         }
         const float deg = (float)(end - beg);
         float qn[CS], dn[CS];
-        lds_vec<CS>(qs + n * CS, qn);
-        lds_vec<CS>(ds + n * CS, dn);
+        lds_row(qs, n, qn);
+        lds_row(ds, n, dn);
         float dp[CS], dq[CS];
 #pragma unroll
         for (int u = 0; u < CS; ++u) {
