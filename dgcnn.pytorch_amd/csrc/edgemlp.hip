@@ -277,8 +277,9 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_bwd_kernel(
 // per wave (the loop is latency-bound otherwise); the combination order is
 // fixed, so the result is deterministic.
 constexpr int EM_U = 8;
+template <typename GT>
 __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
-    const float* __restrict__ g, const float* __restrict__ PQ, int ldpq, const float* __restrict__ sumP,
+    const GT* __restrict__ g, const float* __restrict__ PQ, int ldpq, const float* __restrict__ sumP,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges, int64_t M, int k, int C1,
     const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
     float* __restrict__ dPQ) {
@@ -289,16 +290,16 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
     const float kf = (float)k, deg = (float)(end - beg);
     for (int c = lane; c < C1; c += 64) {
         const float a = scale[c], k0 = c0[c], k1 = c1[c];
-        const float* __restrict__ gp = g + p * k * C1 + c;
+        const GT* __restrict__ gp = g + p * k * C1 + c;
         float sgv[EM_U];
 #pragma unroll
         for (int u = 0; u < EM_U; ++u) sgv[u] = 0.f;
         int s = 0;
         for (; s + EM_U <= k; s += EM_U) {
 #pragma unroll
-            for (int u = 0; u < EM_U; ++u) sgv[u] += gp[(int64_t)(s + u) * C1];
+            for (int u = 0; u < EM_U; ++u) sgv[u] += (float)gp[(int64_t)(s + u) * C1];
         }
-        for (; s < k; ++s) sgv[0] += gp[(int64_t)s * C1];
+        for (; s < k; ++s) sgv[0] += (float)gp[(int64_t)s * C1];
         float igv[EM_U], iqv[EM_U];
 #pragma unroll
         for (int u = 0; u < EM_U; ++u) { igv[u] = 0.f; iqv[u] = 0.f; }
@@ -310,14 +311,14 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
 #pragma unroll
             for (int u = 0; u < EM_U; ++u) {
                 const int64_t src = (int64_t)(id[u] >> 6);
-                igv[u] += g[(src * k + (id[u] & 63)) * C1 + c];
+                igv[u] += (float)g[(src * k + (id[u] & 63)) * C1 + c];
                 iqv[u] += PQ[src * ldpq + C1 + c];
             }
         }
         for (; r < end; ++r) {
             const int32_t id = edges[r];
             const int64_t src = (int64_t)(id >> 6);
-            igv[0] += g[(src * k + (id & 63)) * C1 + c];
+            igv[0] += (float)g[(src * k + (id & 63)) * C1 + c];
             iqv[0] += PQ[src * ldpq + C1 + c];
         }
         float sg = 0.f, ig = 0.f, iq = 0.f;
@@ -639,17 +640,23 @@ int dgx_edge_mlp_h1_bwd_f32(float* dH, const float* PQ, int ldpq, const int32_t*
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const float* sumP, const int32_t* rowptr,
-                             const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
-                             const float* c1, float* dPQ, void* stream) {
+int dgx_edge_mlp_scatter_f32(const void* g, int g_bf16, const float* PQ, int ldpq, const float* sumP,
+                             const int32_t* rowptr, const int32_t* edges, int B, int N, int k, int C1,
+                             const float* scale, const float* c0, const float* c1, float* dPQ, void* stream) {
     if (!g || !PQ || !sumP || !rowptr || !edges || !scale || !c0 || !c1 || !dPQ || B < 1 || N < 1 || k < 1 ||
         k > 64 || C1 < 1 || ldpq < 2 * C1)
         return DGX_EINVAL;
     const int64_t M = (int64_t)B * N;
     const int64_t blocks = (M + EM_THREADS / 64 - 1) / (EM_THREADS / 64);
     if (blocks > 0x7fffffff) return DGX_EUNSUPPORTED;
-    hipLaunchKernelGGL(mlp_h1_scatter_kernel, dim3((unsigned)blocks), dim3(EM_THREADS), 0, dgx_stream(stream), g, PQ,
-                       ldpq, sumP, rowptr, edges, M, k, C1, scale, c0, c1, dPQ);
+    if (g_bf16)
+        hipLaunchKernelGGL(mlp_h1_scatter_kernel<__bf16>, dim3((unsigned)blocks), dim3(EM_THREADS), 0,
+                           dgx_stream(stream), static_cast<const __bf16*>(g), PQ, ldpq, sumP, rowptr, edges, M, k, C1,
+                           scale, c0, c1, dPQ);
+    else
+        hipLaunchKernelGGL(mlp_h1_scatter_kernel<float>, dim3((unsigned)blocks), dim3(EM_THREADS), 0,
+                           dgx_stream(stream), static_cast<const float*>(g), PQ, ldpq, sumP, rowptr, edges, M, k, C1,
+                           scale, c0, c1, dPQ);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

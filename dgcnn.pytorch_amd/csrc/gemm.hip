@@ -36,7 +36,19 @@ constexpr int GB_BM = 128;
 constexpr int GB_BK = 32;
 constexpr int GB_LDK = GB_BK + 8;  // bf16 per LDS row (80 B)
 
-enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4, EPI_DZ2 = 5 };
+enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4, EPI_DZ2 = 5, EPI_H1BWD = 6 };
+
+// Extra operands of the PositionEmbedding edge-MLP epilogues (EPI_H1BWD):
+// g = dH1 * LReLU'(z1) with z1 = a1 (P_j + Q_i) + b1 for edge row e = i*k + s,
+// j = idx[e] (local), plus the BN1-backward column partials (sum g, sum g*yhat).
+struct EpiEdge {
+    const float* PQ;
+    int ldpq;
+    const int32_t* idx;
+    int N, k;
+    const float *scale, *shift, *mean, *invstd;
+    float slope;
+};
 
 template <typename T> struct VecOf;
 template <> struct VecOf<float> { static constexpr int V = 4; typedef float4 type; };
@@ -385,7 +397,7 @@ template <bool TN, int BM, int BN, int EPI>
 __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
     int kchunk, int ka, float* __restrict__ C, int64_t ldc, float* __restrict__ part, const float* __restrict__ addend,
-    int64_t ldd, const uint8_t* __restrict__ aux8 = nullptr) {
+    int64_t ldd, const uint8_t* __restrict__ aux8 = nullptr, EpiEdge ex = EpiEdge{}) {
     static_assert(BM == G2_BM || (EPI != EPI_STATS && EPI != EPI_STATS16), "stats rows are per 128-row tile");
     constexpr int WN = BN >= 128 ? 2 : 1;
     constexpr int WM = 4 / WN;
@@ -523,7 +535,7 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     constexpr int NR = BM * LDT * 4 <= LDSB ? 1 : 2;
     constexpr int RR = BM / NR;
     static_assert(RR * LDT * 4 <= LDSB && WM % NR == 0, "epilogue tile must fit the stage buffers");
-    constexpr int VO = (EPI == EPI_STATS16 || EPI == EPI_DZ2) ? 8 : 4;  // outputs per 16-byte store
+    constexpr int VO = (EPI == EPI_STATS16 || EPI == EPI_DZ2 || EPI == EPI_H1BWD) ? 8 : 4;  // outputs per 16-B store
     constexpr int CPR = BN / VO;
     float* tile = reinterpret_cast<float*>(lds);
     const bool vec_out = (ldc % VO) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
@@ -557,6 +569,79 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
                     for (int b = 0; b < TN_; ++b)
                         tile[(wm * TM * 16 - q * RR + a * 16 + (lane >> 4) * 4 + r) * LDT + wn * TN_ * 16 + b * 16 +
                              (lane & 15)] = acc[a][b][r];
+        }
+        if constexpr (EPI == EPI_H1BWD) {
+            // g = dH1 * LReLU'(a1 (P_j + Q_i) + b1) stored bf16 + BN1-backward column
+            // partials; the rows' ids, P_j and Q_i pieces are loaded for all of this
+            // round's iterations before the tile is ready (latency overlap)
+            constexpr int IT = RR * CPR / GB_THREADS;
+            static_assert(RR * CPR % GB_THREADS == 0 && GB_THREADS % CPR == 0, "whole iterations, fixed columns");
+            const int jc = min(j0 + (tid % CPR) * VO, N - 8);
+            float pv[IT][8], qv[IT][8];
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int e = tid + it * GB_THREADS;
+                const int rr = e / CPR;
+                const int64_t row = min((int64_t)(i0 + q * RR + rr), (int64_t)M - 1);
+                const int64_t pi = row / ex.k;
+                const int64_t pj = (pi / ex.N) * ex.N + ex.idx[row];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    *reinterpret_cast<float4*>(pv[it] + 4 * h) =
+                        *reinterpret_cast<const float4*>(ex.PQ + pj * ex.ldpq + jc + 4 * h);
+                    *reinterpret_cast<float4*>(qv[it] + 4 * h) =
+                        *reinterpret_cast<const float4*>(ex.PQ + pi * ex.ldpq + N + jc + 4 * h);
+                }
+            }
+            float ea[8], eb[8], em[8], ei[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                *reinterpret_cast<float4*>(ea + 4 * h) = *reinterpret_cast<const float4*>(ex.scale + jc + 4 * h);
+                *reinterpret_cast<float4*>(eb + 4 * h) = *reinterpret_cast<const float4*>(ex.shift + jc + 4 * h);
+                *reinterpret_cast<float4*>(em + 4 * h) = *reinterpret_cast<const float4*>(ex.mean + jc + 4 * h);
+                *reinterpret_cast<float4*>(ei + 4 * h) = *reinterpret_cast<const float4*>(ex.invstd + jc + 4 * h);
+            }
+            __syncthreads();
+            float t1[8], t2[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { t1[u] = 0.f; t2[u] = 0.f; }
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int e = tid + it * GB_THREADS;
+                const int rr = e / CPR, c = (e - rr * CPR) * VO;
+                const int64_t i = i0 + q * RR + rr;
+                const int j = j0 + c;
+                if (i >= M || j + 8 > N) continue;
+                const float* src = tile + rr * LDT + c;
+                bf16x8 h;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float y = pv[it][u] + qv[it][u];
+                    const float z = fmaf(ea[u], y, eb[u]);
+                    const float g = src[u] * (z > 0.f ? 1.f : ex.slope);
+                    t1[u] += g;
+                    t2[u] = fmaf(g, (y - em[u]) * ei[u], t2[u]);
+                    h[u] = (bf16)g;
+                }
+                *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(out) + i * ldc + j) = h;
+            }
+            // column partials: the GB_THREADS / CPR threads of each column group
+            __syncthreads();
+            float* red = tile;  // [GB_THREADS][16]
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                red[tid * 16 + u] = t1[u];
+                red[tid * 16 + 8 + u] = t2[u];
+            }
+            __syncthreads();
+            for (int o = tid; o < 2 * BN; o += GB_THREADS) {
+                const int which = o / BN, col = o - which * BN;  // col within the tile
+                const int grp = col / VO, u = col - grp * VO;
+                float acc_s = 0.f;
+                for (int r = grp; r < GB_THREADS; r += CPR) acc_s += red[r * 16 + which * 8 + u];
+                if (j0 + col < N) part[((int64_t)ti * 2 + which) * N + j0 + col] = acc_s;
+            }
+            continue;
         }
         if constexpr (EPI == EPI_DZ2) {
             // the rows' dz / slot pieces are loaded for all of this round's
@@ -1158,6 +1243,27 @@ int dgx_gemm_dz2_bf16(const void* H1, const void* W2, int M, int N, int K, const
                            0, st, a, (int64_t)K, b, (int64_t)K, M, N, K, K, K, out, (int64_t)N, const_cast<float*>(consts),
                            dz, (int64_t)k, arg);
     }
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_gemm_h1bwd_rows(int M) { return M < 1 ? DGX_EINVAL : (M + G2_BM - 1) / G2_BM; }
+
+int dgx_gemm_h1bwd_bf16(const void* dZ2, const void* W2t, int M, int N, int K, const float* PQ, int ldpq,
+                        const int32_t* idx, int Np, int k, const float* scale, const float* shift, const float* mean,
+                        const float* invstd, float slope, void* g, float* partials, int nrows, void* stream) {
+    if (!dZ2 || !W2t || !PQ || !idx || !scale || !shift || !mean || !invstd || !g || !partials) return DGX_EINVAL;
+    if (M < 1 || N < 1 || K < 1 || Np < 1 || k < 1 || M % k || ldpq < 2 * N) return DGX_EINVAL;
+    if (nrows != (M + G2_BM - 1) / G2_BM) return DGX_EINVAL;
+    if (N != 64 || K % G2_BK || ldpq % 4 || !aligned_to(dZ2, 16) || !aligned_to(W2t, 16) || !aligned_to(PQ, 16) ||
+        !aligned_to(g, 16) || !aligned_to(scale, 16) || !aligned_to(shift, 16) || !aligned_to(mean, 16) ||
+        !aligned_to(invstd, 16))
+        return DGX_EUNSUPPORTED;
+    EpiEdge ex{PQ, ldpq, idx, Np, k, scale, shift, mean, invstd, slope};
+    const int nI = (M + G2_BM - 1) / G2_BM;
+    hipLaunchKernelGGL((gemm_lds_kernel<false, G2_BM, 64, EPI_H1BWD>), dim3((unsigned)nI), dim3(GB_THREADS), 0,
+                       dgx_stream(stream), static_cast<const bf16*>(dZ2), (int64_t)K, static_cast<const bf16*>(W2t),
+                       (int64_t)K, M, N, K, K, K, static_cast<float*>(g), (int64_t)N, partials, nullptr, (int64_t)0,
+                       nullptr, ex);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

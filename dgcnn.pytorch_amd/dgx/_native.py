@@ -76,7 +76,11 @@ _SIGS = {
     "dgx_edge_mlp_h1_bwd_rows": [_i32, _i32, _i32, _i32],
     "dgx_edge_mlp_h1_bwd_f32": [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _i32,
                                 _vp],
-    "dgx_edge_mlp_scatter_f32": [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],
+    "dgx_edge_mlp_scatter_f32": [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
+                                 _vp],
+    "dgx_gemm_h1bwd_rows": [_i32],
+    "dgx_gemm_h1bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp,
+                            _vp, _i32, _vp],
     "dgx_hog_1x1_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_edge_mlp_fused_rows": [_i32, _i32],
     "dgx_gemm_dz2_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp],

@@ -52,6 +52,24 @@ def _vec(co, dev):
     return torch.empty(co, dtype=torch.float32, device=dev)
 
 
+def _compact(partials, rows, co, stream):
+    """Pre-reduce a tall (rows, 2, co) partial array (the per-tile partials of
+    the edge-MLP epilogues reach E/128 rows) to about 128 rows with the
+    fixed-order slab sum, so the finalize kernels read few rows (deterministic:
+    the grouping depends only on rows)."""
+    if rows <= 1024:
+        return partials, rows
+    R = 128
+    S = rows // R
+    left = rows - S * R
+    out = torch.empty((R + left, 2, co), dtype=torch.float32, device=partials.device)
+    nat.check(nat.lib().dgx_slab_reduce_f32(nat.f32(partials), S, R, 2 * co, R, nat.f32(out), 2 * co, stream),
+              "bn partial reduce")
+    if left:
+        out[R:].copy_(partials.view(-1, 2, co)[S * R:rows])
+    return out, R + left
+
+
 def batch_stats(partials, rows, count, bn, gamma, beta, stream):
     """Finalize batch statistics from per-block (sum y, sum y^2) partials
     (rows, 2, Co) over ``count`` elements; updates running statistics as
@@ -65,6 +83,7 @@ def batch_stats(partials, rows, count, bn, gamma, beta, stream):
     rm = nat.f32(bn.running_mean) if update else None
     rv = nat.f32(bn.running_var) if update else None
     sync, group = dist_.sync_group(bn)
+    partials, rows = _compact(partials, rows, co, stream)
     if sync:  # SyncBatchNorm: statistics of the global batch, one fp64 all-reduce
         sums, gcount = dist_.allreduce_sums(partials, count, group)
         nat.check(L.dgx_bn_finalize_f64(nat.ptr(sums, nat.F64), 1, co, gcount, nat.f32(gamma), nat.f32(beta), rm, rv,
@@ -102,6 +121,7 @@ def backward_consts(partials, rows, count, st, stream):
     co = st.scale.shape[0]
     dgamma, dbeta, c0, c1 = _vec(co, dev), _vec(co, dev), _vec(co, dev), _vec(co, dev)
     args = (nat.f32(st.scale), nat.f32(st.mean), nat.f32(st.invstd))
+    partials, rows = _compact(partials, rows, co, stream)
     if st.group is None:
         nat.check(L.dgx_bn_bwd_finalize_f32(nat.f32(partials), rows, co, float(count), *args, nat.f32(dgamma),
                                             nat.f32(dbeta), nat.f32(c0), nat.f32(c1), 0, stream), "bn bwd finalize")

@@ -167,31 +167,46 @@ class _EdgeMLP2(torch.autograd.Function):
                 nat.check(L.dgx_edge_mlp_dz_f32(nat.f32(dz), nat.u8(arg), nat.ptr(Z2, nat.F32, nat.BF16), int(z16), B, N,
                                                 k, C2, nat.f32(st2.scale), nat.f32(c0), nat.f32(c1),
                                                 nat.ptr(dZ2, nat.F32, nat.BF16), stream), "edge dz2")
-            # ---- conv2 GEMMs: dH1 = dZ2 W2, dW2 = dZ2^T H1
+            # ---- conv2 GEMMs: dH1 = dZ2 W2, dW2 = dZ2^T H1; then LReLU + BN1 backward
             gw2 = torch.empty((C2, C1), dtype=torch.float32, device=dev)
-            if ctx.wprep is not None and z16:
-                dH1 = G.lds_xwt(dZ2, ctx.wprep[1])
+            if ctx.wprep is not None and z16 and C1 == 64:
+                # dH1 never leaves the GEMM tile: its epilogue forms g = dH1 LReLU'(z1) (bf16)
+                # and the BN1-backward column partials
                 G.lds_atb(dZ2, H1, gw2)
+                rows = L.dgx_gemm_h1bwd_rows(E)
+                part1 = torch.empty((rows, 2, C1), dtype=torch.float32, device=dev)
+                gE = torch.empty((E, C1), dtype=torch.bfloat16, device=dev)
+                nat.check(L.dgx_gemm_h1bwd_bf16(
+                    nat.bf16(dZ2), nat.bf16(ctx.wprep[1]), E, C1, C2, nat.f32(PQ), 2 * C1, nat.i32(idx), N, k,
+                    nat.f32(st1.scale), nat.f32(st1.shift), nat.f32(st1.mean), nat.f32(st1.invstd), slope1,
+                    nat.bf16(gE), nat.f32(part1), rows, stream), "edge h1 bwd gemm")
+                g16 = 1
             else:
-                W2 = w2.reshape(C2, C1)
-                dH1 = prec.mm(dZ2.float(), W2)
-                gw2 = prec.mm(dZ2.float().t(), H1.float())
-            # ---- LReLU + BN1 backward (per edge), then dP / dQ over the graph
-            rows = L.dgx_edge_mlp_h1_bwd_rows(B, N, k, C1)
-            part1 = torch.empty((rows, 2, C1), dtype=torch.float32, device=dev)
-            nat.check(L.dgx_edge_mlp_h1_bwd_f32(nat.f32(dH1), nat.f32(PQ), 2 * C1, nat.i32(idx), B, N, k, C1,
-                                                nat.f32(st1.scale), nat.f32(st1.shift), nat.f32(st1.mean),
-                                                nat.f32(st1.invstd), slope1, nat.f32(part1), rows, stream),
-                      "edge h1 bwd")
+                if ctx.wprep is not None and z16:
+                    gE = G.lds_xwt(dZ2, ctx.wprep[1])
+                    G.lds_atb(dZ2, H1, gw2)
+                else:
+                    W2 = w2.reshape(C2, C1)
+                    gE = prec.mm(dZ2.float(), W2)
+                    gw2 = prec.mm(dZ2.float().t(), H1.float())
+                rows = L.dgx_edge_mlp_h1_bwd_rows(B, N, k, C1)
+                part1 = torch.empty((rows, 2, C1), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_edge_mlp_h1_bwd_f32(nat.f32(gE), nat.f32(PQ), 2 * C1, nat.i32(idx), B, N, k, C1,
+                                                    nat.f32(st1.scale), nat.f32(st1.shift), nat.f32(st1.mean),
+                                                    nat.f32(st1.invstd), slope1, nat.f32(part1), rows, stream),
+                          "edge h1 bwd")
+                g16 = 0
             dg1, db1, e0, e1 = bn_.backward_consts(part1, rows, float(E), st1, stream)
+            # ---- dP / dQ over the graph
             rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
             edges = torch.empty(E, dtype=torch.int32, device=dev)
             nat.check(L.dgx_graph_reverse(nat.i32(idx), B, N, k, nat.i32(rowptr), nat.i32(edges), stream),
                       "reverse graph")
             dPQ = torch.empty((M, 2 * C1), dtype=torch.float32, device=dev)
-            nat.check(L.dgx_edge_mlp_scatter_f32(nat.f32(dH1), nat.f32(PQ), 2 * C1, nat.f32(sumP1), nat.i32(rowptr),
-                                                 nat.i32(edges), B, N, k, C1, nat.f32(st1.scale), nat.f32(e0),
-                                                 nat.f32(e1), nat.f32(dPQ), stream), "edge h1 scatter")
+            nat.check(L.dgx_edge_mlp_scatter_f32(nat.ptr(gE, nat.F32, nat.BF16), g16, nat.f32(PQ), 2 * C1,
+                                                 nat.f32(sumP1), nat.i32(rowptr), nat.i32(edges), B, N, k, C1,
+                                                 nat.f32(st1.scale), nat.f32(e0), nat.f32(e1), nat.f32(dPQ), stream),
+                      "edge h1 scatter")
         # ---- conv1 (K = C, tiny): dW1 = [dP^T X | dQ^T X], dX = dP W1a + dQ W1b
         dx = None
         if ctx.bf16:  # the engine's GEMMs (split-K over the M rows, un-stacked in the slab sum)

@@ -331,15 +331,25 @@ int dgx_edge_mlp_fused_rows(int B, int N);
  * for edge rows e = p*k + s, z2 recomputed on the MFMA from h1 (E x C1 bf16,
  * K = C1 % 64 == 0) and W2 (C2 x C1 bf16) with the BN2 backward in the
  * epilogue; consts = [c0 | c1 | a2] (3 x C2 fp32), dz / arg (E/k x C2). */
+/* ... and the conv2 input gradient with the LReLU + BN1 backward in its
+ * epilogue: dH1 = dZ2 W2 (dZ2 E x C2 bf16, W2t = W2^T as C1 x C2 bf16) never
+ * leaves the tile; g = dH1 * LReLU'(a1 (P_j + Q_i) + b1) is stored bf16 (E x
+ * C1) and the BN1-backward column partials [nrows][2][C1] (sum g, sum g*yhat,
+ * nrows = dgx_gemm_h1bwd_rows(E)) feed dgx_bn_bwd_finalize. C1 = 64. The
+ * scatter then reads g bf16 (dgx_edge_mlp_scatter_f32, g_bf16 = 1). */
+int dgx_gemm_h1bwd_rows(int M);
+int dgx_gemm_h1bwd_bf16(const void* dZ2, const void* W2t, int M, int N, int K, const float* PQ, int ldpq,
+                        const int32_t* idx, int Np, int k, const float* scale, const float* shift, const float* mean,
+                        const float* invstd, float slope, void* g, float* partials, int nrows, void* stream);
 int dgx_gemm_dz2_bf16(const void* H1, const void* W2, int M, int N, int K, const float* dz, const uint8_t* arg,
                       const float* consts, int k, void* dZ2, void* stream);
 int dgx_edge_mlp_fused_fwd_bf16(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1, int C2,
                                 const float* scale1, const float* shift1, float slope1, const void* W2d,
                                 const float* dir2, float* ysel, uint8_t* arg, float* partials, int nrows, void* H1,
                                 void* stream);
-int dgx_edge_mlp_scatter_f32(const float* g, const float* PQ, int ldpq, const float* sumP, const int32_t* rowptr,
-                             const int32_t* edges, int B, int N, int k, int C1, const float* scale, const float* c0,
-                             const float* c1, float* dPQ, void* stream);
+int dgx_edge_mlp_scatter_f32(const void* g, int g_bf16, const float* PQ, int ldpq, const float* sumP,
+                             const int32_t* rowptr, const int32_t* edges, int B, int N, int k, int C1,
+                             const float* scale, const float* c0, const float* c1, float* dPQ, void* stream);
 
 /* ---- f1: compute_hog_1x1 on the device, replaces models/model_partseg.py:26-92
  * after the kNN call (the D2H copy, np.linalg.svd on B*N k x 3 matrices, the H2D
