@@ -173,6 +173,7 @@ __device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (ro
 // same row order: xximg[(b*ntile + s)*16 + i]. A query's own operand (the B
 // side) is read from the same image.
 constexpr int KI_TILES = 1;  // tiles per image-builder block
+constexpr int FIXP_ROWS = 64;  // flagged rows whose fix-up is split over the grid (knn_fix_kernel)
 // One pass over x per layer: the operand image, the |x|^2 image and xx itself
 // (|x_i|^2 in the reference's rounding order, sqnorm_sum on the staged row).
 template <int NSTEP>
@@ -190,7 +191,10 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
     const int s0 = (blockIdx.x - b * tgroups) * KI_TILES;
     const int t = threadIdx.x;
     const float* __restrict__ xb = x + b * sB;
-    if (blockIdx.x == 0 && t < 2) ctl[t] = 0;  // empty fix-up list for the selection that follows
+    if (blockIdx.x == 0) {  // empty fix-up list and split-row counters for the selection that follows
+        if (t < 2) ctl[t] = 0;
+        if (t < 2 * FIXP_ROWS) ctl[4 + (int64_t)B * N + t] = 0;
+    }
     for (int e = t; e < P * CP; e += 256) {
         int p, c;
         if (sN == 1) { c = e / P; p = e - c * P; }   // candidate-fastest: unit stride along n
@@ -520,115 +524,228 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
 // Exact recompute of the rows knn_kernel flagged (rank 0 = -1, rank 1 = the
 // bits of T0, the merged k-th value: at least k candidates reach T0). knn_kernel
 // appends flagged rows to a list in the workspace (ctl[0] = count, rows from
-// ctl[4]); FIX_BLOCKS blocks take its rows round-robin; for each one a block
-// recomputes all N distances (the same k-ordered fmaf chain the MFMA performs,
-// the same rounding sequence), collects the candidates >= T0 (normally k plus
-// the few the overflowing list dropped) and ranks them canonically in one
-// all-pairs pass. If more than FIX_CAP reach T0 (mass ties), wave 0 extracts
-// the top-k from all N by k rounds of a canonical arg-max instead.
+// ctl[4]). A row's recompute is every distance of its cloud (the same k-ordered
+// fmaf chain the MFMA performs, the same rounding sequence), keeping the
+// candidates >= T0 (normally k plus the few the overflowing list dropped),
+// ranked canonically in one all-pairs pass.
+//
+// Split rows (the first FIXP_ROWS of the list, normally all of them): the
+// distances of a row are computed in units of FIXP_TILES image tiles spread over
+// the grid; each unit stages its tiles from the operand image (contiguous,
+// coalesced) into LDS, one thread per candidate runs the chain from LDS, and
+// the candidates go to the row's list in the workspace; the block that finishes
+// a row's last unit ranks it. A row with more than FIXP_CAP candidates (mass
+// ties) and the rows past FIXP_ROWS take the serial path: one block recomputes
+// the row alone, and if more than FIX_CAP reach T0, wave 0 extracts the top-k
+// from all N by k rounds of a canonical arg-max.
 constexpr int FIX_MAXN = 12288;
-constexpr int FIX_CB = 16;    // channels loaded per batch (loads in flight)
+constexpr int FIX_CB = 16;    // channels loaded per batch (loads in flight), serial path
 constexpr int FIX_CAP = 1024;
+constexpr int FIXP_CAP = 256;
+constexpr int FIXP_TILES = 4;
+constexpr int FIX_BLOCKS = 256;
 
-constexpr int FIX_BLOCKS = 64;
+// ctl words: count, exit counter, 2 spare | row list (B*N) | split-row candidate
+// counters and unit counters (FIXP_ROWS each) | candidate values, ids
+inline size_t knn_ctl_words(int B, int N) {
+    return 4 + (size_t)B * N + 2 * FIXP_ROWS + 2 * (size_t)FIXP_ROWS * FIXP_CAP;
+}
+
+struct FixShared {
+    float pd[FIX_MAXN];  // serial path: the row's N values; split path: the unit's staged tiles
+    float cv[FIX_CAP];
+    int cj[FIX_CAP];
+    float xq[128];
+    int ncand;
+    int last;
+};
+
+// Rank n candidates (cv, cj in LDS) canonically; ranks < k are the row's output.
+__device__ __forceinline__ void fix_rank_write(FixShared& sh, int n, int64_t row, int k, int64_t* idx64,
+                                               int32_t* idx32, float* vals) {
+    for (int t = threadIdx.x; t < n; t += 256) {
+        const float v = sh.cv[t];
+        const int j = sh.cj[t];
+        int rank = 0;
+        for (int u = 0; u < n; ++u) rank += canon_better(sh.cv[u], sh.cj[u], v, j) ? 1 : 0;
+        if (rank < k) {
+            if (idx64) idx64[row * k + rank] = j;
+            if (idx32) idx32[row * k + rank] = j;
+            if (vals) vals[row * k + rank] = v;
+        }
+    }
+}
+
+// T0 of a flagged row: the bits knn_kernel left at rank 1.
+__device__ __forceinline__ float fix_t0(int64_t row, int k, const int64_t* idx64, const int32_t* idx32) {
+    if (k <= 1) return -INFINITY;
+    return __int_as_float(idx64 ? (int)idx64[row * k + 1] : idx32[row * k + 1]);
+}
+
+// One block recomputes row `row` alone (block-uniform call).
+__device__ void fix_row_serial(FixShared& sh, int64_t row, const float* __restrict__ x, int64_t sB, int64_t sC,
+                               int64_t sN, const float* __restrict__ xx, int C, int N, int k,
+                               int64_t* __restrict__ idx64, int32_t* __restrict__ idx32, float* __restrict__ vals) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = (int)(row / N), q = (int)(row - (int64_t)b * N);
+    const float* __restrict__ xb = x + b * sB;
+    const float* __restrict__ xxb = xx + (int64_t)b * N;
+    const float t0 = fix_t0(row, k, idx64, idx32);
+    if (tid < C) sh.xq[tid] = xb[tid * sC + q * sN];
+    if (tid == 0) sh.ncand = 0;
+    __syncthreads();
+    const float xxq = xxb[q];
+    auto keep = [&](int j, float v) {
+        sh.pd[j] = v;
+        if (v >= t0) {
+            const int s = atomicAdd(&sh.ncand, 1);
+            if (s < FIX_CAP) { sh.cv[s] = v; sh.cj[s] = j; }
+        }
+    };
+    for (int j0 = tid; j0 < N; j0 += 512) {
+        const int ja = j0, jb = j0 + 256;
+        float da = 0.f, db = 0.f;
+        for (int c0 = 0; c0 < C; c0 += FIX_CB) {
+            float va[FIX_CB], vb[FIX_CB];
+#pragma unroll
+            for (int u = 0; u < FIX_CB; ++u) {
+                const int c = c0 + u;
+                va[u] = c < C ? xb[c * sC + ja * sN] : 0.f;
+                vb[u] = (c < C && jb < N) ? xb[c * sC + jb * sN] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < FIX_CB; ++u) {
+                if (c0 + u < C) {
+                    da = fmaf(va[u], sh.xq[c0 + u], da);
+                    db = fmaf(vb[u], sh.xq[c0 + u], db);
+                }
+            }
+        }
+        const float ta = 2.0f * da, tb = 2.0f * db;
+        const float ua = ta - xxb[ja];
+        keep(ja, ua - xxq);
+        if (jb < N) {
+            const float ub = tb - xxb[jb];
+            keep(jb, ub - xxq);
+        }
+    }
+    __syncthreads();
+    const int n = sh.ncand;
+    if (n <= FIX_CAP) {
+        fix_rank_write(sh, n, row, k, idx64, idx32, vals);
+    } else if (wave == 0) {
+        for (int r = 0; r < k; ++r) {
+            float bv = -INFINITY;
+            int bj = 0x7fffffff;
+            for (int j = lane; j < N; j += 64)
+                if (canon_better(sh.pd[j], j, bv, bj)) { bv = sh.pd[j]; bj = j; }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const float pv = __shfl_xor(bv, o);
+                const int pj = __shfl_xor(bj, o);
+                if (canon_better(pv, pj, bv, bj)) { bv = pv; bj = pj; }
+            }
+            if (lane == 0) {
+                sh.pd[bj] = -INFINITY;  // taken: finite candidates always outrank it
+                if (idx64) idx64[row * k + r] = bj;
+                if (idx32) idx32[row * k + r] = bj;
+                if (vals) vals[row * k + r] = bv;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    __syncthreads();
+}
 
 __global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
-                                                      int64_t sN, const float* __restrict__ xx, int B, int C,
+                                                      int64_t sN, const float* __restrict__ xx,
+                                                      const float* __restrict__ img, int nstep, int B, int C,
                                                       int N, int k, int64_t* __restrict__ idx64,
                                                       int32_t* __restrict__ idx32, float* __restrict__ vals,
                                                       int* __restrict__ ctl) {
 #pragma clang fp contract(off)
-    __shared__ float pd[FIX_MAXN];
-    __shared__ float cv[FIX_CAP];
-    __shared__ int cj[FIX_CAP];
-    __shared__ float xq[128];
-    __shared__ int ncand;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ FixShared sh;
+    const int tid = threadIdx.x;
     const int nr = ctl[0];  // rows knn_kernel appended to the list
     // Nothing flagged (the common case): no block touches the list or the
     // exit counter, so there is nothing to reset and no device-scope fence.
     // Uniform: the list is only reset after every block has read it.
     if (nr == 0) return;
-    for (int i = blockIdx.x; i < nr; i += gridDim.x) {
-        const int64_t row = ctl[4 + i];
+    const int ntile = (N + 15) / 16;
+    const int np = min(nr, FIXP_ROWS);
+    const int nch = (ntile + FIXP_TILES - 1) / FIXP_TILES;
+    const int units = np * nch;
+    int* cnt = ctl + 4 + (int64_t)B * N;
+    int* fin = cnt + FIXP_ROWS;
+    float* candv = reinterpret_cast<float*>(fin + FIXP_ROWS);
+    int* candj = reinterpret_cast<int*>(candv + FIXP_ROWS * FIXP_CAP);
+    const int NS1 = nstep + 1;  // padded LDS row: candidates of a tile hit distinct banks
+    for (int u = blockIdx.x; u < units + (nr - np); u += gridDim.x) {
+        if (u >= units) {
+            fix_row_serial(sh, ctl[4 + np + (u - units)], x, sB, sC, sN, xx, C, N, k, idx64, idx32, vals);
+            continue;
+        }
+        const int r = u / nch, ch = u - r * nch;
+        const int64_t row = ctl[4 + r];
         const int b = (int)(row / N), q = (int)(row - (int64_t)b * N);
-        const float* __restrict__ xb = x + b * sB;
-        const float* __restrict__ xxb = xx + (int64_t)b * N;
-        float t0 = -INFINITY;
-        if (k > 1) t0 = __int_as_float(idx64 ? (int)idx64[row * k + 1] : idx32[row * k + 1]);
-        if (tid < C) xq[tid] = xb[tid * sC + q * sN];
-        if (tid == 0) ncand = 0;
+        const float t0 = fix_t0(row, k, idx64, idx32);
+        const float* __restrict__ ib = img + (int64_t)b * ntile * 64 * nstep;
+        const int s0 = ch * FIXP_TILES, nt = min(FIXP_TILES, ntile - s0);
+        if (tid < C) {  // the query's channels from its own tile
+            const int sq = q >> 4, iq = knn_row(q & 15);
+            sh.xq[tid] = ib[((int64_t)sq * 64 + 16 * (tid & 3) + iq) * nstep + (tid >> 2)];
+        }
+        // stage the unit's tiles: nt * 64 * nstep contiguous floats
+        const float* __restrict__ src = ib + (int64_t)s0 * 64 * nstep;
+        for (int e = tid; e < nt * 64 * nstep; e += 256) {
+            const int l = e / nstep, t = e - l * nstep;
+            sh.pd[l * NS1 + t + (l >> 6) * 16] = src[e];  // + tile skew: the 4 tiles' rows on distinct banks
+        }
         __syncthreads();
-        const float xxq = xxb[q];
-        auto keep = [&](int j, float v) {
-            pd[j] = v;
-            if (v >= t0) {
-                const int s = atomicAdd(&ncand, 1);
-                if (s < FIX_CAP) { cv[s] = v; cj[s] = j; }
-            }
-        };
-        for (int j0 = tid; j0 < N; j0 += 512) {
-            const int ja = j0, jb = j0 + 256;
-            float da = 0.f, db = 0.f;
-            for (int c0 = 0; c0 < C; c0 += FIX_CB) {
-                float va[FIX_CB], vb[FIX_CB];
-#pragma unroll
-                for (int u = 0; u < FIX_CB; ++u) {
-                    const int c = c0 + u;
-                    va[u] = c < C ? xb[c * sC + ja * sN] : 0.f;
-                    vb[u] = (c < C && jb < N) ? xb[c * sC + jb * sN] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < FIX_CB; ++u) {
-                    if (c0 + u < C) {
-                        da = fmaf(va[u], xq[c0 + u], da);
-                        db = fmaf(vb[u], xq[c0 + u], db);
+        if (tid < nt * 16) {  // one thread per candidate j = 16 (s0 + sl) + p
+            const int sl = tid >> 4, p = tid & 15, i = knn_row(p);
+            const int j = 16 * (s0 + sl) + p;
+            if (j < N) {
+                const float* xs = sh.pd + (sl * 64 + i) * NS1 + sl * 16;
+                float d = 0.f;
+                for (int c = 0; c < C; ++c) d = fmaf(xs[16 * (c & 3) * NS1 + (c >> 2)], sh.xq[c], d);
+                const float* __restrict__ xxb = xx + (int64_t)b * N;
+                const float v = (2.0f * d - xxb[j]) - xxb[q];
+                if (v >= t0) {
+                    const int s = atomicAdd(&cnt[r], 1);
+                    if (s < FIXP_CAP) {
+                        candv[r * FIXP_CAP + s] = v;
+                        candj[r * FIXP_CAP + s] = j;
                     }
                 }
             }
-            const float ta = 2.0f * da, tb = 2.0f * db;
-            const float ua = ta - xxb[ja];
-            keep(ja, ua - xxq);
-            if (jb < N) {
-                const float ub = tb - xxb[jb];
-                keep(jb, ub - xxq);
-            }
+        }
+        __threadfence();  // release this unit's candidates (each storing thread)
+        __syncthreads();
+        if (tid == 0) {
+            sh.last = atomicAdd(&fin[r], 1) == nch - 1;
         }
         __syncthreads();
-        const int n = ncand;
-        if (n <= FIX_CAP) {
-            for (int t = tid; t < n; t += 256) {
-                const float v = cv[t];
-                const int j = cj[t];
-                int rank = 0;
-                for (int u = 0; u < n; ++u) rank += canon_better(cv[u], cj[u], v, j) ? 1 : 0;
-                if (rank < k) {
-                    if (idx64) idx64[row * k + rank] = j;
-                    if (idx32) idx32[row * k + rank] = j;
-                    if (vals) vals[row * k + rank] = v;
+        if (sh.last) {  // every unit of row r is in: rank it
+            __threadfence();  // acquire the other units' candidates
+            const int n = __hip_atomic_load(&cnt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (n <= FIXP_CAP) {
+                for (int t = tid; t < n; t += 256) {
+                    sh.cv[t] = __hip_atomic_load(&candv[r * FIXP_CAP + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    sh.cj[t] = __hip_atomic_load(&candj[r * FIXP_CAP + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
+                __syncthreads();
+                fix_rank_write(sh, n, row, k, idx64, idx32, vals);
+                __syncthreads();
+            } else {
+                fix_row_serial(sh, row, x, sB, sC, sN, xx, C, N, k, idx64, idx32, vals);
             }
-        } else if (wave == 0) {
-            for (int r = 0; r < k; ++r) {
-                float bv = -INFINITY;
-                int bj = 0x7fffffff;
-                for (int j = lane; j < N; j += 64)
-                    if (canon_better(pd[j], j, bv, bj)) { bv = pd[j]; bj = j; }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const float pv = __shfl_xor(bv, o);
-                    const int pj = __shfl_xor(bj, o);
-                    if (canon_better(pv, pj, bv, bj)) { bv = pv; bj = pj; }
-                }
-                if (lane == 0) {
-                    pd[bj] = -INFINITY;  // taken: finite candidates always outrank it
-                    if (idx64) idx64[row * k + r] = bj;
-                    if (idx32) idx32[row * k + r] = bj;
-                    if (vals) vals[row * k + r] = bv;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (tid == 0) {  // the row's counters are clean for the next selection
+                cnt[r] = 0;
+                fin[r] = 0;
             }
         }
         __syncthreads();
@@ -667,8 +784,8 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
                        xximg, xx, B, N, k, nqb, idx64, idx32, vals, ctl);
     if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH;
-    hipLaunchKernelGGL(knn_fix_kernel, dim3(FIX_BLOCKS), dim3(256), 0, st, x, sB, sC, sN, xx, B, C, N, k, idx64,
-                       idx32, vals, ctl);
+    hipLaunchKernelGGL(knn_fix_kernel, dim3(FIX_BLOCKS), dim3(256), 0, st, x, sB, sC, sN, xx, img, NSTEP, B, C, N,
+                       k, idx64, idx32, vals, ctl);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -722,7 +839,7 @@ int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
 size_t dgx_knn_image_bytes(int B, int C, int N) {
     if (B < 0 || C < 1 || N < 1) return 0;
     // operand image | |x|^2 image | fix-up control words + row list
-    return ((size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) + 4 + (size_t)B * N) * sizeof(float);
+    return ((size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) + knn_ctl_words(B, N)) * sizeof(float);
 }
 
 size_t dgx_knn_workspace_bytes(int B, int C, int N) {

@@ -125,10 +125,12 @@ def test_knn_list_overflow_fixup(cuda, C, N, k):
         np.testing.assert_array_equal(vals.cpu().numpy(), ref_vals)
 
 
-def test_knn_all_points_equal(cuda):
-    """Every distance ties: the canonical answer is indices 0..k-1 for every row."""
+@pytest.mark.parametrize("N", [300, 2048])
+def test_knn_all_points_equal(cuda, N):
+    """Every distance ties: the canonical answer is indices 0..k-1 for every row
+    (N = 2048: more than FIX_CAP candidates reach T0, the arg-max path)."""
     from models.dgcnn import knn
-    pts = np.full((2, 300, 3), 0.25, np.float32)
+    pts = np.full((2, N, 3), 0.25, np.float32)
     idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
     np.testing.assert_array_equal(idx, oracle.knn(_cpu_view(pts, "perm"), 20))
     np.testing.assert_array_equal(idx[0, 7], np.arange(20))
