@@ -82,6 +82,12 @@ _SIGS = {
     "dgx_gemm_h1bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp,
                             _vp, _i32, _vp],
     "dgx_hog_1x1_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    "dgx_attn_fwd": [_i32] + [_vp, _i64, _i64, _i64] * 4 + [_vp, _i32, _i32, _i32, _i32, _i32, _f32, _f32,
+                                                             ctypes.c_uint64, _vp],
+    "dgx_attn_bwd": [_i32] + [_vp, _i64, _i64, _i64] * 3 + [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _i32, _i32,
+                                                           _i32, _i32, _f32, _f32, ctypes.c_uint64]
+                    + [_vp, _i64, _i64, _i64] * 3 + [_vp],
+    "dgx_attn_dropout_mask": [_i64, _i32, _f32, ctypes.c_uint64, _vp, _vp],
     "dgx_edge_mlp_fused_rows": [_i32, _i32],
     "dgx_gemm_dz2_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp],
     "dgx_edge_mlp_fused_fwd_bf16": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp,
@@ -137,8 +143,8 @@ def ptr(t, *dtypes):
     return ctypes.c_void_p(t.data_ptr())
 
 
-F32, BF16, I32, I64, U8, F64 = (torch.float32, torch.bfloat16, torch.int32, torch.int64, torch.uint8,
-                               torch.float64)
+F32, BF16, I32, I64, U8, F64, F16 = (torch.float32, torch.bfloat16, torch.int32, torch.int64, torch.uint8,
+                                    torch.float64, torch.float16)
 
 
 def f32(t):
