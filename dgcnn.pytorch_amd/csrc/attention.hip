@@ -4,7 +4,10 @@
 // its backward, without materialising the (B, H, Nq, Nk) score matrix.
 //
 // Operands are 16-bit (fp16 or bf16: v_mfma_f32_16x16x32_{f16,bf16}), every sum
-// and the softmax are fp32. Layout: element (b, n, h, d) of Q/K/V/O/dO at
+// and the softmax are fp32. The fp32 mode splits each fp32 operand into two
+// bf16 planes, x = hi + lo (hi = bf16(x), lo = bf16(x - hi)), and every product
+// into hi.hi + hi.lo + lo.hi (three MFMAs; the dropped lo.lo term is ~2^-16
+// relative), P and dS likewise: ~16-bit-mantissa products for fp32 parity. Layout: element (b, n, h, d) of Q/K/V/O/dO at
 // b*sB + n*sN + h*sH + d (d contiguous) — the (B, N, E) projections of
 // nn.MultiheadAttention (batch_first) viewed as (B, N, H, D) without a copy.
 //
@@ -117,14 +120,35 @@ __device__ __forceinline__ s16x8 lds_tr8(const uint32_t* t, int r0, int c0, int 
 
 // The B operand of a product summing over the 32 rows {4g+r, 16+4g+r} of two
 // accumulator tiles (lane = column): elements 0..3 from tile a, 4..7 from b.
-template <typename T>
-__device__ __forceinline__ s16x8 pack_acc(const f32x4& a, const f32x4& b) {
-    const uint32_t w0 = Mma<T>::pack(a[0], a[1]), w1 = Mma<T>::pack(a[2], a[3]);
-    const uint32_t w2 = Mma<T>::pack(b[0], b[1]), w3 = Mma<T>::pack(b[2], b[3]);
-    return __builtin_bit_cast(s16x8, make_uint4(w0, w1, w2, w3));
+// NP = 2 (split fp32): plane 0 = bf16(x), plane 1 = bf16(x - plane 0).
+template <typename T, int NP>
+__device__ __forceinline__ void pack_acc(const f32x4& a, const f32x4& b, s16x8 (&out)[NP]) {
+    float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = Mma<T>::pack(x[2 * i], x[2 * i + 1]);
+    out[0] = __builtin_bit_cast(s16x8, make_uint4(w[0], w[1], w[2], w[3]));
+    if constexpr (NP == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float h0 = __uint_as_float(w[i] << 16), h1 = __uint_as_float(w[i] & 0xffff0000u);
+            w[i] = Mma<T>::pack(x[2 * i] - h0, x[2 * i + 1] - h1);
+        }
+        out[1] = __builtin_bit_cast(s16x8, make_uint4(w[0], w[1], w[2], w[3]));
+    }
 }
 
-// Register-staged copy of a [64][D] 16-bit tile (rows from `rows0`, row stride
+// c += a b over the planes: hi.hi (+ hi.lo + lo.hi when split; lo.lo ~ 2^-16 is dropped)
+template <typename T, int NP>
+__device__ __forceinline__ f32x4 mmp(const s16x8 (&a)[NP], const s16x8 (&b)[NP], f32x4 c) {
+    if constexpr (NP == 2) {
+        c = Mma<T>::run(a[0], b[1], c);
+        c = Mma<T>::run(a[1], b[0], c);
+    }
+    return Mma<T>::run(a[0], b[0], c);
+}
+
+// Register-staged copy of a [64][D] 16-bit tile (rows from `row0`, row stride
 // sN elements) into LDS: issue() loads into registers, commit() writes them.
 template <int D>
 struct TileStage {
@@ -160,40 +184,53 @@ __device__ __forceinline__ float wsum16(float v) {
     return v + __shfl_xor(v, 32);
 }
 
+// One operand: planes at p, p + sP; element (b, n, h, d) at b*sB + n*sN + h*sH + d.
+struct AtOp {
+    const uint16_t* p;
+    int64_t sP, sB, sN, sH;
+    __device__ __forceinline__ const uint16_t* at(int pl, int b, int h) const { return p + pl * sP + b * sB + h * sH; }
+};
+
 struct AtArgs {
-    const uint16_t *q, *k, *v, *o, *dout;
-    int64_t qsB, qsN, qsH, ksB, ksN, ksH, vsB, vsN, vsH, osB, osN, osH;
+    AtOp q, k, v, dout;                 // dout shares O's (sB, sN, sH)
+    const void* o;                      // forward output as stored (16-bit, or fp32 when split)
+    const float* dout32;                // split mode: dO in fp32 (for delta)
+    int64_t osB, osN, osH;
     float *lse, *delta;
     int H, Nq, Nk;
-    float scale_log2;   // log2(e) / sqrt(D) (or the caller's scale)
-    float scale;        // the softmax scale itself
+    float scale_log2;   // log2(e) * scale
+    float scale;        // the softmax scale
     uint32_t p32;       // dropout threshold (0: no dropout)
     float rdrop;        // 1 / (1 - p)
     uint32_t s0, s1;    // dropout seed
 };
 
+template <int D, int NP>
+constexpr int at_lds_bytes_qk() { return 2 * NP * 64 * at_rsw<D>() * 4; }
+
 // ---------------------------------------------------------------- forward --
-template <typename T, int D, bool DROP>
-__global__ __launch_bounds__(AT_THREADS, 2) void attn_fwd_kernel(AtArgs a, uint16_t* __restrict__ out) {
+template <typename T, int D, bool DROP, int NP>
+__global__ __launch_bounds__(AT_THREADS, NP == 2 ? 1 : 2) void attn_fwd_kernel(AtArgs a, void* __restrict__ out) {
     constexpr int RSW = at_rsw<D>();
-    constexpr int KS = D / 32, DB = D / 16;
-    __shared__ uint32_t kl[AT_KT * RSW];
-    __shared__ uint32_t vl[AT_KT * RSW];
+    constexpr int KS = D / 32, DB = D / 16, TW = 64 * RSW;
+    extern __shared__ __attribute__((aligned(16))) uint32_t at_lds[];
+    uint32_t* kl = at_lds;             // [NP][64][RSW]
+    uint32_t* vl = at_lds + NP * TW;   // [NP][64][RSW]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, c = lane & 15;
     const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
     const int q0 = blockIdx.x * AT_QB + wave * AT_QW;
-    const uint16_t* qb = a.q + b * a.qsB + h * a.qsH;
-    const uint16_t* kb = a.k + b * a.ksB + h * a.ksH;
-    const uint16_t* vb = a.v + b * a.vsB + h * a.vsH;
 
-    s16x8 qf[2][KS];  // B operand of Sᵀ = K Qᵀ: lane (g, c) holds Q[q0 + 16qt + c][32ks + 8g .. +7]
+    s16x8 qf[2][KS][NP];  // B operand of Sᵀ = K Qᵀ: lane (g, c) holds Q[q0 + 16qt + c][32ks + 8g .. +7]
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
         const int q = min(q0 + 16 * qt + c, a.Nq - 1);
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-            qf[qt][ks] = *reinterpret_cast<const s16x8*>(qb + (int64_t)q * a.qsN + 32 * ks + 8 * g);
+        for (int pl = 0; pl < NP; ++pl) {
+            const uint16_t* qp = a.q.at(pl, b, h) + (int64_t)q * a.q.sN;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) qf[qt][ks][pl] = *reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g);
+        }
     }
     f32x4 o[2][DB];
 #pragma unroll
@@ -203,17 +240,26 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_fwd_kernel(AtArgs a, uint1
     float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
     const uint32_t row0 = (uint32_t)bh * (uint32_t)a.Nq + (uint32_t)q0;
 
-    TileStage<D> ks_, vs_;
-    ks_.issue(kb, a.ksN, 0, a.Nk);
-    vs_.issue(vb, a.vsN, 0, a.Nk);
+    TileStage<D> ks_[NP], vs_[NP];
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+        ks_[pl].issue(a.k.at(pl, b, h), a.k.sN, 0, a.Nk);
+        vs_[pl].issue(a.v.at(pl, b, h), a.v.sN, 0, a.Nk);
+    }
     for (int kv0 = 0; kv0 < a.Nk; kv0 += AT_KT) {
         __syncthreads();  // the previous tile's LDS reads are done
-        ks_.commit(kl);
-        vs_.commit(vl);
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl) {
+            ks_[pl].commit(kl + pl * TW);
+            vs_[pl].commit(vl + pl * TW);
+        }
         __syncthreads();
         if (kv0 + AT_KT < a.Nk) {  // next tile in flight during this one's math
-            ks_.issue(kb, a.ksN, kv0 + AT_KT, a.Nk);
-            vs_.issue(vb, a.vsN, kv0 + AT_KT, a.Nk);
+#pragma unroll
+            for (int pl = 0; pl < NP; ++pl) {
+                ks_[pl].issue(a.k.at(pl, b, h), a.k.sN, kv0 + AT_KT, a.Nk);
+                vs_[pl].issue(a.v.at(pl, b, h), a.v.sN, kv0 + AT_KT, a.Nk);
+            }
         }
         f32x4 s[2][4];
 #pragma unroll
@@ -224,9 +270,11 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_fwd_kernel(AtArgs a, uint1
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                const s16x8 kf = lds_row8<RSW>(kl, 16 * kt + c, 32 * ks + 8 * g);
+                s16x8 kf[NP];
 #pragma unroll
-                for (int qt = 0; qt < 2; ++qt) s[qt][kt] = Mma<T>::run(kf, qf[qt][ks], s[qt][kt]);
+                for (int pl = 0; pl < NP; ++pl) kf[pl] = lds_row8<RSW>(kl + pl * TW, 16 * kt + c, 32 * ks + 8 * g);
+#pragma unroll
+                for (int qt = 0; qt < 2; ++qt) s[qt][kt] = mmp<T, NP>(kf, qf[qt][ks], s[qt][kt]);
             }
         // online softmax, lane = query 16qt + c, registers = keys 16kt + 4g + r
 #pragma unroll
@@ -266,13 +314,16 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_fwd_kernel(AtArgs a, uint1
         // Oᵀ += Vᵀ Pᵀ over two 32-key steps
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-            const s16x8 pf0 = pack_acc<T>(s[0][2 * st], s[0][2 * st + 1]);
-            const s16x8 pf1 = pack_acc<T>(s[1][2 * st], s[1][2 * st + 1]);
+            s16x8 pf0[NP], pf1[NP];
+            pack_acc<T, NP>(s[0][2 * st], s[0][2 * st + 1], pf0);
+            pack_acc<T, NP>(s[1][2 * st], s[1][2 * st + 1], pf1);
 #pragma unroll
             for (int db = 0; db < DB; ++db) {
-                const s16x8 vf = lds_tr8<RSW>(vl, 32 * st, 16 * db, lane);
-                o[0][db] = Mma<T>::run(vf, pf0, o[0][db]);
-                o[1][db] = Mma<T>::run(vf, pf1, o[1][db]);
+                s16x8 vf[NP];
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl) vf[pl] = lds_tr8<RSW>(vl + pl * TW, 32 * st, 16 * db, lane);
+                o[0][db] = mmp<T, NP>(vf, pf0, o[0][db]);
+                o[1][db] = mmp<T, NP>(vf, pf1, o[1][db]);
             }
         }
     }
@@ -282,53 +333,43 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_fwd_kernel(AtArgs a, uint1
         const int q = q0 + 16 * qt + c;
         if (q < a.Nq) {
             const float inv = (DROP ? a.rdrop : 1.f) / l[qt];
-            uint16_t* op = out + b * a.osB + h * a.osH + (int64_t)q * a.osN;
+            const int64_t off = b * a.osB + h * a.osH + (int64_t)q * a.osN;
 #pragma unroll
             for (int db = 0; db < DB; ++db) {
-                const uint32_t w0 = Mma<T>::pack(o[qt][db][0] * inv, o[qt][db][1] * inv);
-                const uint32_t w1 = Mma<T>::pack(o[qt][db][2] * inv, o[qt][db][3] * inv);
-                *reinterpret_cast<uint2*>(op + 16 * db + 4 * g) = make_uint2(w0, w1);
+                if constexpr (NP == 2) {
+                    *reinterpret_cast<float4*>(static_cast<float*>(out) + off + 16 * db + 4 * g) =
+                        make_float4(o[qt][db][0] * inv, o[qt][db][1] * inv, o[qt][db][2] * inv, o[qt][db][3] * inv);
+                } else {
+                    const uint32_t w0 = Mma<T>::pack(o[qt][db][0] * inv, o[qt][db][1] * inv);
+                    const uint32_t w1 = Mma<T>::pack(o[qt][db][2] * inv, o[qt][db][3] * inv);
+                    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(out) + off + 16 * db + 4 * g) =
+                        make_uint2(w0, w1);
+                }
             }
             if (g == 0) a.lse[(int64_t)bh * a.Nq + q] = m[qt] + __log2f(l[qt]);
         }
     }
 }
 
-// delta[row] = sum_d dO . O (fp32), one 16-lane group per row.
+// delta[row] = sum_d dO . O (fp32), one 16-lane group per row; fmt 0 f16, 1 bf16, 2 f32.
+__device__ __forceinline__ float at_load(const void* p, int64_t i, int fmt) {
+    if (fmt == 2) return static_cast<const float*>(p)[i];
+    const uint16_t u = static_cast<const uint16_t*>(p)[i];
+    return fmt == 1 ? __uint_as_float((uint32_t)u << 16) : (float)__builtin_bit_cast(_Float16, u);
+}
+
 template <int D>
-__global__ __launch_bounds__(256) void attn_delta_kernel(AtArgs a, int B, const uint16_t* __restrict__ o16,
-                                                         bool bf16) {
+__global__ __launch_bounds__(256) void attn_delta_kernel(AtArgs a, int B, int fmt) {
     const int64_t rowg = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     const int i = threadIdx.x & 15;
     const int64_t rows = (int64_t)B * a.H * a.Nq;
     float acc = 0.f;
-    int64_t bh = 0, q = 0;
     if (rowg < rows) {
-        bh = rowg / a.Nq;
-        q = rowg - bh * a.Nq;
+        const int64_t bh = rowg / a.Nq, q = rowg - bh * a.Nq;
         const int b = (int)(bh / a.H), h = (int)(bh - (int64_t)b * a.H);
-        const uint16_t* op = o16 + b * a.osB + h * a.osH + q * a.osN;
-        const uint16_t* gp = a.dout + b * a.osB + h * a.osH + q * a.osN;
-        for (int d = 8 * i; d < D; d += 128) {
-            const uint4 ov = *reinterpret_cast<const uint4*>(op + d);
-            const uint4 gv = *reinterpret_cast<const uint4*>(gp + d);
-            const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const uint16_t ob = (uint16_t)(ow[u] >> (16 * hh)), gb = (uint16_t)(gw[u] >> (16 * hh));
-                    float of, gf;
-                    if (bf16) {
-                        of = __uint_as_float((uint32_t)ob << 16);
-                        gf = __uint_as_float((uint32_t)gb << 16);
-                    } else {
-                        of = (float)__builtin_bit_cast(_Float16, ob);
-                        gf = (float)__builtin_bit_cast(_Float16, gb);
-                    }
-                    acc = fmaf(of, gf, acc);
-                }
-        }
+        const int64_t off = b * a.osB + h * a.osH + q * a.osN;
+        const void* gsrc = fmt == 2 ? static_cast<const void*>(a.dout32) : static_cast<const void*>(a.dout.p);
+        for (int d = i; d < D; d += 16) acc = fmaf(at_load(a.o, off + d, fmt), at_load(gsrc, off + d, fmt), acc);
     }
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
@@ -336,31 +377,33 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AtArgs a, int B, const 
 }
 
 // ------------------------------------------------------------- backward dQ --
-template <typename T, int D, bool DROP>
-__global__ __launch_bounds__(AT_THREADS, D == 128 ? 1 : 2) void attn_bwd_dq_kernel(AtArgs a, float* __restrict__ dq, int64_t dsB,
-                                                                    int64_t dsN, int64_t dsH) {
+template <typename T, int D, bool DROP, int NP>
+__global__ __launch_bounds__(AT_THREADS, (D == 128 || NP == 2) ? 1 : 2) void attn_bwd_dq_kernel(
+    AtArgs a, float* __restrict__ dq, int64_t dsB, int64_t dsN, int64_t dsH) {
     constexpr int RSW = at_rsw<D>();
-    constexpr int KS = D / 32, DB = D / 16;
-    __shared__ uint32_t kl[AT_KT * RSW];
-    __shared__ uint32_t vl[AT_KT * RSW];
+    constexpr int KS = D / 32, DB = D / 16, TW = 64 * RSW;
+    extern __shared__ __attribute__((aligned(16))) uint32_t at_lds[];
+    uint32_t* kl = at_lds;
+    uint32_t* vl = at_lds + NP * TW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, c = lane & 15;
     const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
     const int q0 = blockIdx.x * AT_QB + wave * AT_QW;
-    const uint16_t* qb = a.q + b * a.qsB + h * a.qsH;
-    const uint16_t* gb = a.dout + b * a.osB + h * a.osH;
-    const uint16_t* kb = a.k + b * a.ksB + h * a.ksH;
-    const uint16_t* vb = a.v + b * a.vsB + h * a.vsH;
 
-    s16x8 qf[2][KS], gf[2][KS];
+    s16x8 qf[2][KS][NP], gf[2][KS][NP];
     float lse[2], dl[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
         const int q = min(q0 + 16 * qt + c, a.Nq - 1);
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            qf[qt][ks] = *reinterpret_cast<const s16x8*>(qb + (int64_t)q * a.qsN + 32 * ks + 8 * g);
-            gf[qt][ks] = *reinterpret_cast<const s16x8*>(gb + (int64_t)q * a.osN + 32 * ks + 8 * g);
+        for (int pl = 0; pl < NP; ++pl) {
+            const uint16_t* qp = a.q.at(pl, b, h) + (int64_t)q * a.q.sN;
+            const uint16_t* gp = a.dout.at(pl, b, h) + (int64_t)q * a.osN;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                qf[qt][ks][pl] = *reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g);
+                gf[qt][ks][pl] = *reinterpret_cast<const s16x8*>(gp + 32 * ks + 8 * g);
+            }
         }
         lse[qt] = a.lse[(int64_t)bh * a.Nq + q];
         dl[qt] = a.delta[(int64_t)bh * a.Nq + q];
@@ -372,17 +415,26 @@ __global__ __launch_bounds__(AT_THREADS, D == 128 ? 1 : 2) void attn_bwd_dq_kern
         for (int db = 0; db < DB; ++db) acc[qt][db] = f32x4{0.f, 0.f, 0.f, 0.f};
     const uint32_t row0 = (uint32_t)bh * (uint32_t)a.Nq + (uint32_t)q0;
 
-    TileStage<D> ks_, vs_;
-    ks_.issue(kb, a.ksN, 0, a.Nk);
-    vs_.issue(vb, a.vsN, 0, a.Nk);
+    TileStage<D> ks_[NP], vs_[NP];
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+        ks_[pl].issue(a.k.at(pl, b, h), a.k.sN, 0, a.Nk);
+        vs_[pl].issue(a.v.at(pl, b, h), a.v.sN, 0, a.Nk);
+    }
     for (int kv0 = 0; kv0 < a.Nk; kv0 += AT_KT) {
         __syncthreads();
-        ks_.commit(kl);
-        vs_.commit(vl);
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl) {
+            ks_[pl].commit(kl + pl * TW);
+            vs_[pl].commit(vl + pl * TW);
+        }
         __syncthreads();
         if (kv0 + AT_KT < a.Nk) {
-            ks_.issue(kb, a.ksN, kv0 + AT_KT, a.Nk);
-            vs_.issue(vb, a.vsN, kv0 + AT_KT, a.Nk);
+#pragma unroll
+            for (int pl = 0; pl < NP; ++pl) {
+                ks_[pl].issue(a.k.at(pl, b, h), a.k.sN, kv0 + AT_KT, a.Nk);
+                vs_[pl].issue(a.v.at(pl, b, h), a.v.sN, kv0 + AT_KT, a.Nk);
+            }
         }
         f32x4 s[2][4], dp[2][4];
 #pragma unroll
@@ -393,12 +445,16 @@ __global__ __launch_bounds__(AT_THREADS, D == 128 ? 1 : 2) void attn_bwd_dq_kern
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                const s16x8 kf = lds_row8<RSW>(kl, 16 * kt + c, 32 * ks + 8 * g);
-                const s16x8 vf = lds_row8<RSW>(vl, 16 * kt + c, 32 * ks + 8 * g);
+                s16x8 kf[NP], vf[NP];
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl) {
+                    kf[pl] = lds_row8<RSW>(kl + pl * TW, 16 * kt + c, 32 * ks + 8 * g);
+                    vf[pl] = lds_row8<RSW>(vl + pl * TW, 16 * kt + c, 32 * ks + 8 * g);
+                }
 #pragma unroll
                 for (int qt = 0; qt < 2; ++qt) {
-                    s[qt][kt] = Mma<T>::run(kf, qf[qt][ks], s[qt][kt]);
-                    dp[qt][kt] = Mma<T>::run(vf, gf[qt][ks], dp[qt][kt]);
+                    s[qt][kt] = mmp<T, NP>(kf, qf[qt][ks], s[qt][kt]);
+                    dp[qt][kt] = mmp<T, NP>(vf, gf[qt][ks], dp[qt][kt]);
                 }
             }
         // dSᵀ = P (dP (keep / (1-p)) - delta), scaled by 2^8 for the MFMA
@@ -419,13 +475,16 @@ __global__ __launch_bounds__(AT_THREADS, D == 128 ? 1 : 2) void attn_bwd_dq_kern
         // dQᵀ += Kᵀ dSᵀ
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-            const s16x8 d0 = pack_acc<T>(s[0][2 * st], s[0][2 * st + 1]);
-            const s16x8 d1 = pack_acc<T>(s[1][2 * st], s[1][2 * st + 1]);
+            s16x8 d0[NP], d1[NP];
+            pack_acc<T, NP>(s[0][2 * st], s[0][2 * st + 1], d0);
+            pack_acc<T, NP>(s[1][2 * st], s[1][2 * st + 1], d1);
 #pragma unroll
             for (int db = 0; db < DB; ++db) {
-                const s16x8 kf = lds_tr8<RSW>(kl, 32 * st, 16 * db, lane);
-                acc[0][db] = Mma<T>::run(kf, d0, acc[0][db]);
-                acc[1][db] = Mma<T>::run(kf, d1, acc[1][db]);
+                s16x8 kf[NP];
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl) kf[pl] = lds_tr8<RSW>(kl + pl * TW, 32 * st, 16 * db, lane);
+                acc[0][db] = mmp<T, NP>(kf, d0, acc[0][db]);
+                acc[1][db] = mmp<T, NP>(kf, d1, acc[1][db]);
             }
         }
     }
@@ -444,31 +503,34 @@ __global__ __launch_bounds__(AT_THREADS, D == 128 ? 1 : 2) void attn_bwd_dq_kern
 }
 
 // ---------------------------------------------------------- backward dK, dV --
-template <typename T, int D, bool DROP>
-__global__ __launch_bounds__(AT_THREADS, 2) void attn_bwd_dkv_kernel(AtArgs a, float* __restrict__ dk, int64_t ksB,
-                                                                     int64_t ksN, int64_t ksH, float* __restrict__ dv,
-                                                                     int64_t vsB, int64_t vsN, int64_t vsH) {
+template <typename T, int D, bool DROP, int NP>
+__global__ __launch_bounds__(AT_THREADS, NP == 2 ? 1 : 2) void attn_bwd_dkv_kernel(
+    AtArgs a, float* __restrict__ dk, int64_t ksB, int64_t ksN, int64_t ksH, float* __restrict__ dv, int64_t vsB,
+    int64_t vsN, int64_t vsH) {
     constexpr int RSW = at_rsw<D>();
-    constexpr int KS = D / 32, DB = D / 16;
-    __shared__ uint32_t ql[AT_QT * RSW];
-    __shared__ uint32_t gl[AT_QT * RSW];
-    __shared__ float lsel[AT_QT], dll[AT_QT];
+    constexpr int KS = D / 32, DB = D / 16, TW = 64 * RSW;
+    extern __shared__ __attribute__((aligned(16))) uint32_t at_lds[];
+    uint32_t* ql = at_lds;              // [NP][64][RSW]
+    uint32_t* gl = at_lds + NP * TW;    // [NP][64][RSW]
+    float* lsel = reinterpret_cast<float*>(at_lds + 2 * NP * TW);
+    float* dll = lsel + AT_QT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, c = lane & 15;
     const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
     const int key = blockIdx.x * AT_KB + wave * AT_KW + c;  // this lane's key (column of S)
-    const uint16_t* qb = a.q + b * a.qsB + h * a.qsH;
-    const uint16_t* gb = a.dout + b * a.osB + h * a.osH;
 
-    s16x8 kf[KS], vf[KS];  // B operands: lane (g, c) holds K/V[key][32ks + 8g .. +7]
+    s16x8 kf[KS][NP], vf[KS][NP];  // B operands: lane (g, c) holds K/V[key][32ks + 8g .. +7]
     {
         const int kk = min(key, a.Nk - 1);
-        const uint16_t* kp = a.k + b * a.ksB + h * a.ksH + (int64_t)kk * a.ksN;
-        const uint16_t* vp = a.v + b * a.vsB + h * a.vsH + (int64_t)kk * a.vsN;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            kf[ks] = *reinterpret_cast<const s16x8*>(kp + 32 * ks + 8 * g);
-            vf[ks] = *reinterpret_cast<const s16x8*>(vp + 32 * ks + 8 * g);
+        for (int pl = 0; pl < NP; ++pl) {
+            const uint16_t* kp = a.k.at(pl, b, h) + (int64_t)kk * a.k.sN;
+            const uint16_t* vp = a.v.at(pl, b, h) + (int64_t)kk * a.v.sN;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                kf[ks][pl] = *reinterpret_cast<const s16x8*>(kp + 32 * ks + 8 * g);
+                vf[ks][pl] = *reinterpret_cast<const s16x8*>(vp + 32 * ks + 8 * g);
+            }
         }
     }
     f32x4 ak[DB], av[DB];
@@ -476,13 +538,19 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_bwd_dkv_kernel(AtArgs a, f
     for (int db = 0; db < DB; ++db) ak[db] = av[db] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bool kvalid = key < a.Nk;
 
-    TileStage<D> qs_, gs_;
-    qs_.issue(qb, a.qsN, 0, a.Nq);
-    gs_.issue(gb, a.osN, 0, a.Nq);
+    TileStage<D> qs_[NP], gs_[NP];
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+        qs_[pl].issue(a.q.at(pl, b, h), a.q.sN, 0, a.Nq);
+        gs_[pl].issue(a.dout.at(pl, b, h), a.osN, 0, a.Nq);
+    }
     for (int qv0 = 0; qv0 < a.Nq; qv0 += AT_QT) {
         __syncthreads();
-        qs_.commit(ql);
-        gs_.commit(gl);
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl) {
+            qs_[pl].commit(ql + pl * TW);
+            gs_[pl].commit(gl + pl * TW);
+        }
         if (threadIdx.x < AT_QT) {
             const int q = qv0 + threadIdx.x;
             // padded rows: P = exp2(-inf) = 0 and delta 0, so they add nothing
@@ -491,8 +559,11 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_bwd_dkv_kernel(AtArgs a, f
         }
         __syncthreads();
         if (qv0 + AT_QT < a.Nq) {
-            qs_.issue(qb, a.qsN, qv0 + AT_QT, a.Nq);
-            gs_.issue(gb, a.osN, qv0 + AT_QT, a.Nq);
+#pragma unroll
+            for (int pl = 0; pl < NP; ++pl) {
+                qs_[pl].issue(a.q.at(pl, b, h), a.q.sN, qv0 + AT_QT, a.Nq);
+                gs_[pl].issue(a.dout.at(pl, b, h), a.osN, qv0 + AT_QT, a.Nq);
+            }
         }
         f32x4 s[4], dp[4];  // [query tile]: lane = key, registers = queries 16qt + 4g + r
 #pragma unroll
@@ -501,8 +572,14 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_bwd_dkv_kernel(AtArgs a, f
         for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                s[qt] = Mma<T>::run(lds_row8<RSW>(ql, 16 * qt + c, 32 * ks + 8 * g), kf[ks], s[qt]);
-                dp[qt] = Mma<T>::run(lds_row8<RSW>(gl, 16 * qt + c, 32 * ks + 8 * g), vf[ks], dp[qt]);
+                s16x8 qa[NP], ga[NP];
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl) {
+                    qa[pl] = lds_row8<RSW>(ql + pl * TW, 16 * qt + c, 32 * ks + 8 * g);
+                    ga[pl] = lds_row8<RSW>(gl + pl * TW, 16 * qt + c, 32 * ks + 8 * g);
+                }
+                s[qt] = mmp<T, NP>(qa, kf[ks], s[qt]);
+                dp[qt] = mmp<T, NP>(ga, vf[ks], dp[qt]);
             }
 #pragma unroll
         for (int qt = 0; qt < 4; ++qt)
@@ -523,12 +600,19 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attn_bwd_dkv_kernel(AtArgs a, f
         // dVᵀ += dOᵀ P, dKᵀ += Qᵀ dS over two 32-query steps
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-            const s16x8 pf = pack_acc<T>(s[2 * st], s[2 * st + 1]);
-            const s16x8 df = pack_acc<T>(dp[2 * st], dp[2 * st + 1]);
+            s16x8 pf[NP], df[NP];
+            pack_acc<T, NP>(s[2 * st], s[2 * st + 1], pf);
+            pack_acc<T, NP>(dp[2 * st], dp[2 * st + 1], df);
 #pragma unroll
             for (int db = 0; db < DB; ++db) {
-                av[db] = Mma<T>::run(lds_tr8<RSW>(gl, 32 * st, 16 * db, lane), pf, av[db]);
-                ak[db] = Mma<T>::run(lds_tr8<RSW>(ql, 32 * st, 16 * db, lane), df, ak[db]);
+                s16x8 gt[NP], qtr[NP];
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl) {
+                    gt[pl] = lds_tr8<RSW>(gl + pl * TW, 32 * st, 16 * db, lane);
+                    qtr[pl] = lds_tr8<RSW>(ql + pl * TW, 32 * st, 16 * db, lane);
+                }
+                av[db] = mmp<T, NP>(gt, pf, av[db]);
+                ak[db] = mmp<T, NP>(qtr, df, ak[db]);
             }
         }
     }
@@ -573,87 +657,107 @@ Drop drop_params(float p) {
     return d;
 }
 
-bool aligned16(const void* p, int64_t sB, int64_t sN, int64_t sH) {
-    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && sB % 8 == 0 && sN % 8 == 0 && sH % 8 == 0;
+// 16-byte operand rows: pointer and every stride a multiple of 8 elements
+bool op_ok(const void* p, int64_t sP, int64_t sB, int64_t sN, int64_t sH) {
+    return p && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && sP % 8 == 0 && sB % 8 == 0 && sN % 8 == 0 &&
+           sH % 8 == 0;
 }
+
+// Launch kernel K<T, D, DROP, NP> for (dtype, D, dropout): dtype 0 fp16, 1 bf16, 2 split fp32 (bf16 planes).
+#define DGX_ATTN_DISPATCH(LAUNCH)                                                  \
+    do {                                                                           \
+        if (dtype == 0) {                                                          \
+            if (D == 128) { if (dr.on) LAUNCH(_Float16, 128, true, 1); else LAUNCH(_Float16, 128, false, 1); } \
+            else { if (dr.on) LAUNCH(_Float16, 64, true, 1); else LAUNCH(_Float16, 64, false, 1); }            \
+        } else if (dtype == 1) {                                                   \
+            if (D == 128) { if (dr.on) LAUNCH(__bf16, 128, true, 1); else LAUNCH(__bf16, 128, false, 1); }     \
+            else { if (dr.on) LAUNCH(__bf16, 64, true, 1); else LAUNCH(__bf16, 64, false, 1); }                \
+        } else {                                                                   \
+            if (D == 128) { if (dr.on) LAUNCH(__bf16, 128, true, 2); else LAUNCH(__bf16, 128, false, 2); }     \
+            else { if (dr.on) LAUNCH(__bf16, 64, true, 2); else LAUNCH(__bf16, 64, false, 2); }                \
+        }                                                                          \
+    } while (0)
 
 }  // namespace
 
 extern "C" {
 
-int dgx_attn_fwd(int dtype, const void* q, int64_t qsB, int64_t qsN, int64_t qsH, const void* k, int64_t ksB,
-                 int64_t ksN, int64_t ksH, const void* v, int64_t vsB, int64_t vsN, int64_t vsH, void* o,
-                 int64_t osB, int64_t osN, int64_t osH, float* lse, int B, int H, int Nq, int Nk, int D, float scale,
-                 float dropout_p, uint64_t seed, void* stream) {
-    if (!q || !k || !v || !o || !lse || B < 0 || H < 1 || Nq < 0 || Nk < 1 || !(scale > 0.f)) return DGX_EINVAL;
+int dgx_attn_fwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN, int64_t qsH, const void* k,
+                 int64_t ksP, int64_t ksB, int64_t ksN, int64_t ksH, const void* v, int64_t vsP, int64_t vsB,
+                 int64_t vsN, int64_t vsH, void* o, int64_t osB, int64_t osN, int64_t osH, float* lse, int B, int H,
+                 int Nq, int Nk, int D, float scale, float dropout_p, uint64_t seed, void* stream) {
+    if (!o || !lse || B < 0 || H < 1 || Nq < 0 || Nk < 1 || !(scale > 0.f)) return DGX_EINVAL;
     if (!(dropout_p >= 0.f && dropout_p < 1.f)) return DGX_EINVAL;
-    if ((dtype != 0 && dtype != 1) || (D != 64 && D != 128)) return DGX_EUNSUPPORTED;
-    if (!aligned16(q, qsB, qsN, qsH) || !aligned16(k, ksB, ksN, ksH) || !aligned16(v, vsB, vsN, vsH) ||
-        (reinterpret_cast<uintptr_t>(o) & 7) != 0 || osB % 4 != 0 || osN % 4 != 0 || osH % 4 != 0)
+    if (dtype < 0 || dtype > 2 || (D != 64 && D != 128)) return DGX_EUNSUPPORTED;
+    if (!op_ok(q, qsP, qsB, qsN, qsH) || !op_ok(k, ksP, ksB, ksN, ksH) || !op_ok(v, vsP, vsB, vsN, vsH) ||
+        (reinterpret_cast<uintptr_t>(o) & 15) != 0 || osB % 4 != 0 || osN % 4 != 0 || osH % 4 != 0)
         return DGX_EINVAL;
     if (B == 0 || Nq == 0) return DGX_OK;
     const Drop dr = drop_params(dropout_p);
-    AtArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(v),
-             nullptr, nullptr, qsB, qsN, qsH, ksB, ksN, ksH, vsB, vsN, vsH, osB, osN, osH, lse, nullptr, H, Nq, Nk,
-             scale * 1.4426950408889634f, scale, dr.p32, dr.rdrop, (uint32_t)seed, (uint32_t)(seed >> 32)};
+    AtArgs a{};
+    a.q = AtOp{static_cast<const uint16_t*>(q), qsP, qsB, qsN, qsH};
+    a.k = AtOp{static_cast<const uint16_t*>(k), ksP, ksB, ksN, ksH};
+    a.v = AtOp{static_cast<const uint16_t*>(v), vsP, vsB, vsN, vsH};
+    a.osB = osB, a.osN = osN, a.osH = osH;
+    a.lse = lse, a.H = H, a.Nq = Nq, a.Nk = Nk;
+    a.scale_log2 = scale * 1.4426950408889634f, a.scale = scale;
+    a.p32 = dr.p32, a.rdrop = dr.rdrop, a.s0 = (uint32_t)seed, a.s1 = (uint32_t)(seed >> 32);
     const dim3 grid((Nq + AT_QB - 1) / AT_QB, B * H);
     hipStream_t st = dgx_stream(stream);
-    uint16_t* out = static_cast<uint16_t*>(o);
-#define DGX_ATTN_FWD(T, DV, DR) hipLaunchKernelGGL((attn_fwd_kernel<T, DV, DR>), grid, dim3(AT_THREADS), 0, st, a, out)
-    if (dtype == 0) {
-        if (D == 128) { if (dr.on) DGX_ATTN_FWD(_Float16, 128, true); else DGX_ATTN_FWD(_Float16, 128, false); }
-        else { if (dr.on) DGX_ATTN_FWD(_Float16, 64, true); else DGX_ATTN_FWD(_Float16, 64, false); }
-    } else {
-        if (D == 128) { if (dr.on) DGX_ATTN_FWD(__bf16, 128, true); else DGX_ATTN_FWD(__bf16, 128, false); }
-        else { if (dr.on) DGX_ATTN_FWD(__bf16, 64, true); else DGX_ATTN_FWD(__bf16, 64, false); }
-    }
+#define DGX_ATTN_FWD(T, DV, DR, NPV)                                                                      \
+    hipLaunchKernelGGL((attn_fwd_kernel<T, DV, DR, NPV>), grid, dim3(AT_THREADS), (at_lds_bytes_qk<DV, NPV>()), \
+                       st, a, o)
+    DGX_ATTN_DISPATCH(DGX_ATTN_FWD);
 #undef DGX_ATTN_FWD
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-int dgx_attn_bwd(int dtype, const void* q, int64_t qsB, int64_t qsN, int64_t qsH, const void* k, int64_t ksB,
-                 int64_t ksN, int64_t ksH, const void* v, int64_t vsB, int64_t vsN, int64_t vsH, const void* o,
-                 const void* dout, int64_t osB, int64_t osN, int64_t osH, const float* lse, float* delta, int B, int H,
-                 int Nq, int Nk, int D, float scale, float dropout_p, uint64_t seed, float* dq, int64_t dqsB,
-                 int64_t dqsN, int64_t dqsH, float* dk, int64_t dksB, int64_t dksN, int64_t dksH, float* dv,
-                 int64_t dvsB, int64_t dvsN, int64_t dvsH, void* stream) {
-    if (!q || !k || !v || !o || !dout || !lse || !delta || !dq || !dk || !dv || B < 0 || H < 1 || Nq < 0 || Nk < 1 ||
-        !(scale > 0.f))
+int dgx_attn_bwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN, int64_t qsH, const void* k,
+                 int64_t ksP, int64_t ksB, int64_t ksN, int64_t ksH, const void* v, int64_t vsP, int64_t vsB,
+                 int64_t vsN, int64_t vsH, const void* o, const void* dout, int64_t gsP, int64_t osB, int64_t osN,
+                 int64_t osH, const float* dout32, const float* lse, float* delta, int B, int H, int Nq, int Nk, int D,
+                 float scale, float dropout_p, uint64_t seed, float* dq, int64_t dqsB, int64_t dqsN, int64_t dqsH,
+                 float* dk, int64_t dksB, int64_t dksN, int64_t dksH, float* dv, int64_t dvsB, int64_t dvsN,
+                 int64_t dvsH, void* stream) {
+    if (!o || !lse || !delta || !dq || !dk || !dv || B < 0 || H < 1 || Nq < 0 || Nk < 1 || !(scale > 0.f))
         return DGX_EINVAL;
     if (!(dropout_p >= 0.f && dropout_p < 1.f)) return DGX_EINVAL;
-    if ((dtype != 0 && dtype != 1) || (D != 64 && D != 128)) return DGX_EUNSUPPORTED;
-    if (!aligned16(q, qsB, qsN, qsH) || !aligned16(k, ksB, ksN, ksH) || !aligned16(v, vsB, vsN, vsH) ||
-        !aligned16(o, osB, osN, osH) || !aligned16(dout, osB, osN, osH))
+    if (dtype < 0 || dtype > 2 || (D != 64 && D != 128)) return DGX_EUNSUPPORTED;
+    if (dtype == 2 && !dout32) return DGX_EINVAL;
+    if (!op_ok(q, qsP, qsB, qsN, qsH) || !op_ok(k, ksP, ksB, ksN, ksH) || !op_ok(v, vsP, vsB, vsN, vsH) ||
+        !op_ok(dout, gsP, osB, osN, osH) || (reinterpret_cast<uintptr_t>(o) & 15) != 0)
         return DGX_EINVAL;
     if ((reinterpret_cast<uintptr_t>(dq) | reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) & 15 ||
         dqsN % 4 || dqsH % 4 || dksN % 4 || dksH % 4 || dvsN % 4 || dvsH % 4 || dqsB % 4 || dksB % 4 || dvsB % 4)
         return DGX_EINVAL;
     if (B == 0 || Nq == 0) return DGX_OK;
     const Drop dr = drop_params(dropout_p);
-    AtArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(v),
-             static_cast<const uint16_t*>(o), static_cast<const uint16_t*>(dout), qsB, qsN, qsH, ksB, ksN, ksH, vsB,
-             vsN, vsH, osB, osN, osH, const_cast<float*>(lse), delta, H, Nq, Nk, scale * 1.4426950408889634f, scale,
-             dr.p32, dr.rdrop, (uint32_t)seed, (uint32_t)(seed >> 32)};
+    AtArgs a{};
+    a.q = AtOp{static_cast<const uint16_t*>(q), qsP, qsB, qsN, qsH};
+    a.k = AtOp{static_cast<const uint16_t*>(k), ksP, ksB, ksN, ksH};
+    a.v = AtOp{static_cast<const uint16_t*>(v), vsP, vsB, vsN, vsH};
+    a.dout = AtOp{static_cast<const uint16_t*>(dout), gsP, osB, osN, osH};
+    a.o = o, a.dout32 = dout32;
+    a.osB = osB, a.osN = osN, a.osH = osH;
+    a.lse = const_cast<float*>(lse), a.delta = delta, a.H = H, a.Nq = Nq, a.Nk = Nk;
+    a.scale_log2 = scale * 1.4426950408889634f, a.scale = scale;
+    a.p32 = dr.p32, a.rdrop = dr.rdrop, a.s0 = (uint32_t)seed, a.s1 = (uint32_t)(seed >> 32);
     hipStream_t st = dgx_stream(stream);
     const int64_t rows = (int64_t)B * H * Nq;
     const unsigned dblocks = (unsigned)((rows * 16 + 255) / 256);
-    if (D == 128) hipLaunchKernelGGL((attn_delta_kernel<128>), dim3(dblocks), dim3(256), 0, st, a, B, a.o, dtype == 1);
-    else hipLaunchKernelGGL((attn_delta_kernel<64>), dim3(dblocks), dim3(256), 0, st, a, B, a.o, dtype == 1);
+    if (D == 128) hipLaunchKernelGGL((attn_delta_kernel<128>), dim3(dblocks), dim3(256), 0, st, a, B, dtype);
+    else hipLaunchKernelGGL((attn_delta_kernel<64>), dim3(dblocks), dim3(256), 0, st, a, B, dtype);
     DGX_CHECK_LAUNCH();
     const dim3 gq((Nq + AT_QB - 1) / AT_QB, B * H), gk((Nk + AT_KB - 1) / AT_KB, B * H);
-#define DGX_ATTN_BWD(T, DV, DR)                                                                                  \
-    do {                                                                                                         \
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DV, DR>), gq, dim3(AT_THREADS), 0, st, a, dq, dqsB, dqsN, dqsH); \
-        hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DV, DR>), gk, dim3(AT_THREADS), 0, st, a, dk, dksB, dksN, dksH, \
-                           dv, dvsB, dvsN, dvsH);                                                                \
+#define DGX_ATTN_BWD(T, DV, DR, NPV)                                                                          \
+    do {                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DV, DR, NPV>), gq, dim3(AT_THREADS),                        \
+                           (at_lds_bytes_qk<DV, NPV>()), st, a, dq, dqsB, dqsN, dqsH);                        \
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DV, DR, NPV>), gk, dim3(AT_THREADS),                       \
+                           (at_lds_bytes_qk<DV, NPV>() + 2 * AT_QT * 4), st, a, dk, dksB, dksN, dksH, dv, dvsB, \
+                           dvsN, dvsH);                                                                       \
     } while (0)
-    if (dtype == 0) {
-        if (D == 128) { if (dr.on) DGX_ATTN_BWD(_Float16, 128, true); else DGX_ATTN_BWD(_Float16, 128, false); }
-        else { if (dr.on) DGX_ATTN_BWD(_Float16, 64, true); else DGX_ATTN_BWD(_Float16, 64, false); }
-    } else {
-        if (D == 128) { if (dr.on) DGX_ATTN_BWD(__bf16, 128, true); else DGX_ATTN_BWD(__bf16, 128, false); }
-        else { if (dr.on) DGX_ATTN_BWD(__bf16, 64, true); else DGX_ATTN_BWD(__bf16, 64, false); }
-    }
+    DGX_ATTN_DISPATCH(DGX_ATTN_BWD);
 #undef DGX_ATTN_BWD
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }

@@ -15,8 +15,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-TOL_FWD = {torch.float16: 2e-3, torch.bfloat16: 1.2e-2}
-TOL_BWD = {torch.float16: 5e-3, torch.bfloat16: 3e-2}
+# fp32: the split-plane mode (x = bf16 hi + bf16 lo, three MFMAs per product)
+TOL_FWD = {torch.float16: 2e-3, torch.bfloat16: 1.2e-2, torch.float32: 1e-4}
+TOL_BWD = {torch.float16: 5e-3, torch.bfloat16: 3e-2, torch.float32: 2e-4}
 
 
 def _nerr(a, b):
@@ -59,7 +60,7 @@ CASES = [  # B, heads, Nq, Nk, D
 ]
 
 
-@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,H,Nq,Nk,D", CASES)
 def test_attention_forward_backward(cuda, dt, B, H, Nq, Nk, D):
     from dgx.attention import attention
@@ -70,6 +71,7 @@ def test_attention_forward_backward(cuda, dt, B, H, Nq, Nk, D):
     v.requires_grad_(True)
     o = attention(q, k, v, H)
     assert o.dtype == dt and o.shape == (B, Nq, E)
+    assert q.dtype != torch.float32 or __import__("dgx.precision").precision.get() == "fp32"
     scale = 1.0 / math.sqrt(D)
     qr, kr, vr = (t.detach().double().requires_grad_(True) for t in (q, k, v))
     ref = _ref(qr, kr, vr, H, scale)
@@ -92,8 +94,8 @@ def test_attention_strided_projection_views(cuda, dt):
     torch.testing.assert_close(o1, o2, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("p", [0.5, 0.1])
-def test_attention_dropout_matches_masked_reference(cuda, monkeypatch, p):
+@pytest.mark.parametrize("p,dt", [(0.5, torch.float16), (0.1, torch.float16), (0.5, torch.float32)])
+def test_attention_dropout_matches_masked_reference(cuda, monkeypatch, p, dt):
     """Forward and backward with dropout equal the fp64 reference that applies
     the kernels' own keep mask (dgx_attn_dropout_mask) to the softmax weights."""
     import dgx.attention as A
@@ -101,19 +103,19 @@ def test_attention_dropout_matches_masked_reference(cuda, monkeypatch, p):
     E = H * D
     seed = 0x1234_5678_9ABC
     monkeypatch.setattr(A, "new_seed", lambda: seed)
-    q, k, v = _inputs(B, N, N, E, torch.float16, cuda, 21)
+    q, k, v = _inputs(B, N, N, E, dt, cuda, 21)
     for t in (q, k, v):
         t.requires_grad_(True)
     o = A.attention(q, k, v, H, dropout_p=p)
     mask = A.dropout_mask(B * H * N, N, p, seed, cuda)
     qr, kr, vr = (t.detach().double().requires_grad_(True) for t in (q, k, v))
     ref = _ref(qr, kr, vr, H, 1.0 / math.sqrt(D), mask=mask, p=p)
-    assert _nerr(o, ref) < TOL_FWD[torch.float16]
-    go = torch.randn(o.shape, generator=torch.Generator().manual_seed(5)).half().to(cuda)
+    assert _nerr(o, ref) < TOL_FWD[dt]
+    go = torch.randn(o.shape, generator=torch.Generator().manual_seed(5)).to(dt).to(cuda)
     o.backward(go)
     ref.backward(go.double())
     for got, want in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
-        assert _nerr(got, want) < TOL_BWD[torch.float16]
+        assert _nerr(got, want) < TOL_BWD[dt]
 
 
 def test_dropout_mask_statistics(cuda):
