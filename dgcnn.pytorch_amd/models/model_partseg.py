@@ -1,5 +1,5 @@
 """Drop-in for reference ``models/model_partseg.py``: ``compute_hog_1x1``,
-``MLPHead``, ``Net`` (SURVEY §8 rows a7, a9, f1).
+``MLPHead``, ``Net`` (SURVEY §8 rows a7, a9, f1, f2).
 
 Engine work on this path: the kNN, which ``Net.forward`` reaches three times on
 the same cloud — the four EdgeConv blocks of ``emb_nn`` (model_partseg.py:177),
@@ -10,8 +10,13 @@ as the reference binds them (model_partseg.py:11-12) — and the rest of
 neighbourhoods, H2D copy and histogram votes (model_partseg.py:28-92) are one
 device call (dgx.hog, csrc/hog.hip) with LAPACK's singular-vector signs.
 
-The transformer / attention / MLP head stay the reference's own PyTorch
-composition (stock PyTorch-ROCm modules; out of the engine's scope). Two
+The transformer and the final attention keep the reference's modules and
+state_dict (``nn.Transformer``, ``nn.MultiheadAttention``), with every
+multi-head attention inside them switched to ``dgx.attention.
+EngineMultiheadAttention`` (row f2): the attention itself — scores, softmax,
+dropout on the weights, weighted sum and their backward — is one fused HIP
+kernel pair per call instead of scaled_dot_product_attention. Projections,
+LayerNorms, feed-forward blocks and the MLP head stay stock PyTorch. Two
 reference behaviours are reproduced on purpose, because checkpoints and
 downstream numbers depend on them:
   * the HOG gathers rows of ``x.contiguous().view(B*N, -1)`` with LOCAL ids
@@ -25,6 +30,7 @@ import os
 import torch
 import torch.nn as nn
 
+from dgx.attention import use_engine_attention
 from dgx.hog import hog_1x1
 from models.dgcnn import DGCNN, knn
 from models.layers import PositionEmbedding
@@ -93,6 +99,9 @@ class Net(nn.Module):
                                           batch_first=True)
         self.attention = nn.MultiheadAttention(embed_dim=e, num_heads=args.n_heads, dropout=args.dropout,
                                                batch_first=True)
+        # f2: the 3 attentions of each transformer call and the final one on the engine
+        use_engine_attention(self.transformer)
+        use_engine_attention(self.attention)
         self.head = MLPHead(args)
 
     def forward(self, src, lbl):

@@ -183,3 +183,35 @@ def test_engine_mha_train_step(cuda):
     y_tr, _ = m(x, x, x, need_weights=False)
     y_ev, _ = m.eval()(x, x, x, need_weights=False)
     assert torch.equal(y_tr, y_ev)
+
+
+def test_net_attention_on_engine(cuda):
+    """Net's transformer and final attention run on the engine (row f2): every
+    nn.MultiheadAttention inside Net is the engine class, an eval forward
+    matches the same weights on stock PyTorch attention (fp32 parity mode),
+    and a dropout-0.5 training step (the reference default) has finite grads."""
+    import types
+    from dgx import synth
+    from dgx.attention import EngineMultiheadAttention
+    from models.model_partseg import Net
+    torch.manual_seed(4)
+    args = types.SimpleNamespace(k=20, emb_dim=128, n_heads=2, n_blocks=1, ff_dims=128, dropout=0.5, nclasses=50)
+    net = Net(args).to(cuda)
+    mhas = [m for m in net.modules() if isinstance(m, torch.nn.MultiheadAttention)]
+    assert len(mhas) == 4 and all(type(m) is EngineMultiheadAttention for m in mhas)
+    src = torch.from_numpy(synth.cube_clouds(2, 512, 3)).to(cuda).permute(0, 2, 1).contiguous()
+    lbl = torch.nn.functional.one_hot(torch.tensor([1, 9]), 16).float().to(cuda)
+    net.eval()
+    with torch.no_grad():
+        got = net(src, lbl)
+        for m in mhas:
+            m.__class__ = torch.nn.MultiheadAttention
+        want = net(src, lbl)
+        for m in mhas:
+            m.__class__ = EngineMultiheadAttention
+    assert _nerr(got, want) < 1e-4, _nerr(got, want)
+    net.train()
+    out = net(src, lbl)
+    out.square().mean().backward()
+    for n, p in net.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), n
