@@ -71,6 +71,7 @@ def parse(argv=None):
     p.add_argument("--no-posemb-leg", action="store_true",
                    help="skip the PositionEmbedding edge-MLP timing (partseg geometry)")
     p.add_argument("--no-roofline-leg", action="store_true", help="skip the event-timed kNN region")
+    p.add_argument("--no-attention-leg", action="store_true", help="skip the Net attention (f2) timing")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse several ranks "
                         "on one GPU)")
@@ -272,6 +273,42 @@ def posemb_edge_leg(dev, B=32, N=2048, k=40, reps=5):
     return out
 
 
+def attention_leg(dev, B=32, N=2048, E=512, H=4, p=0.5, reps=5):
+    """f2: one attention of Net (reference models/model_partseg.py:167-171,
+    187-191: nn.Transformer / nn.MultiheadAttention at the partseg geometry,
+    BASELINE cfg4 per GPU: B 32, N 2048, emb 512, 4 heads, dropout 0.5), fp16
+    operands as the reference's AMP run has them, fwd+bwd: the engine kernels
+    (dgx.attention) next to torch's scaled_dot_product_attention."""
+    import torch
+    import torch.nn.functional as F
+    from dgx.attention import attention
+    g = torch.Generator(device=dev).manual_seed(0)
+    D = E // H
+    qkv = torch.randn((B, N, 3 * E), device=dev, generator=g).half()
+    go = torch.randn((B, N, E), device=dev, generator=g).half()
+    q, k, v = (qkv[..., i * E:(i + 1) * E].detach().clone().requires_grad_(True) for i in range(3))
+
+    def engine():
+        attention(q, k, v, H, p).backward(go)
+
+    qh, kh, vh = (t.detach().reshape(B, N, H, D).transpose(1, 2).requires_grad_(True) for t in (q, k, v))
+    goh = go.reshape(B, N, H, D).transpose(1, 2)
+
+    def sdpa():
+        F.scaled_dot_product_attention(qh, kh, vh, dropout_p=p).backward(goh)
+
+    flops = 3.5 * 4.0 * B * H * N * N * D  # fwd 2 products + bwd 5 (FlashAttention accounting)
+    out = {"config": f"B={B} N={N} E={E} heads={H} D={D} dropout={p}, fp16 operands, fwd+bwd"}
+    out["engine_ms"] = round(_ms(engine, reps, warm=2), 3)
+    out["engine_tflops"] = round(flops / (out["engine_ms"] * 1e-3) / 1e12, 1)
+    try:
+        out["torch_sdpa_ms"] = round(_ms(sdpa, reps, warm=2), 3)
+        out["speedup"] = round(out["torch_sdpa_ms"] / out["engine_ms"], 2)
+    except RuntimeError as e:
+        out["torch_sdpa_ms"] = {"error": str(e)[:200]}
+    return out
+
+
 def cpu_baseline(args, clouds):
     """oracle/reference.py (torch-CPU restatement of the reference, pinned by
     tests/golden) timed on this job's host cores for DGCNN(emb) train fwd+bwd
@@ -457,6 +494,8 @@ def main():
             result["edgeconv_fwd_bwd_ms"] = edgeconv_legs(model, x)
         if not args.no_posemb_leg:
             result["posemb_edge_mlp"] = posemb_edge_leg(dev)
+        if not args.no_attention_leg:
+            result["net_attention"] = attention_leg(dev)
         if not args.no_eager_baseline:
             eager = {}
             ours32 = result["ms_per_step"] if args.precision == "fp32" else result.get("fp32_mode", {}).get(
