@@ -300,7 +300,10 @@ __global__ __launch_bounds__(256) void bwd16_dz_lt_kernel(const float* __restric
 // PASS 0 with the transposed tile over RS_LT consecutive 128-point tiles per
 // block: per-thread sums over its 4 points, then over the 32 lanes of its
 // channel group (one shuffle tree), one partial row per block.
-constexpr int RS_LT = 1;
+#ifndef DGX_RS_LT
+#define DGX_RS_LT 2
+#endif
+constexpr int RS_LT = DGX_RS_LT;
 __global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __restrict__ dout,
                                                              const bf16* __restrict__ Z, int N, int C,
                                                              const float* __restrict__ scale,
@@ -338,7 +341,7 @@ __global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __rest
             const float4 v = load_row4(dout, ((int64_t)b * C + oo) * N, n, N, oo < C);
             g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
         }
-        __syncthreads();  // previous tile's reads done
+        if (it > 0) __syncthreads();  // previous tile's reads done (a barrier here would also wait for the dout loads)
         stage_ztile(Z, b, n0, o0, N, C, zt);
         __syncthreads();
         float z[4][8];
