@@ -10,7 +10,7 @@
 //     in registers: 8 lanes per query (4 lanes x 2 candidate halves), merged
 //     at the end.
 //
-// Three launches per call:
+// Two launches per call:
 //   knn_image_kernel  one pass over x: |x|^2 in the reference's order and an
 //                     MFMA A-operand "image" of each cloud (16-candidate tiles,
 //                     lane-ordered so a wave fetches a tile with 16-B loads).
@@ -21,7 +21,8 @@
 //                     no LDS staging, no barrier until the final merge. Each
 //                     query's candidates are dealt over 8 register lists (4 lanes
 //                     x 2 halves) with an admission bound shared through LDS.
-//   knn_fix_kernel    exact recompute of the (rare) rows whose list overflowed.
+//                     A (rare) row whose list overflowed is recomputed exactly
+//                     by the same block at the end (knn_fix_row).
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -145,11 +146,11 @@ __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[
 // KQ_LISTS = 8 lanes (interleaved by index, see knn_row), so the true top-k
 // splits ~Binomial(k, 1/8) over its lists; KL is where that distribution's
 // upper tail drops to ~2e-6 per lane. A lane needing more than KL slots flags
-// its row, which is recomputed exactly (knn_fix_kernel).
+// its row, which is recomputed exactly (knn_fix_row).
 template <int KB>
 struct KnnList {
     // (KL 10 / 9 at KB 20 measured: fewer insertion VALU, but the rows they flag
-    // cost more in knn_fix_kernel than the lists save)
+    // cost more in the fix-up than the lists save)
     static constexpr int KL = KB <= 16 ? 10 : (KB <= 20 ? 12 : (KB <= 32 ? 15 : (KB <= 40 ? 17 : 23)));
     static constexpr int RPL = (KB + 3) / 4;   // ranks per lane of a wave's 4-list merge
 };
@@ -173,15 +174,13 @@ __device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (ro
 // same row order: xximg[(b*ntile + s)*16 + i]. A query's own operand (the B
 // side) is read from the same image.
 constexpr int KI_TILES = 1;  // tiles per image-builder block
-constexpr int FIXP_ROWS = 64;  // flagged rows whose fix-up is split over the grid (knn_fix_kernel)
 // One pass over x per layer: the operand image, the |x|^2 image and xx itself
 // (|x_i|^2 in the reference's rounding order, sqnorm_sum on the staged row).
 template <int NSTEP>
 __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
                                                         int64_t sN, int B, int C, int N, int order, int ntile,
                                                         int tgroups, float* __restrict__ xx,
-                                                        float* __restrict__ img, float* __restrict__ xximg,
-                                                        int* __restrict__ ctl) {
+                                                        float* __restrict__ img, float* __restrict__ xximg) {
 #pragma clang fp contract(off)
     constexpr int CP = NSTEP * 4;
     constexpr int P = 16 * KI_TILES;
@@ -191,10 +190,6 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
     const int s0 = (blockIdx.x - b * tgroups) * KI_TILES;
     const int t = threadIdx.x;
     const float* __restrict__ xb = x + b * sB;
-    if (blockIdx.x == 0) {  // empty fix-up list and split-row counters for the selection that follows
-        if (t < 2) ctl[t] = 0;
-        if (t < 2 * FIXP_ROWS) ctl[4 + (int64_t)B * N + t] = 0;
-    }
     for (int e = t; e < P * CP; e += 256) {
         int p, c;
         if (sN == 1) { c = e / P; p = e - c * P; }   // candidate-fastest: unit stride along n
@@ -229,13 +224,17 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
 inline int knn_nstep(int C) { return C <= 4 ? 1 : (C <= 12 ? 3 : (C <= 32 ? 8 : (C <= 64 ? 16 : 32))); }
 inline int knn_ntile(int N) { return (N + 15) / 16; }
 
+constexpr int FIX_MAXN = 12288;  // largest N (the fix-up's tie bitmap)
+constexpr int FX_CAP = 256;      // candidates above T0 ranked directly by the fix-up
+
 template <int KB>
 constexpr int knn_smem_floats() {
     constexpr int stream = KQ_HALVES * KQ_QPB                     // published admission bounds
                            + KQ_WAVES * KQ_QCAP * 64              // FIFO values
                            + KQ_WAVES * KQ_QCAP * 32;             // FIFO indices (u16)
     constexpr int merge = KQ_HALVES * KQ_QPB * KB * 2 + 2 * KQ_QPB;  // half lists | k-th | flags
-    return stream > merge ? stream : merge;
+    constexpr int fix = merge + 2 * FX_CAP + 8 + FIX_MAXN / 32;      // ... | fix-up candidates, counters, tie bitmap
+    return stream > fix ? stream : fix;
 }
 
 // Canonical order: value descending, then index ascending.
@@ -260,6 +259,134 @@ __device__ __forceinline__ void ld_vec(const float* __restrict__ p, float (&r)[V
     }
 }
 
+// ------------------------------------------------------------- fix-up ----
+// Exact recompute of one flagged query row qf of cloud b by the whole block
+// (called block-uniformly after the merge). T0 = the merged k-th value of the
+// row's lists: at least k candidates reach it, so the true k-th value is >= T0.
+// Every distance is recomputed by the same MFMA chain on the same operands as
+// the main stream (the query's doubled operand replicated over the 16 output
+// columns; wave w takes tiles w, w+4, ...), so the values are identical.
+//   n_gt = #{v > T0}. If n_gt >= k the top-k is among them: rank them
+//   canonically (all-pairs) when they fit FX_CAP. If n_gt < k the k-th value is
+//   T0 itself: the n_gt candidates above it, then the k - n_gt smallest indices
+//   with v == T0 (a bitmap of ties, scanned in index order). With more than
+//   FX_CAP candidates above T0 (mass ties) the row is extracted by k rounds of a
+//   canonical arg-max over re-streamed values (slow, correct).
+template <int NSTEP>
+__device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const float* __restrict__ xib,
+                            const float* __restrict__ xxb, int N, int k, int qf, float t0, int64_t row,
+                            int64_t* __restrict__ idx64, int32_t* __restrict__ idx32, float* __restrict__ vals) {
+#pragma clang fp contract(off)
+    float* cv = fixa;
+    int* cj = reinterpret_cast<int*>(fixa + FX_CAP);
+    int* cnt = reinterpret_cast<int*>(fixa + 2 * FX_CAP);       // [0]: candidates above T0
+    float* bestv = fixa + 2 * FX_CAP + 4;                        // [KQ_WAVES]: arg-max path per-wave values
+    uint32_t* bits = reinterpret_cast<uint32_t*>(fixa + 2 * FX_CAP + 8);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
+    const int ntile = (N + 15) >> 4, nw = (N + 31) >> 5;
+    if (tid == 0) cnt[0] = 0;
+    for (int w = tid; w < nw; w += KQ_THREADS) bits[w] = 0u;
+    float bq[NSTEP];
+    ld_vec<NSTEP>(ib + ((int64_t)(qf >> 4) * 64 + g * 16 + knn_row(qf & 15)) * NSTEP, bq);
+#pragma unroll
+    for (int t = 0; t < NSTEP; ++t) bq[t] *= 2.0f;
+    const float xxq = xxb[qf];
+    __syncthreads();
+    // act(v, j) on every candidate; lanes with ql == 0 hold column 0 (all columns are the same query)
+    auto stream = [&](auto&& act) {
+        for (int s = wave; s < ntile; s += KQ_WAVES) {
+            float a[NSTEP];
+            ld_vec<NSTEP>(ib + ((int64_t)s * 64 + lane) * NSTEP, a);
+            const float4 xc = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < NSTEP; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bq[t], acc, 0, 0, 0);
+            if (ql == 0) {
+                const int j0 = s * 16 + g;
+                const float xcv[4] = {xc.x, xc.y, xc.z, xc.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = j0 + 4 * r;
+                    const float tq = acc[r] - xcv[r];
+                    if (j < N) act(tq - xxq, j);
+                }
+            }
+        }
+    };
+    stream([&](float v, int j) {
+        if (v > t0) {
+            const int sl = atomicAdd(&cnt[0], 1);
+            if (sl < FX_CAP) { cv[sl] = v; cj[sl] = j; }
+        } else if (v == t0) {
+            atomicOr(&bits[j >> 5], 1u << (j & 31));
+        }
+    });
+    __syncthreads();
+    const int ngt = cnt[0];
+    auto put = [&](int rank, int j, float v) {
+        if (idx64) idx64[row * k + rank] = j;
+        if (idx32) idx32[row * k + rank] = j;
+        if (vals) vals[row * k + rank] = v;
+    };
+    if (ngt <= FX_CAP) {
+        for (int t = tid; t < ngt; t += KQ_THREADS) {
+            const float v = cv[t];
+            const int j = cj[t];
+            int rank = 0;
+            for (int u = 0; u < ngt; ++u) rank += canon_better(cv[u], cj[u], v, j) ? 1 : 0;
+            if (rank < k) put(rank, j, v);
+        }
+        if (ngt < k && wave == 0) {  // ranks ngt..k-1: ties at T0 in index order
+            const int per = (nw + 63) >> 6;
+            const int w0 = min(lane * per, nw), w1 = min(w0 + per, nw);
+            int c = 0;
+            for (int w = w0; w < w1; ++w) c += __popc(bits[w]);
+            int inc = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            int rank = ngt + inc - c;
+            for (int w = w0; w < w1 && rank < k; ++w) {
+                uint32_t m = bits[w];
+                while (m && rank < k) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    put(rank++, (w << 5) + bit, t0);
+                }
+            }
+        }
+    } else {
+        // mass ties above T0: rank r = the canonically best candidate worse than rank r-1
+        float pv = INFINITY;
+        int pj = -1;
+        for (int r = 0; r < k; ++r) {
+            float bv = -INFINITY;
+            int bj = 0x7fffffff;
+            stream([&](float v, int j) {
+                if (canon_better(pv, pj, v, j) && canon_better(v, j, bv, bj)) { bv = v; bj = j; }
+            });
+#pragma unroll
+            for (int o = 16; o < 64; o <<= 1) {
+                const float ov = __shfl_xor(bv, o);
+                const int oj = __shfl_xor(bj, o);
+                if (canon_better(ov, oj, bv, bj)) { bv = ov; bj = oj; }
+            }
+            __syncthreads();  // previous round's picks are read
+            if (lane == 0) { bestv[wave] = bv; cj[wave] = bj; }
+            __syncthreads();
+            pv = bestv[0];
+            pj = cj[0];
+#pragma unroll
+            for (int w = 1; w < KQ_WAVES; ++w)
+                if (canon_better(bestv[w], cj[w], pv, pj)) { pv = bestv[w]; pj = cj[w]; }
+            if (tid == 0) put(r, pj, pv);
+        }
+    }
+    __syncthreads();  // the fix-up area is free for the next row
+}
+
 // ------------------------------------------------------------ knn kernel ----
 // Block = KQ_GROUPS query groups x 2 candidate halves, one wave each. A wave
 // streams the tiles s = h, h+2, h+4, ... of its cloud's image with its loads
@@ -270,8 +397,7 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
                                                          const float* __restrict__ xximg,
                                                          const float* __restrict__ xx, int B, int N, int k,
                                                          int nqb, int64_t* __restrict__ idx64,
-                                                         int32_t* __restrict__ idx32, float* __restrict__ vals,
-                                                         int* __restrict__ ctl) {
+                                                         int32_t* __restrict__ idx32, float* __restrict__ vals) {
 #pragma clang fp contract(off)
     constexpr int KL = KnnList<KB>::KL;
     constexpr int RPL = KnnList<KB>::RPL;
@@ -502,261 +628,25 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     const float kv = kth[qq];
     if (last != -INFINITY && last >= kv) flg[qq] = 1;
     __syncthreads();
-    if (q < N) {
-        const bool flag = flg[qq] != 0;
-        if (flag && h == 0 && g == 0) ctl[4 + atomicAdd(ctl, 1)] = b * N + q;  // fix-up list
+    if (q < N && flg[qq] == 0) {  // flagged rows are written by the fix-up below
         const int64_t row = ((int64_t)b * N + q) * k;
 #pragma unroll
         for (int t = 0; t < RPL; ++t) {
             const int r = rk[t];
             if (r < k) {
-                // flagged: rank 0 = -1 marker, rank 1 = bits of the merged k-th
-                // value (a lower bound of the true k-th) for the fix-up pass
-                const int j = !flag ? oj[t] : (r == 0 ? -1 : (r == 1 ? __float_as_int(kv) : oj[t]));
-                if (idx64) idx64[row + r] = j;
-                if (idx32) idx32[row + r] = j;
+                if (idx64) idx64[row + r] = oj[t];
+                if (idx32) idx32[row + r] = oj[t];
                 if (vals) vals[row + r] = ov[t];
             }
         }
     }
-}
-
-// Exact recompute of the rows knn_kernel flagged (rank 0 = -1, rank 1 = the
-// bits of T0, the merged k-th value: at least k candidates reach T0). knn_kernel
-// appends flagged rows to a list in the workspace (ctl[0] = count, rows from
-// ctl[4]). A row's recompute is every distance of its cloud (the same k-ordered
-// fmaf chain the MFMA performs, the same rounding sequence), keeping the
-// candidates >= T0 (normally k plus the few the overflowing list dropped),
-// ranked canonically in one all-pairs pass.
-//
-// Split rows (the first FIXP_ROWS of the list, normally all of them): the
-// distances of a row are computed in units of FIXP_TILES image tiles spread over
-// the grid; each unit stages its tiles from the operand image (contiguous,
-// coalesced) into LDS, one thread per candidate runs the chain from LDS, and
-// the candidates go to the row's list in the workspace; the block that finishes
-// a row's last unit ranks it. A row with more than FIXP_CAP candidates (mass
-// ties) and the rows past FIXP_ROWS take the serial path: one block recomputes
-// the row alone, and if more than FIX_CAP reach T0, wave 0 extracts the top-k
-// from all N by k rounds of a canonical arg-max.
-constexpr int FIX_MAXN = 12288;
-constexpr int FIX_CB = 16;    // channels loaded per batch (loads in flight), serial path
-constexpr int FIX_CAP = 1024;
-constexpr int FIXP_CAP = 256;
-constexpr int FIXP_TILES = 4;
-constexpr int FIX_BLOCKS = 256;
-
-// ctl words: count, exit counter, 2 spare | row list (B*N) | split-row candidate
-// counters and unit counters (FIXP_ROWS each) | candidate values, ids
-inline size_t knn_ctl_words(int B, int N) {
-    return 4 + (size_t)B * N + 2 * FIXP_ROWS + 2 * (size_t)FIXP_ROWS * FIXP_CAP;
-}
-
-struct FixShared {
-    float pd[FIX_MAXN];  // serial path: the row's N values; split path: the unit's staged tiles
-    float cv[FIX_CAP];
-    int cj[FIX_CAP];
-    float xq[128];
-    int ncand;
-    int last;
-};
-
-// Rank n candidates (cv, cj in LDS) canonically; ranks < k are the row's output.
-__device__ __forceinline__ void fix_rank_write(FixShared& sh, int n, int64_t row, int k, int64_t* idx64,
-                                               int32_t* idx32, float* vals) {
-    for (int t = threadIdx.x; t < n; t += 256) {
-        const float v = sh.cv[t];
-        const int j = sh.cj[t];
-        int rank = 0;
-        for (int u = 0; u < n; ++u) rank += canon_better(sh.cv[u], sh.cj[u], v, j) ? 1 : 0;
-        if (rank < k) {
-            if (idx64) idx64[row * k + rank] = j;
-            if (idx32) idx32[row * k + rank] = j;
-            if (vals) vals[row * k + rank] = v;
-        }
-    }
-}
-
-// T0 of a flagged row: the bits knn_kernel left at rank 1.
-__device__ __forceinline__ float fix_t0(int64_t row, int k, const int64_t* idx64, const int32_t* idx32) {
-    if (k <= 1) return -INFINITY;
-    return __int_as_float(idx64 ? (int)idx64[row * k + 1] : idx32[row * k + 1]);
-}
-
-// One block recomputes row `row` alone (block-uniform call).
-__device__ void fix_row_serial(FixShared& sh, int64_t row, const float* __restrict__ x, int64_t sB, int64_t sC,
-                               int64_t sN, const float* __restrict__ xx, int C, int N, int k,
-                               int64_t* __restrict__ idx64, int32_t* __restrict__ idx32, float* __restrict__ vals) {
-#pragma clang fp contract(off)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b = (int)(row / N), q = (int)(row - (int64_t)b * N);
-    const float* __restrict__ xb = x + b * sB;
-    const float* __restrict__ xxb = xx + (int64_t)b * N;
-    const float t0 = fix_t0(row, k, idx64, idx32);
-    if (tid < C) sh.xq[tid] = xb[tid * sC + q * sN];
-    if (tid == 0) sh.ncand = 0;
-    __syncthreads();
-    const float xxq = xxb[q];
-    auto keep = [&](int j, float v) {
-        sh.pd[j] = v;
-        if (v >= t0) {
-            const int s = atomicAdd(&sh.ncand, 1);
-            if (s < FIX_CAP) { sh.cv[s] = v; sh.cj[s] = j; }
-        }
-    };
-    for (int j0 = tid; j0 < N; j0 += 512) {
-        const int ja = j0, jb = j0 + 256;
-        float da = 0.f, db = 0.f;
-        for (int c0 = 0; c0 < C; c0 += FIX_CB) {
-            float va[FIX_CB], vb[FIX_CB];
-#pragma unroll
-            for (int u = 0; u < FIX_CB; ++u) {
-                const int c = c0 + u;
-                va[u] = c < C ? xb[c * sC + ja * sN] : 0.f;
-                vb[u] = (c < C && jb < N) ? xb[c * sC + jb * sN] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < FIX_CB; ++u) {
-                if (c0 + u < C) {
-                    da = fmaf(va[u], sh.xq[c0 + u], da);
-                    db = fmaf(vb[u], sh.xq[c0 + u], db);
-                }
-            }
-        }
-        const float ta = 2.0f * da, tb = 2.0f * db;
-        const float ua = ta - xxb[ja];
-        keep(ja, ua - xxq);
-        if (jb < N) {
-            const float ub = tb - xxb[jb];
-            keep(jb, ub - xxq);
-        }
-    }
-    __syncthreads();
-    const int n = sh.ncand;
-    if (n <= FIX_CAP) {
-        fix_rank_write(sh, n, row, k, idx64, idx32, vals);
-    } else if (wave == 0) {
-        for (int r = 0; r < k; ++r) {
-            float bv = -INFINITY;
-            int bj = 0x7fffffff;
-            for (int j = lane; j < N; j += 64)
-                if (canon_better(sh.pd[j], j, bv, bj)) { bv = sh.pd[j]; bj = j; }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const float pv = __shfl_xor(bv, o);
-                const int pj = __shfl_xor(bj, o);
-                if (canon_better(pv, pj, bv, bj)) { bv = pv; bj = pj; }
-            }
-            if (lane == 0) {
-                sh.pd[bj] = -INFINITY;  // taken: finite candidates always outrank it
-                if (idx64) idx64[row * k + r] = bj;
-                if (idx32) idx32[row * k + r] = bj;
-                if (vals) vals[row * k + r] = bv;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(256) void knn_fix_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
-                                                      int64_t sN, const float* __restrict__ xx,
-                                                      const float* __restrict__ img, int nstep, int B, int C,
-                                                      int N, int k, int64_t* __restrict__ idx64,
-                                                      int32_t* __restrict__ idx32, float* __restrict__ vals,
-                                                      int* __restrict__ ctl) {
-#pragma clang fp contract(off)
-    __shared__ FixShared sh;
-    const int tid = threadIdx.x;
-    const int nr = ctl[0];  // rows knn_kernel appended to the list
-    // Nothing flagged (the common case): no block touches the list or the
-    // exit counter, so there is nothing to reset and no device-scope fence.
-    // Uniform: the list is only reset after every block has read it.
-    if (nr == 0) return;
-    const int ntile = (N + 15) / 16;
-    const int np = min(nr, FIXP_ROWS);
-    const int nch = (ntile + FIXP_TILES - 1) / FIXP_TILES;
-    const int units = np * nch;
-    int* cnt = ctl + 4 + (int64_t)B * N;
-    int* fin = cnt + FIXP_ROWS;
-    float* candv = reinterpret_cast<float*>(fin + FIXP_ROWS);
-    int* candj = reinterpret_cast<int*>(candv + FIXP_ROWS * FIXP_CAP);
-    const int NS1 = nstep + 1;  // padded LDS row: candidates of a tile hit distinct banks
-    for (int u = blockIdx.x; u < units + (nr - np); u += gridDim.x) {
-        if (u >= units) {
-            fix_row_serial(sh, ctl[4 + np + (u - units)], x, sB, sC, sN, xx, C, N, k, idx64, idx32, vals);
-            continue;
-        }
-        const int r = u / nch, ch = u - r * nch;
-        const int64_t row = ctl[4 + r];
-        const int b = (int)(row / N), q = (int)(row - (int64_t)b * N);
-        const float t0 = fix_t0(row, k, idx64, idx32);
-        const float* __restrict__ ib = img + (int64_t)b * ntile * 64 * nstep;
-        const int s0 = ch * FIXP_TILES, nt = min(FIXP_TILES, ntile - s0);
-        if (tid < C) {  // the query's channels from its own tile
-            const int sq = q >> 4, iq = knn_row(q & 15);
-            sh.xq[tid] = ib[((int64_t)sq * 64 + 16 * (tid & 3) + iq) * nstep + (tid >> 2)];
-        }
-        // stage the unit's tiles: nt * 64 * nstep contiguous floats
-        const float* __restrict__ src = ib + (int64_t)s0 * 64 * nstep;
-        for (int e = tid; e < nt * 64 * nstep; e += 256) {
-            const int l = e / nstep, t = e - l * nstep;
-            sh.pd[l * NS1 + t + (l >> 6) * 16] = src[e];  // + tile skew: the 4 tiles' rows on distinct banks
-        }
-        __syncthreads();
-        if (tid < nt * 16) {  // one thread per candidate j = 16 (s0 + sl) + p
-            const int sl = tid >> 4, p = tid & 15, i = knn_row(p);
-            const int j = 16 * (s0 + sl) + p;
-            if (j < N) {
-                const float* xs = sh.pd + (sl * 64 + i) * NS1 + sl * 16;
-                float d = 0.f;
-                for (int c = 0; c < C; ++c) d = fmaf(xs[16 * (c & 3) * NS1 + (c >> 2)], sh.xq[c], d);
-                const float* __restrict__ xxb = xx + (int64_t)b * N;
-                const float v = (2.0f * d - xxb[j]) - xxb[q];
-                if (v >= t0) {
-                    const int s = atomicAdd(&cnt[r], 1);
-                    if (s < FIXP_CAP) {
-                        candv[r * FIXP_CAP + s] = v;
-                        candj[r * FIXP_CAP + s] = j;
-                    }
-                }
-            }
-        }
-        __threadfence();  // release this unit's candidates (each storing thread)
-        __syncthreads();
-        if (tid == 0) {
-            sh.last = atomicAdd(&fin[r], 1) == nch - 1;
-        }
-        __syncthreads();
-        if (sh.last) {  // every unit of row r is in: rank it
-            __threadfence();  // acquire the other units' candidates
-            const int n = __hip_atomic_load(&cnt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (n <= FIXP_CAP) {
-                for (int t = tid; t < n; t += 256) {
-                    sh.cv[t] = __hip_atomic_load(&candv[r * FIXP_CAP + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    sh.cj[t] = __hip_atomic_load(&candj[r * FIXP_CAP + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __syncthreads();
-                fix_rank_write(sh, n, row, k, idx64, idx32, vals);
-                __syncthreads();
-            } else {
-                fix_row_serial(sh, row, x, sB, sC, sN, xx, C, N, k, idx64, idx32, vals);
-            }
-            if (tid == 0) {  // the row's counters are clean for the next selection
-                cnt[r] = 0;
-                fin[r] = 0;
-            }
-        }
-        __syncthreads();
-    }
-    // the last block out resets the list for the next selection on this workspace
-    if (tid == 0) {
-        __threadfence();
-        if (atomicAdd(&ctl[1], 1) == (int)gridDim.x - 1) {
-            ctl[0] = 0;
-            ctl[1] = 0;
-        }
+    // the block's flagged rows (rare), one at a time; flg / kth are block-uniform LDS reads
+    float* fixa = smem + KQ_HALVES * KQ_QPB * KB * 2 + 2 * KQ_QPB;
+    for (int f = 0; f < KQ_QPB; ++f) {
+        const int qf = qb * KQ_QPB + f;
+        if (flg[f] != 0 && qf < N)
+            knn_fix_row<NSTEP>(fixa, ib, xib, xx + (int64_t)b * N, N, k, qf, kth[f], (int64_t)b * N + qf, idx64,
+                               idx32, vals);
     }
 }
 
@@ -769,9 +659,8 @@ int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
                    float* img, float* xximg, hipStream_t st) {
     const int ntile = knn_ntile(N);
     const int tgroups = (ntile + KI_TILES - 1) / KI_TILES;
-    int* ctl = reinterpret_cast<int*>(xximg + (size_t)B * knn_xximg_floats(N));
     hipLaunchKernelGGL(knn_image_kernel<NSTEP>, dim3((unsigned)(B * tgroups)), dim3(256), 0, st, x, sB, sC, sN, B, C,
-                       N, order, ntile, tgroups, xx, img, xximg, ctl);
+                       N, order, ntile, tgroups, xx, img, xximg);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -780,12 +669,8 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
                hipStream_t st) {
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
-    int* ctl = const_cast<int*>(reinterpret_cast<const int*>(xximg + (size_t)B * knn_xximg_floats(N)));
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
-                       xximg, xx, B, N, k, nqb, idx64, idx32, vals, ctl);
-    if (hipGetLastError() != hipSuccess) return DGX_ELAUNCH;
-    hipLaunchKernelGGL(knn_fix_kernel, dim3(FIX_BLOCKS), dim3(256), 0, st, x, sB, sC, sN, xx, img, NSTEP, B, C, N,
-                       k, idx64, idx32, vals, ctl);
+                       xximg, xx, B, N, k, nqb, idx64, idx32, vals);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -838,8 +723,8 @@ int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
 
 size_t dgx_knn_image_bytes(int B, int C, int N) {
     if (B < 0 || C < 1 || N < 1) return 0;
-    // operand image | |x|^2 image | fix-up control words + row list
-    return ((size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) + knn_ctl_words(B, N)) * sizeof(float);
+    // operand image | |x|^2 image
+    return (size_t)B * (knn_image_floats(C, N) + knn_xximg_floats(N)) * sizeof(float);
 }
 
 size_t dgx_knn_workspace_bytes(int B, int C, int N) {

@@ -36,9 +36,8 @@ def test_version_and_errors():
     # argument validation happens before any device work
     assert L.dgx_knn_f32(None, 0, 0, 0, 1, 3, 8, 2, 0, None, None, None, 0, None) == -1
     # |x|^2 (B*N floats) + operand image (64 tiles x 64 lanes x 16 floats + 64 x 16 norms per cloud at C=64)
-    # + fix-up words: 4 control words, the row list (B*N), split-row counters (2 x 64) and candidates (2 x 64 x 256)
-    assert L.dgx_knn_workspace_bytes(2, 64, 1024) == 2 * 1024 * 4 + (2 * (64 * 64 * 16 + 64 * 16) + 4 + 2048 + 2 * 64 + 2 * 64 * 256) * 4
-    assert L.dgx_knn_image_bytes(2, 3, 1000) == (2 * (63 * 64 * 1 + 63 * 16) + 4 + 2000 + 2 * 64 + 2 * 64 * 256) * 4
+    assert L.dgx_knn_workspace_bytes(2, 64, 1024) == 2 * 1024 * 4 + 2 * (64 * 64 * 16 + 64 * 16) * 4
+    assert L.dgx_knn_image_bytes(2, 3, 1000) == 2 * (63 * 64 * 1 + 63 * 16) * 4
 
 
 def test_cpu_tensors_rejected():
