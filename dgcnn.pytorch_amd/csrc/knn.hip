@@ -149,8 +149,9 @@ __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[
 // its row, which is recomputed exactly (knn_fix_row).
 template <int KB>
 struct KnnList {
-    // (KL 10 / 9 at KB 20 measured: fewer insertion VALU, but the rows they flag
-    // cost more in the fix-up than the lists save)
+    // (KL 10 / 11 at KB 20 measured with the in-block fix-up: 87 -> 98 / 87 us
+    // at C = 64, 154 -> 184 / 167 us at C = 128 — the rows they flag cost more
+    // than the shorter insertion rounds save)
     static constexpr int KL = KB <= 16 ? 10 : (KB <= 20 ? 12 : (KB <= 32 ? 15 : (KB <= 40 ? 17 : 23)));
     static constexpr int RPL = (KB + 3) / 4;   // ranks per lane of a wave's 4-list merge
 };
