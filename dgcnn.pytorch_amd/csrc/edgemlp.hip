@@ -517,6 +517,337 @@ __global__ __launch_bounds__(256) void emlp_fwd_kernel(
     }
 }
 
+// ---- fused backward (bf16 mode) of conv2 + LReLU/BN1: per edge row e = (i, s)
+//   z2   = W2 h1_e                         (recomputed, h1 rebuilt from P_j, Q_i)
+//   dZ2  = c1 z2 + c0 + [arg_i == s] a2 dz_i   (BN2 backward; rounded to bf16
+//                                             as the unfused path stores it)
+//   dH1  = W2^T dZ2,  g = dH1 LReLU'(z1)  -> gE (bf16) + BN1-backward partials
+// with z2 and dZ2 living only in registers: the chain runs TRANSPOSED,
+// z2^T = W2 h1^T (A = W2 rows, B = the h1 fragments the forward builds), so
+// each lane's z2^T accumulators (4 consecutive c2 of one edge per 16-row tile)
+// are, after the BN2 backward and a bf16 pack, exactly the B fragments of
+// dH1^T = W2^T dZ2^T when W2^T's K columns are taken in the same permuted c2
+// order (wt below): no LDS round trip, no HBM for z2 / dZ2 / dH1.
+// A pair of waves (one block) takes EMB_PPB points; wave `half` holds c2 in
+// [64 half, 64 half + 64) and forms a partial dH1^T over its c2; the pair adds
+// the partials through LDS (double-buffered by tile parity: one barrier per
+// tile) and wave `half` finishes c1 tiles 2 half, 2 half + 1.
+// dW2 = sum_e dZ2_e h1_e^T is accumulated in the same pass: the tile's dZ2 and
+// h1 rows are written to LDS as [edge][channel] and read back with the gfx950
+// transposing read (ds_read_b64_tr_b16) as 16x16x16 MFMA operands whose K is
+// the 16 edges; wave `half` owns dW2 rows c2 in its half. Blocks of a cloud
+// stay on one XCD (its P rows are L2-resident); partial-stat / dW2-slab row =
+// block.
+constexpr int EMB_PPB = 64;
+constexpr int EMB_DZW = (128 + 8) / 2;  // words per LDS dZ2 row (16-bit, padded)
+constexpr int EMB_HW = (64 + 8) / 2;    // words per LDS h1 row
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+// Transposed 16x16x16 operand from a row-major [16][*] 16-bit LDS tile: lane
+// (g, i) gets t[4 g + q][c0 + i], q = 0..3 (K = tile row, M/N = column). Lane
+// 4q + p of a 16-lane group supplies the address of row 4g + q, columns 4p..
+__device__ __forceinline__ s16x4_t lds_tr4(const uint32_t* t, int rsw, int c0, int lane) {
+#ifdef DGX_EMB_TR_SCALAR
+    const int g = lane >> 4, i = lane & 15;
+    const short* e = reinterpret_cast<const short*>(t);
+    return s16x4_t{e[(4 * g + 0) * 2 * rsw + c0 + i], e[(4 * g + 1) * 2 * rsw + c0 + i],
+                   e[(4 * g + 2) * 2 * rsw + c0 + i], e[(4 * g + 3) * 2 * rsw + c0 + i]};
+#else
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(t + (4 * g + q) * rsw + (c0 + 4 * p) / 2));
+#endif
+}
+
+// One wave of the pair; HALF (the wave's c2 half) is a template constant so
+// every register-array index below is static (a runtime half made each such
+// access a select chain: ~1100 VALU per tile instead of ~300).
+template <int KT, int HALF>
+__device__ __forceinline__ void emlp_bwd_wave(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int N, int k, int tiles, int b,
+    int tile, const float* __restrict__ scale1, float slope1, const __bf16* __restrict__ W2,
+    const float* __restrict__ dz, const uint8_t* __restrict__ arg, __bf16* __restrict__ gE,
+    float* __restrict__ part1, float* __restrict__ dw2slab, float (*xch)[2][2][4][64],
+    uint32_t (*dzt)[16 * EMB_DZW], uint32_t (*h1t)[16 * EMB_HW], const float* cst) {
+    constexpr int C1 = 64, C2 = 128, NTW = 4;
+    constexpr int half = HALF;
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, r16 = lane & 15;
+    // A fragments of W2 (z2^T = W2 h1^T): rows c2 = (4 half + ct) * 16 + r16, K = c1 32 ks + 8 g ..
+    bf16x8_t wf[NTW][2];
+#pragma unroll
+    for (int ct = 0; ct < NTW; ++ct)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+            wf[ct][ks] = *reinterpret_cast<const bf16x8_t*>(W2 + ((4 * half + ct) * 16 + r16) * C1 + ks * 32 + 8 * g);
+    // A fragments of W2^T over this wave's c2 half, K slots in the z2^T register
+    // order: slot 8 g + t of step kk is c2 = 64 half + 32 kk + 16 (t / 4) + 4 g + t % 4
+    bf16x8_t wt[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                wt[mt][kk][t] = W2[(64 * half + 32 * kk + 16 * (t >> 2) + 4 * g + (t & 3)) * C1 + 16 * mt + r16];
+    // h1 build (as emlp_fwd_kernel): channels 32 ks + 8 g + u
+    float a1[2][8];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) ld8(scale1 + ks * 32 + 8 * g, a1[ks]);
+    float t1[2][4], t2[2][4];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { t1[jt][r] = 0.f; t2[jt][r] = 0.f; }
+    // dW2 rows c2 = 64 half + 16 ct + 4 g + r, columns c1 = 16 nt + r16
+    f32x4_t wacc[NTW][4];
+#pragma unroll
+    for (int ct = 0; ct < NTW; ++ct)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) wacc[ct][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int64_t cbase = (int64_t)b * N;
+    const int n0 = tile * EMB_PPB;
+    const int np = max(0, min(EMB_PPB, N - n0));
+    int par = 0;  // exchange buffer parity
+    // Software pipeline: the next tile's P_j rows are loaded during the current
+    // tile, the next point's ids / Q_i / dz / slots during the current point
+    // (a tile's own gather would otherwise cost two dependent L2 round trips).
+    int jv[KT], jn[KT];
+    float qr[2][8], qen[2][4];  // next point's raw Q_i (h1 channels, epilogue channels)
+    float4 dzn[NTW];
+    uint32_t sln[NTW];
+    auto load_point = [&](int pp) {
+        const int64_t i = cbase + n0 + pp;
+#pragma unroll
+        for (int rt = 0; rt < KT; ++rt) jn[rt] = idx[i * k + min(rt * 16 + r16, k - 1)];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) ld8(PQ + i * ldpq + C1 + ks * 32 + 8 * g, qr[ks]);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const float4 v = ld4(PQ + i * ldpq + C1 + 16 * (2 * half + jt) + 4 * g);
+            qen[jt][0] = v.x; qen[jt][1] = v.y; qen[jt][2] = v.z; qen[jt][3] = v.w;
+        }
+#pragma unroll
+        for (int ct = 0; ct < NTW; ++ct) {
+            const int c = 64 * half + 16 * ct + 4 * g;
+            dzn[ct] = ld4(dz + i * C2 + c);
+            sln[ct] = *reinterpret_cast<const uint32_t*>(arg + i * C2 + c);
+        }
+    };
+    float pbn[2][8], pen[2][4];  // next tile's P_j (h1 channels, epilogue channels)
+    auto load_p = [&](int j) {
+        const float* __restrict__ pj = PQ + (cbase + j) * ldpq;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) ld8(pj + ks * 32 + 8 * g, pbn[ks]);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            const float4 v = ld4(pj + 16 * (2 * half + jt) + 4 * g);
+            pen[jt][0] = v.x; pen[jt][1] = v.y; pen[jt][2] = v.z; pen[jt][3] = v.w;
+        }
+    };
+    float qb[2][8], T[NTW][4], qe[2][4];
+    uint32_t sl[NTW];
+    if (np > 0) {
+        load_point(0);
+        load_p(jn[0]);
+    }
+#pragma unroll 1
+    for (int pp = 0; pp < np; ++pp) {
+        const int64_t i = cbase + n0 + pp;
+        // this point's state from the prefetched raw values
+        {
+            float b1[2][8];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) ld8(cst + 3 * C2 + C1 + ks * 32 + 8 * g, b1[ks]);  // shift1 (LDS)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) qb[ks][u] = fmaf(a1[ks][u], qr[ks][u], b1[ks][u]);
+        }
+#pragma unroll
+        for (int rt = 0; rt < KT; ++rt) jv[rt] = jn[rt];
+#pragma unroll
+        for (int ct = 0; ct < NTW; ++ct) {
+            const float4 a2 = *reinterpret_cast<const float4*>(cst + 2 * C2 + 64 * half + 16 * ct + 4 * g);
+            T[ct][0] = a2.x * dzn[ct].x; T[ct][1] = a2.y * dzn[ct].y;
+            T[ct][2] = a2.z * dzn[ct].z; T[ct][3] = a2.w * dzn[ct].w;
+            sl[ct] = sln[ct];
+        }
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) qe[jt][r] = qen[jt][r];
+        if (pp + 1 < np) load_point(pp + 1);
+#pragma unroll
+        for (int rt = 0; rt < KT; ++rt) {
+            const int s = rt * 16 + r16;
+            const bool valid = s < k;
+            float pb[2][8], pe[2][4];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) pb[ks][u] = pbn[ks][u];
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) pe[jt][r] = pen[jt][r];
+            if (rt + 1 < KT) load_p(jv[rt + 1]);
+            else if (pp + 1 < np) load_p(jn[0]);
+            bf16x8_t af[2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) af[ks][u] = (__bf16)lrelu(fmaf(a1[ks][u], pb[ks][u], qb[ks][u]), slope1);
+            // z2^T tiles: acc[ct][r] = z2[edge s][c2 = 64 half + 16 ct + 4 g + r]
+            f32x4_t acc[NTW];
+#pragma unroll
+            for (int ct = 0; ct < NTW; ++ct) {
+                acc[ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][ks], af[ks], acc[ct], 0, 0, 0);
+            }
+            // dZ2^T (bf16), packed as the B fragments of step kk = ct / 2
+            bf16x8_t dzb[2];
+#pragma unroll
+            for (int ct = 0; ct < NTW; ++ct) {
+                const int c = 64 * half + 16 * ct + 4 * g;
+                const float4 v0 = *reinterpret_cast<const float4*>(cst + c);
+                const float4 v1 = *reinterpret_cast<const float4*>(cst + C2 + c);
+                const float k0[4] = {v0.x, v0.y, v0.z, v0.w}, k1[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t slot = (sl[ct] >> (8 * r)) & 0xffu;
+                    float d = fmaf(k1[r], acc[ct][r], k0[r]) + (slot == (uint32_t)s ? T[ct][r] : 0.f);
+                    d = valid ? d : 0.f;
+                    dzb[ct >> 1][4 * (ct & 1) + r] = (__bf16)d;
+                }
+            }
+            // partial dH1^T over this wave's c2: dacc[mt][r] = dH1[edge s][c1 = 16 mt + 4 g + r]
+            f32x4_t dacc[4];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                dacc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+                    dacc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[mt][kk], dzb[kk], dacc[mt], 0, 0, 0);
+            }
+            // pair exchange: hand the partner its two c1 tiles, take ours; this
+            // tile's dZ2 (this wave's c2) and h1 (channels 32 half ..) rows to LDS
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xch[par][half][jt][r][lane] = dacc[2 * (1 - half) + jt][r];
+#pragma unroll
+            for (int ct = 0; ct < NTW; ++ct) {
+                // whole-vector bit cast (element-wise casts of the bf16 vector miscompile)
+                const uint4 w = __builtin_bit_cast(uint4, dzb[ct >> 1]);
+                *reinterpret_cast<uint2*>(dzt[par] + r16 * EMB_DZW + (64 * half + 16 * ct + 4 * g) / 2) =
+                    (ct & 1) ? make_uint2(w.z, w.w) : make_uint2(w.x, w.y);
+            }
+            *reinterpret_cast<bf16x8_t*>(h1t[par] + r16 * EMB_HW + (32 * half + 8 * g) / 2) = af[half];
+            __syncthreads();
+            // dW2 += dZ2^T h1 over the tile's 16 edges (padding edges carry dZ2 = 0)
+#pragma unroll
+            for (int ct = 0; ct < NTW; ++ct) {
+                const s16x4_t a = lds_tr4(dzt[par], EMB_DZW, 64 * half + 16 * ct, lane);
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+                    wacc[ct][nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, lds_tr4(h1t[par], EMB_HW, 16 * nt, lane),
+                                                                           wacc[ct][nt], 0, 0, 0);
+            }
+            float dh[2][4];
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dh[jt][r] = dacc[2 * half + jt][r] + xch[par][1 - half][jt][r][lane];
+            par ^= 1;
+            // g = dH1 LReLU'(z1) -> gE (bf16) and the BN1-backward partials
+            if (valid) {
+                __bf16* __restrict__ ge = gE + (i * k + s) * C1;
+#pragma unroll
+                for (int jt = 0; jt < 2; ++jt) {
+                    const int c = 16 * (2 * half + jt) + 4 * g;
+                    const float4 va = *reinterpret_cast<const float4*>(cst + 3 * C2 + c);
+                    const float4 vb = *reinterpret_cast<const float4*>(cst + 3 * C2 + C1 + c);
+                    const float4 vm = *reinterpret_cast<const float4*>(cst + 3 * C2 + 2 * C1 + c);
+                    const float4 vi = *reinterpret_cast<const float4*>(cst + 3 * C2 + 3 * C1 + c);
+                    const float ea[4] = {va.x, va.y, va.z, va.w}, eb[4] = {vb.x, vb.y, vb.z, vb.w};
+                    const float em[4] = {vm.x, vm.y, vm.z, vm.w}, ei[4] = {vi.x, vi.y, vi.z, vi.w};
+                    bf16x4_t h;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float y = pe[jt][r] + qe[jt][r];
+                        const float z = fmaf(ea[r], y, eb[r]);
+                        const float gv = dh[jt][r] * (z > 0.f ? 1.f : slope1);
+                        t1[jt][r] += gv;
+                        t2[jt][r] = fmaf(gv, (y - em[r]) * ei[r], t2[jt][r]);
+                        h[r] = (__bf16)gv;
+                    }
+                    *reinterpret_cast<bf16x4_t*>(ge + 16 * (2 * half + jt) + 4 * g) = h;
+                }
+            }
+        }
+    }
+    // BN1 partials: sum over the 16 edge lanes, lanes r16 == 0 write
+    const int prow = b * tiles + tile;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v1 = t1[jt][r], v2 = t2[jt][r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                v1 += __shfl_xor(v1, o);
+                v2 += __shfl_xor(v2, o);
+            }
+            if (r16 == 0) {
+                const int c = 16 * (2 * half + jt) + 4 * g + r;
+                part1[(int64_t)prow * 2 * C1 + c] = v1;
+                part1[(int64_t)prow * 2 * C1 + C1 + c] = v2;
+            }
+        }
+    float* __restrict__ ws = dw2slab + (int64_t)prow * C2 * C1;
+#pragma unroll
+    for (int ct = 0; ct < NTW; ++ct)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ws[(64 * half + 16 * ct + 4 * g + r) * C1 + 16 * nt + r16] = wacc[ct][nt][r];
+}
+
+template <int KT>
+__global__ __launch_bounds__(128) void emlp_bwd_kernel(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int B, int N, int k, int tiles,
+    const float* __restrict__ scale1, const float* __restrict__ shift1, const float* __restrict__ mean1,
+    const float* __restrict__ invstd1, float slope1, const __bf16* __restrict__ W2, const float* __restrict__ dz,
+    const uint8_t* __restrict__ arg, const float* __restrict__ consts2, __bf16* __restrict__ gE,
+    float* __restrict__ part1, float* __restrict__ dw2slab) {
+    constexpr int C1 = 64, C2 = 128;
+    __shared__ float xch[2][2][2][4][64];  // [tile parity][from wave][its tile j][r][lane]
+    __shared__ __attribute__((aligned(16))) uint32_t dzt[2][16 * EMB_DZW];  // [parity][edge][c2] bf16
+    __shared__ __attribute__((aligned(16))) uint32_t h1t[2][16 * EMB_HW];   // [parity][edge][c1] bf16
+    // block constants in LDS (read back as 4-lane broadcasts): BN2-backward
+    // [c0 | c1 | a2] (3 x C2) and BN1 [scale | shift | mean | invstd] (4 x C1)
+    __shared__ __attribute__((aligned(16))) float cst[3 * C2 + 4 * C1];
+    int b, tile;
+    if (!dgx_xcd_cloud_map(blockIdx.x, B, tiles, b, tile)) return;
+    for (int t = threadIdx.x; t < 3 * C2; t += 128) cst[t] = consts2[t];
+    for (int t = threadIdx.x; t < C1; t += 128) {
+        cst[3 * C2 + t] = scale1[t];
+        cst[3 * C2 + C1 + t] = shift1[t];
+        cst[3 * C2 + 2 * C1 + t] = mean1[t];
+        cst[3 * C2 + 3 * C1 + t] = invstd1[t];
+    }
+    __syncthreads();
+    if (threadIdx.x >> 6)
+        emlp_bwd_wave<KT, 1>(PQ, ldpq, idx, N, k, tiles, b, tile, scale1, slope1, W2, dz, arg, gE, part1, dw2slab, xch,
+                             dzt, h1t, cst);
+    else
+        emlp_bwd_wave<KT, 0>(PQ, ldpq, idx, N, k, tiles, b, tile, scale1, slope1, W2, dz, arg, gE, part1, dw2slab, xch,
+                             dzt, h1t, cst);
+}
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
@@ -579,6 +910,43 @@ int dgx_edge_mlp_fused_fwd_bf16(const float* PQ, int ldpq, const int32_t* idx, i
         }
     }
 #undef DGX_EMF
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_mlp_fused_bwd_rows(int B, int N) {
+    if (B < 1 || N < 1) return DGX_EINVAL;
+    return B * ((N + EMB_PPB - 1) / EMB_PPB);
+}
+
+int dgx_edge_mlp_fused_bwd_bf16(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1, int C2,
+                                const float* scale1, const float* shift1, const float* mean1, const float* invstd1,
+                                float slope1, const void* W2, const float* dz, const uint8_t* arg,
+                                const float* consts2, void* gE, float* part1, float* dw2slab, int nrows,
+                                void* stream) {
+    if (!PQ || !idx || !scale1 || !shift1 || !mean1 || !invstd1 || !W2 || !dz || !arg || !consts2 || !gE || !part1 ||
+        !dw2slab)
+        return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || ldpq < 2 * C1) return DGX_EINVAL;
+    if (C1 != 64 || C2 != 128 || k > 64 || ldpq % 4 || !al16(PQ) || !al16(scale1) || !al16(shift1) || !al16(mean1) ||
+        !al16(invstd1) || !al16(W2) || !al16(dz) || !al16(consts2) || (reinterpret_cast<uintptr_t>(arg) & 3) ||
+        (reinterpret_cast<uintptr_t>(gE) & 7))
+        return DGX_EUNSUPPORTED;
+    const int tiles = (N + EMB_PPB - 1) / EMB_PPB;
+    if (nrows != B * tiles) return DGX_EINVAL;
+    const dim3 grid(dgx_xcd_cloud_grid(B, tiles));
+    const __bf16* w = static_cast<const __bf16*>(W2);
+    __bf16* ge = static_cast<__bf16*>(gE);
+    hipStream_t st = dgx_stream(stream);
+#define DGX_EMB(KTV)                                                                                              \
+    hipLaunchKernelGGL((emlp_bwd_kernel<KTV>), grid, dim3(128), 0, st, PQ, ldpq, idx, B, N, k, tiles, scale1, shift1, \
+                       mean1, invstd1, slope1, w, dz, arg, consts2, ge, part1, dw2slab)
+    switch ((k + 15) / 16) {
+        case 1: DGX_EMB(1); break;
+        case 2: DGX_EMB(2); break;
+        case 3: DGX_EMB(3); break;
+        default: DGX_EMB(4); break;
+    }
+#undef DGX_EMB
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -90,6 +90,9 @@ _SIGS = {
                     + [_vp, _i64, _i64, _i64] * 3 + [_vp],
     "dgx_attn_dropout_mask": [_i64, _i32, _f32, ctypes.c_uint64, _vp, _vp],
     "dgx_edge_mlp_fused_rows": [_i32, _i32],
+    "dgx_edge_mlp_fused_bwd_rows": [_i32, _i32],
+    "dgx_edge_mlp_fused_bwd_bf16": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_gemm_dz2_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp],
     "dgx_edge_mlp_fused_fwd_bf16": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp,
                                     _vp, _i32, _vp, _vp],

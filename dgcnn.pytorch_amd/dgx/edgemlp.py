@@ -25,6 +25,16 @@ from . import precision as prec
 from .edgeconv import edge_select, split_weight
 from .ops import knn_raw, reduction_order
 
+# bf16 mode, C1 = 64 / C2 = 128 (PositionEmbedding): one backward kernel for
+# conv2 + LReLU/BN1 (dgx_edge_mlp_fused_bwd_bf16: z2, dZ2, dH1 and dW2 in
+# registers / LDS, h1 rebuilt from PQ), so the forward does not store h1.
+# False keeps the unfused GEMM path (dZ2 / dH1 / dW2 GEMMs over a stored h1).
+FUSED_BWD = True
+
+
+def _fused_bwd_ok(bf16, C1, C2, k):
+    return FUSED_BWD and bf16 and C1 == 64 and C2 == 128 and k <= 64
+
 
 class _EdgeMLP2(torch.autograd.Function):
     @staticmethod
@@ -65,7 +75,9 @@ class _EdgeMLP2(torch.autograd.Function):
                 wprep = G.prep_weight(w2, C2, C1, False)
                 dir2 = torch.where(g2 < 0, -1.0, 1.0).to(torch.float32).contiguous()
                 W2d = (W2 * dir2.view(C2, 1)).to(torch.bfloat16).contiguous()
-                H1 = torch.empty((E, C1), dtype=torch.bfloat16, device=dev) if need_grad else None
+                # h1 (bf16) for the unfused backward's GEMMs; the fused backward rebuilds it
+                keep_h1 = need_grad and not _fused_bwd_ok(bf16, C1, C2, k)
+                H1 = torch.empty((E, C1), dtype=torch.bfloat16, device=dev) if keep_h1 else None
                 rows2 = L.dgx_edge_mlp_fused_rows(B, N)
                 part2 = torch.empty((rows2, 2, C2), dtype=torch.float32, device=dev)
                 ysel = torch.empty((M, C2), dtype=torch.float32, device=dev)
@@ -144,6 +156,7 @@ class _EdgeMLP2(torch.autograd.Function):
         L = nat.lib()
         stream = nat.stream_of(X)
         fused = Z2 is None  # fused forward: z2 was never stored
+        fused_bwd = fused and H1 is None  # ... and h1 neither: the fused backward kernel
         z16 = fused or Z2.dtype == torch.bfloat16
         dY = dout.float().permute(0, 2, 1).reshape(M, C2).contiguous()
         with torch.cuda.device(dev):
@@ -155,7 +168,22 @@ class _EdgeMLP2(torch.autograd.Function):
                                             nat.f32(st2.shift), nat.f32(st2.mean), nat.f32(st2.invstd), slope2,
                                             nat.f32(dz), nat.f32(part), nblk, stream), "edge bwd dz")
             dg2, db2, c0, c1 = bn_.backward_consts(part, nblk, float(E), st2, stream)
-            if fused:
+            if fused_bwd:
+                # conv2 + LReLU/BN1 backward in one pass: gE, BN1 partials, dW2 slabs
+                rows = L.dgx_edge_mlp_fused_bwd_rows(B, N)
+                part1 = torch.empty((rows, 2, C1), dtype=torch.float32, device=dev)
+                slab = torch.empty((rows, C2, C1), dtype=torch.float32, device=dev)
+                gE = torch.empty((E, C1), dtype=torch.bfloat16, device=dev)
+                consts = torch.cat([c0, c1, st2.scale]).contiguous()
+                nat.check(L.dgx_edge_mlp_fused_bwd_bf16(
+                    nat.f32(PQ), 2 * C1, nat.i32(idx), B, N, k, C1, C2, nat.f32(st1.scale), nat.f32(st1.shift),
+                    nat.f32(st1.mean), nat.f32(st1.invstd), slope1, nat.bf16(ctx.wprep[0]), nat.f32(dz), nat.u8(arg),
+                    nat.f32(consts), nat.bf16(gE), nat.f32(part1), nat.f32(slab), rows, stream), "edge mlp fused bwd")
+                gw2 = torch.empty((C2, C1), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_slab_reduce_f32(nat.f32(slab), rows, C2, C1, C2, nat.f32(gw2), C1, stream),
+                          "dW2 slab reduce")
+                g16 = 1
+            elif fused:
                 # z2 recomputed from h1 on the MFMA, BN2 backward in the GEMM's epilogue:
                 # dZ2 = c1 z2 + c0 + [slot] a2 dz, stored bf16 (z2 never reaches HBM)
                 dZ2 = torch.empty((E, C2), dtype=torch.bfloat16, device=dev)
@@ -168,8 +196,10 @@ class _EdgeMLP2(torch.autograd.Function):
                                                 k, C2, nat.f32(st2.scale), nat.f32(c0), nat.f32(c1),
                                                 nat.ptr(dZ2, nat.F32, nat.BF16), stream), "edge dz2")
             # ---- conv2 GEMMs: dH1 = dZ2 W2, dW2 = dZ2^T H1; then LReLU + BN1 backward
-            gw2 = torch.empty((C2, C1), dtype=torch.float32, device=dev)
-            if ctx.wprep is not None and z16 and C1 == 64:
+            if fused_bwd:
+                pass
+            elif ctx.wprep is not None and z16 and C1 == 64:
+                gw2 = torch.empty((C2, C1), dtype=torch.float32, device=dev)
                 # dH1 never leaves the GEMM tile: its epilogue forms g = dH1 LReLU'(z1) (bf16)
                 # and the BN1-backward column partials
                 G.lds_atb(dZ2, H1, gw2)
@@ -182,6 +212,7 @@ class _EdgeMLP2(torch.autograd.Function):
                     nat.bf16(gE), nat.f32(part1), rows, stream), "edge h1 bwd gemm")
                 g16 = 1
             else:
+                gw2 = torch.empty((C2, C1), dtype=torch.float32, device=dev)
                 if ctx.wprep is not None and z16:
                     gE = G.lds_xwt(dZ2, ctx.wprep[1])
                     G.lds_atb(dZ2, H1, gw2)

@@ -347,6 +347,21 @@ int dgx_edge_mlp_fused_fwd_bf16(const float* PQ, int ldpq, const int32_t* idx, i
                                 const float* scale1, const float* shift1, float slope1, const void* W2d,
                                 const float* dir2, float* ysel, uint8_t* arg, float* partials, int nrows, void* H1,
                                 void* stream);
+/* bf16 mode, backward of the same stage (autograd of layers.py:48-52): with
+ * dz = dgx_edge_bwd_dz_f32 of the max's output gradient and consts2 =
+ * [c0 | c1 | a2] (BN2 backward, 3*C2 floats), per edge row e = (i, s):
+ *   z2 = W2 h1_e (h1 rebuilt from P_j, Q_i as the forward did), dZ2 = c1 z2 + c0
+ *   + [arg_i == s] a2 dz_i (bf16), dH1 = W2^T dZ2, g = dH1 LReLU'(z1) -> gE
+ *   (E x C1 bf16), BN1-backward partials part1 (nrows x 2 x C1) and dW2 =
+ *   sum_e dZ2_e h1_e^T per block in dw2slab (nrows x C2 x C1; reduce with
+ *   dgx_slab_reduce_f32). z2, dZ2, dH1 and h1 never reach HBM. W2: bf16
+ *   (C2 x C1). C1 = 64, C2 = 128, k <= 64; nrows = dgx_edge_mlp_fused_bwd_rows. */
+int dgx_edge_mlp_fused_bwd_rows(int B, int N);
+int dgx_edge_mlp_fused_bwd_bf16(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int C1, int C2,
+                                const float* scale1, const float* shift1, const float* mean1, const float* invstd1,
+                                float slope1, const void* W2, const float* dz, const uint8_t* arg,
+                                const float* consts2, void* gE, float* part1, float* dw2slab, int nrows,
+                                void* stream);
 int dgx_edge_mlp_scatter_f32(const void* g, int g_bf16, const float* PQ, int ldpq, const float* sumP,
                              const int32_t* rowptr, const int32_t* edges, int B, int N, int k, int C1,
                              const float* scale, const float* c0, const float* c1, float* dPQ, void* stream);
