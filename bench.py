@@ -70,6 +70,8 @@ def parse(argv=None):
     p.add_argument("--no-edgeconv-leg", action="store_true", help="skip the EdgeConv-only fwd+bwd timing")
     p.add_argument("--no-posemb-leg", action="store_true",
                    help="skip the PositionEmbedding edge-MLP timing (partseg geometry)")
+    p.add_argument("--no-graph", action="store_true",
+                   help="N=1: time the eager-launched step instead of its HIP-graph replay")
     p.add_argument("--no-roofline-leg", action="store_true", help="skip the event-timed kNN region")
     p.add_argument("--no-attention-leg", action="store_true", help="skip the Net attention (f2) timing")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -431,8 +433,34 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # the same step with every launch issued from Python (autograd + ctypes):
+    # ~60 launches per step, so a slow or contended host can starve the GPU
+    elapsed_eager = reduce_elapsed(timed_region(step, args.steps, world), world, dev)
+    launch = "eager"
+    run = step
+    if world == 1 and not args.no_graph:
+        # one HIP graph per train step (fwd + bwd + SGD, the same kernels and
+        # buffers as the eager step, captured once): replay issues the whole step
+        # with one launch, independent of host speed. Grads are None when the
+        # capture starts, so backward writes fresh gradient buffers (graph pool)
+        # on every replay, as zero_grad(set_to_none=True) + backward does.
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            net(x).backward(gy)
+            opt.step()
+        run = graph.replay
+        for _ in range(2):
+            run()
+        launch = "hip_graph"
     # headline: the timed region runs uninstrumented
-    elapsed = reduce_elapsed(timed_region(step, args.steps, world), world, dev)
+    elapsed = reduce_elapsed(timed_region(run, args.steps, world), world, dev)
     result = {
         "metric": METRIC,
         "value": round(total * args.steps / elapsed, 2),
@@ -441,6 +469,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "launch": launch,
+        "eager_launch_ms_per_step": round(elapsed_eager / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,

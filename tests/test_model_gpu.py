@@ -125,3 +125,48 @@ def test_dgcnn_semseg_stages_match_stock_ops(cuda):
         assert rel_err(x3.view(2, 1024, -1).permute(0, 2, 1).cpu(), r3.cpu()) < TOL
     y.square().mean().backward()
     assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+@pytest.mark.parametrize("precision_mode", ["bf16", "fp32"])
+def test_dgcnn_train_step_graph_replay_equals_eager(cuda, precision_mode):
+    """bench.py times the N=1 train step as one HIP-graph replay (torch.cuda.CUDAGraph
+    capture of fwd + bwd + SGD): every engine launch goes to the capture stream,
+    nothing syncs the host, and one replay from a given state gives bit-for-bit
+    the parameters and BN statistics of one eager step from that state."""
+    from dgx import precision, synth
+    from models.dgcnn import DGCNN
+    torch.manual_seed(3)
+    precision.set(precision_mode)
+    try:
+        m = DGCNN(types.SimpleNamespace(emb_dim=256, k=20)).to(cuda).train()
+        init = copy.deepcopy(m.state_dict())
+        opt = torch.optim.SGD(m.parameters(), lr=0.05)
+        x = torch.from_numpy(synth.cube_clouds(4, 512, 1)).to(cuda).permute(0, 2, 1)
+        gy = torch.from_numpy(synth.uniform(2, (4, 256, 512)) - 0.5).float().to(cuda)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            m(x).backward(gy)
+            opt.step()
+
+        side = torch.cuda.Stream(cuda)
+        side.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream(cuda).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            m(x).backward(gy)
+            opt.step()
+        m.load_state_dict(init)  # in place: the captured buffers stay valid
+        graph.replay()
+        torch.cuda.synchronize()
+        replayed = {n: t.clone() for n, t in m.state_dict().items()}
+        m.load_state_dict(init)
+        step()
+        torch.cuda.synchronize()
+        for n, t in m.state_dict().items():
+            assert torch.equal(t, replayed[n]), n
+    finally:
+        precision.set("fp32")
