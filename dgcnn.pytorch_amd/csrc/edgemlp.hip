@@ -303,23 +303,50 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
         float igv[EM_U], iqv[EM_U];
 #pragma unroll
         for (int u = 0; u < EM_U; ++u) { igv[u] = 0.f; iqv[u] = 0.f; }
-        int32_t r = beg;
-        for (; r + EM_U <= end; r += EM_U) {
-            int32_t id[EM_U];
+        // the in-edge ids come in with one load per 64 (lane u holds id u of the
+        // chunk) and are broadcast with readlane: no dependent id load per batch
+        // (needs every lane active: C1 a multiple of 64; else one id load per batch)
+        if (C1 % 64 != 0) {
+            int32_t r = beg;
+            for (; r + EM_U <= end; r += EM_U) {
+                int32_t id[EM_U];
 #pragma unroll
-            for (int u = 0; u < EM_U; ++u) id[u] = edges[r + u];
+                for (int u = 0; u < EM_U; ++u) id[u] = edges[r + u];
 #pragma unroll
-            for (int u = 0; u < EM_U; ++u) {
-                const int64_t src = (int64_t)(id[u] >> 6);
-                igv[u] += (float)g[(src * k + (id[u] & 63)) * C1 + c];
-                iqv[u] += PQ[src * ldpq + C1 + c];
+                for (int u = 0; u < EM_U; ++u) {
+                    const int64_t src = (int64_t)(id[u] >> 6);
+                    igv[u] += (float)g[(src * k + (id[u] & 63)) * C1 + c];
+                    iqv[u] += PQ[src * ldpq + C1 + c];
+                }
+            }
+            for (; r < end; ++r) {
+                const int32_t id = edges[r];
+                const int64_t src = (int64_t)(id >> 6);
+                igv[0] += (float)g[(src * k + (id & 63)) * C1 + c];
+                iqv[0] += PQ[src * ldpq + C1 + c];
             }
         }
-        for (; r < end; ++r) {
-            const int32_t id = edges[r];
-            const int64_t src = (int64_t)(id >> 6);
-            igv[0] += (float)g[(src * k + (id & 63)) * C1 + c];
-            iqv[0] += PQ[src * ldpq + C1 + c];
+        for (int32_t r0 = beg; C1 % 64 == 0 && r0 < end; r0 += 64) {
+            const int cnt = min(64, (int)(end - r0));
+            const int32_t mine = lane < cnt ? edges[r0 + lane] : 0;
+            int u0 = 0;
+            for (; u0 + EM_U <= cnt; u0 += EM_U) {
+                int32_t id[EM_U];
+#pragma unroll
+                for (int u = 0; u < EM_U; ++u) id[u] = __builtin_amdgcn_readlane(mine, u0 + u);
+#pragma unroll
+                for (int u = 0; u < EM_U; ++u) {
+                    const int64_t src = (int64_t)(id[u] >> 6);
+                    igv[u] += (float)g[(src * k + (id[u] & 63)) * C1 + c];
+                    iqv[u] += PQ[src * ldpq + C1 + c];
+                }
+            }
+            for (; u0 < cnt; ++u0) {
+                const int32_t id = __builtin_amdgcn_readlane(mine, u0);
+                const int64_t src = (int64_t)(id >> 6);
+                igv[0] += (float)g[(src * k + (id & 63)) * C1 + c];
+                iqv[0] += PQ[src * ldpq + C1 + c];
+            }
         }
         float sg = 0.f, ig = 0.f, iq = 0.f;
 #pragma unroll
