@@ -9,7 +9,7 @@ REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH=(python3 "$REPO/bench.py" --no-graph --no-cpu-baseline --no-eager-baseline --no-posemb-leg --no-edgeconv-leg
+BENCH=(python3 "$REPO/bench.py" --no-graph --no-cpu-baseline --no-eager-baseline --no-posemb-leg --no-edgeconv-leg --no-attention-leg
        --no-fp32-leg "$@")
 cd /tmp || exit 1
 echo "== kernel trace: ${BENCH[*]}"
