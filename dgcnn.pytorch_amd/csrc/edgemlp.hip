@@ -575,15 +575,8 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 // (g, i) gets t[4 g + q][c0 + i], q = 0..3 (K = tile row, M/N = column). Lane
 // 4q + p of a 16-lane group supplies the address of row 4g + q, columns 4p..
 __device__ __forceinline__ s16x4_t lds_tr4(const uint32_t* t, int rsw, int c0, int lane) {
-#ifdef DGX_EMB_TR_SCALAR
-    const int g = lane >> 4, i = lane & 15;
-    const short* e = reinterpret_cast<const short*>(t);
-    return s16x4_t{e[(4 * g + 0) * 2 * rsw + c0 + i], e[(4 * g + 1) * 2 * rsw + c0 + i],
-                   e[(4 * g + 2) * 2 * rsw + c0 + i], e[(4 * g + 3) * 2 * rsw + c0 + i]};
-#else
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(t + (4 * g + q) * rsw + (c0 + 4 * p) / 2));
-#endif
 }
 
 // One wave of the pair; HALF (the wave's c2 half) is a template constant so

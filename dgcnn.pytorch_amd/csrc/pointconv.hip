@@ -300,10 +300,7 @@ __global__ __launch_bounds__(256) void bwd16_dz_lt_kernel(const float* __restric
 // PASS 0 with the transposed tile over RS_LT consecutive 128-point tiles per
 // block: per-thread sums over its 4 points, then over the 32 lanes of its
 // channel group (one shuffle tree), one partial row per block.
-#ifndef DGX_RS_LT
-#define DGX_RS_LT 2
-#endif
-constexpr int RS_LT = DGX_RS_LT;
+constexpr int RS_LT = 2;
 __global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __restrict__ dout,
                                                              const bf16* __restrict__ Z, int N, int C,
                                                              const float* __restrict__ scale,
