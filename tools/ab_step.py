@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--points", type=int, default=1024)
+    ap.add_argument("--graph", action="store_true", help="time HIP-graph replays (one capture per variant)")
     a = ap.parse_args()
     import torch
 
@@ -49,13 +50,28 @@ def main():
         opt.step()
 
     res = {v: [] for v in a.variants}
-    for v in a.variants:  # warm every variant
+    runs = {}
+    for v in a.variants:  # warm every variant (and capture its graph)
         apply(v)
         for _ in range(5):
             step()
+        runs[v] = step
+        if a.graph:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(g):
+                model(x).backward(gy)
+                opt.step()
+            runs[v] = g.replay
     for r in range(a.rounds):
         for v in a.variants:
             apply(v)
+            step = runs[v]
             step()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
