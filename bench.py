@@ -131,6 +131,21 @@ def reduce_elapsed(elapsed, world, dev):
     return float(t.item())
 
 
+def replicas_in_sync(model, world, dev):
+    """N > 1: every rank holds bitwise the same parameters after the timed steps
+    (fp64 checksum of all parameters, min == max over ranks). None at N = 1."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return None
+    with torch.no_grad():
+        c = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum().view(1)
+    lo, hi = c.clone(), c.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(lo.item() == hi.item())
+
+
 def sync_all(world):
     import torch
     import torch.distributed as dist
@@ -161,6 +176,22 @@ def _ms(fn, reps, warm=2):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
+def _ms_graph(fn, reps, warm=2):
+    """ms per call of ``fn`` captured once as a HIP graph and replayed (the
+    engine's GPU time, independent of the host's launch rate)."""
+    import torch
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(warm):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        fn()
+    return _ms(graph.replay, reps, warm=1)
+
+
 def edgeconv_legs(model, x, reps=10):
     """The metric's second number: the 4-block EdgeConv chain alone, fwd+bwd
     (train-mode BN, grads w.r.t. W, gamma, beta), and each block on its own
@@ -176,12 +207,23 @@ def edgeconv_legs(model, x, reps=10):
         if key not in g:
             g[key] = torch.randn(key, device=out.device)
         out.backward(g[key])
-    res = {"chain": round(_ms(lambda: run(x, blocks), reps), 3)}
+    res = {"timing": "HIP-graph replay of each leg (fwd+bwd)",
+           "chain": round(_ms_graph(lambda: run(x, blocks), reps), 3)}
     B, _, N = x.shape
+    # block i runs on the features block i-1 produces from the same input (the
+    # chain's own kNN graphs; random high-dimensional features would time the
+    # hub-heavy graphs of Gaussian data instead)
+    with torch.no_grad():
+        feats = edgeconv_stack(x, model.k, blocks)
+    off = 0
     for i, blk in enumerate(blocks):
         cin = blk[0].weight.shape[1] // 2
-        xi = x if i == 0 else torch.relu(torch.randn(B, cin, N, device=x.device))
-        res[f"block{i + 1}"] = round(_ms(lambda: run(xi, [blk]), reps), 3)
+        if i == 0:
+            xi = x
+        else:
+            xi = feats[:, off - cin:off].reshape(B, N, cin).permute(0, 2, 1).contiguous()
+        off += blk[0].weight.shape[0]
+        res[f"block{i + 1}"] = round(_ms_graph(lambda: run(xi, [blk]), reps), 3)
     return res
 
 
@@ -266,7 +308,8 @@ def posemb_edge_leg(dev, B=32, N=2048, k=40, reps=5):
         e2(e1(e)).max(dim=-1)[0].backward(g)
 
     out = {"config": f"B={B} N={N} k={k}, conv 6->64->128, train-mode BN, fwd+bwd"}
-    out["engine_ms"] = round(_ms(engine, reps, warm=1), 3)
+    out["engine_ms"] = round(_ms_graph(engine, reps, warm=1), 3)
+    out["engine_eager_launch_ms"] = round(_ms(engine, reps, warm=1), 3)
     try:
         out["torch_eager_gpu_ms"] = round(_ms(eager, reps, warm=1), 2)
         out["speedup"] = round(out["torch_eager_gpu_ms"] / out["engine_ms"], 2)
@@ -412,10 +455,20 @@ def main():
     torch.manual_seed(0)
     model = DGCNN(types.SimpleNamespace(emb_dim=args.emb, k=args.k, in_dims=args.in_dims)).to(dev).train()
     net = model
+    # N > 1 without SyncBN: each rank's fwd + bwd is one HIP graph accumulating
+    # every parameter gradient into ONE flat buffer, then ONE collective
+    # all-reduce of it (sum / N: DDP's averaging) and the fused SGD step; with
+    # --sync-bn (collectives inside the forward / backward) or --no-graph: DDP
+    flat_dp = world > 1 and not args.sync_bn and not args.no_graph
     if world > 1:
         if args.sync_bn:
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
-        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+        if flat_dp:
+            with torch.no_grad():  # replicas start identical (what DDP's constructor does)
+                for t in model.state_dict().values():
+                    dist.broadcast(t, 0)
+        else:
+            net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
     try:  # one fused kernel for the whole parameter list (same math as the foreach form)
         opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
     except (RuntimeError, TypeError, ValueError):
@@ -425,11 +478,32 @@ def main():
 
     gy = upstream_grad((per_gpu, args.emb, args.points), dev)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        y = net(x)
-        y.backward(gy)
-        opt.step()
+    if flat_dp:
+        params = [p for p in model.parameters() if p.requires_grad]
+        flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=dev)
+        off = 0
+        for p in params:  # every .grad is a view of the flat buffer: backward accumulates in place
+            p.grad = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+        def fwd_bwd():
+            flat.zero_()
+            net(x).backward(gy)
+
+        def reduce_and_step():
+            dist.all_reduce(flat)
+            flat.mul_(1.0 / world)
+            opt.step()
+
+        def step():
+            fwd_bwd()
+            reduce_and_step()
+    else:
+        def step():
+            opt.zero_grad(set_to_none=True)
+            y = net(x)
+            y.backward(gy)
+            opt.step()
 
     for _ in range(args.warmup):
         step()
@@ -459,6 +533,23 @@ def main():
         for _ in range(2):
             run()
         launch = "hip_graph"
+    elif flat_dp:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                fwd_bwd()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd_bwd()
+
+        def run():
+            graph.replay()
+            reduce_and_step()
+        for _ in range(2):
+            run()
+        launch = "hip_graph+allreduce"
     # headline: the timed region runs uninstrumented
     elapsed = reduce_elapsed(timed_region(run, args.steps, world), world, dev)
     result = {
@@ -471,6 +562,7 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "launch": launch,
         "eager_launch_ms_per_step": round(elapsed_eager / args.steps * 1e3, 3),
+        "replicas_in_sync": replicas_in_sync(model, world, dev),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,

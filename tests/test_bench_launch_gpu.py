@@ -34,6 +34,14 @@ def test_bench_self_launch_two_ranks_weak():
     assert r["n_gpus"] == 2 and r["scaling"] == "weak"
     assert r["config"]["global_batch"] == 8 and r["config"]["batch_per_gpu"] == 4
     assert r["value"] > 0 and r["config"]["parallelism"] == "dp2"
+    # fwd+bwd graph per rank + one all-reduce of the flat gradient buffer
+    assert r["launch"] == "hip_graph+allreduce" and r["replicas_in_sync"] is True
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launch_two_ranks_ddp():
+    r = _run(["--no-graph"])
+    assert r["n_gpus"] == 2 and r["launch"] == "eager" and r["replicas_in_sync"] is True
 
 
 @pytest.mark.timeout(300)
@@ -42,3 +50,4 @@ def test_bench_self_launch_two_ranks_strong_syncbn():
     assert r["n_gpus"] == 2 and r["scaling"] == "strong"
     assert r["config"]["global_batch"] == 4 and r["config"]["batch_per_gpu"] == 2
     assert r["config"]["parallelism"] == "dp2+syncbn"
+    assert r["launch"] == "eager" and r["replicas_in_sync"] is True
