@@ -541,7 +541,9 @@ def main():
                 fwd_bwd()
         torch.cuda.current_stream(dev).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread_local: the collective backend's watchdog thread may query events
+        # while this thread captures (a global capture mode would reject that)
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             fwd_bwd()
 
         def run():
