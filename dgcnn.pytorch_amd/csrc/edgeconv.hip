@@ -493,6 +493,49 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
     }
 }
 
+// The same dz and partials for a CHANNEL-major dY (B, Co, N) — the gradient of
+// a (B, C, N) module output that the engine keeps point-major (PositionEmbedding's
+// edge stage, layers.py:52): block = (cloud, 64-point tile) x 64-channel tile,
+// dY tile loaded along n (coalesced), transposed through LDS, then lanes =
+// channels as in edge_bwd_dz_kernel. Partial row = blockIdx.x.
+__global__ __launch_bounds__(256) void edge_bwd_dz_cm_kernel(
+    const float* __restrict__ dY, const float* __restrict__ ysel, int N, int Co, int ntn,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float slope, float* __restrict__ dz, float* __restrict__ partials) {
+    __shared__ float t[64][65];
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = blockIdx.x / ntn, n0 = (blockIdx.x - b * ntn) * 64, c0 = blockIdx.y * 64;
+    for (int r = wave; r < 64; r += 4) {
+        const int c = c0 + r, n = n0 + lane;
+        t[r][lane] = (c < Co && n < N) ? dY[((int64_t)b * Co + c) * N + n] : 0.f;
+    }
+    __syncthreads();
+    const int o = c0 + lane;
+    const bool ok = o < Co;
+    float acc1 = 0.f, acc2 = 0.f;
+    if (ok) {
+        const float a = scale[o], sh = shift[o], mu = mean[o], is = invstd[o];
+        for (int rr = wave; rr < 64 && n0 + rr < N; rr += 4) {
+            const int64_t i = (int64_t)b * N + n0 + rr;
+            const float y = ysel[i * Co + o];
+            const float z = fmaf(a, y, sh);
+            const float d = t[lane][rr] * (z > 0.f ? 1.f : slope);
+            dz[i * Co + o] = d;
+            acc1 += d;
+            acc2 = fmaf(d, (y - mu) * is, acc2);
+        }
+    }
+    red[0][wave][lane] = acc1;
+    red[1][wave][lane] = acc2;
+    __syncthreads();
+    if (wave == 0 && ok) {
+        partials[(int64_t)blockIdx.x * 2 * Co + o] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+        partials[(int64_t)blockIdx.x * 2 * Co + Co + o] =
+            red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const T* __restrict__ partials, int nrows,
                                                               int Co, double count, const float* __restrict__ scale,
@@ -1044,6 +1087,22 @@ int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, int M, int
     const int rows = (M + nrows - 1) / nrows;
     hipLaunchKernelGGL(edge_bwd_dz_kernel, dim3(nrows, (Co + 63) / 64), dim3(256), 0, dgx_stream(stream), dY, lddy,
                        ysel, M, Co, scale, shift, mean, invstd, slope, dz, partials, rows);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_bwd_dz_cm_rows(int B, int N) {
+    if (B < 1 || N < 1) return DGX_EINVAL;
+    return B * ((N + 63) / 64);
+}
+
+int dgx_edge_bwd_dz_cm_f32(const float* dY, const float* ysel, int B, int N, int Co, const float* scale,
+                           const float* shift, const float* mean, const float* invstd, float slope, float* dz,
+                           float* partials, int nrows, void* stream) {
+    if (!dY || !ysel || !scale || !shift || !mean || !invstd || !dz || !partials) return DGX_EINVAL;
+    if (B < 1 || N < 1 || Co < 1 || nrows != dgx_edge_bwd_dz_cm_rows(B, N)) return DGX_EINVAL;
+    const int ntn = (N + 63) / 64;
+    hipLaunchKernelGGL(edge_bwd_dz_cm_kernel, dim3(B * ntn, (Co + 63) / 64), dim3(256), 0, dgx_stream(stream), dY,
+                       ysel, N, Co, ntn, scale, shift, mean, invstd, slope, dz, partials);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

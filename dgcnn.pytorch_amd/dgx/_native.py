@@ -45,6 +45,8 @@ _SIGS = {
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
     "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp],
     "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
+    "dgx_edge_bwd_dz_cm_rows": [_i32, _i32],
+    "dgx_edge_bwd_dz_cm_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_graph_reverse": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_graph_reverse_multi": [_i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp],

@@ -158,15 +158,24 @@ class _EdgeMLP2(torch.autograd.Function):
         fused = Z2 is None  # fused forward: z2 was never stored
         fused_bwd = fused and H1 is None  # ... and h1 neither: the fused backward kernel
         z16 = fused or Z2.dtype == torch.bfloat16
-        dY = dout.float().permute(0, 2, 1).reshape(M, C2).contiguous()
+        dout = dout.float()
+        dY_pm = dout.permute(0, 2, 1)  # (B, N, C2): point-major if the gradient came that way
         with torch.cuda.device(dev):
             # ---- BN2 + LReLU backward at the selected edges, then dense over all edges
-            nblk = max(1, min(1024, (M + 63) // 64))
             dz = torch.empty((M, C2), dtype=torch.float32, device=dev)
-            part = torch.empty((nblk, 2, C2), dtype=torch.float32, device=dev)
-            nat.check(L.dgx_edge_bwd_dz_f32(nat.f32(dY), C2, nat.f32(ysel), M, C2, nat.f32(st2.scale),
-                                            nat.f32(st2.shift), nat.f32(st2.mean), nat.f32(st2.invstd), slope2,
-                                            nat.f32(dz), nat.f32(part), nblk, stream), "edge bwd dz")
+            if dY_pm.is_contiguous():
+                nblk = max(1, min(1024, (M + 63) // 64))
+                part = torch.empty((nblk, 2, C2), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_edge_bwd_dz_f32(nat.f32(dY_pm), C2, nat.f32(ysel), M, C2, nat.f32(st2.scale),
+                                                nat.f32(st2.shift), nat.f32(st2.mean), nat.f32(st2.invstd), slope2,
+                                                nat.f32(dz), nat.f32(part), nblk, stream), "edge bwd dz")
+            else:  # (B, C2, N) gradient (a contiguous downstream): read channel-major, no transpose copy
+                dcm = dout.contiguous()
+                nblk = L.dgx_edge_bwd_dz_cm_rows(B, N)
+                part = torch.empty((nblk, 2, C2), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_edge_bwd_dz_cm_f32(nat.f32(dcm), nat.f32(ysel), B, N, C2, nat.f32(st2.scale),
+                                                   nat.f32(st2.shift), nat.f32(st2.mean), nat.f32(st2.invstd),
+                                                   slope2, nat.f32(dz), nat.f32(part), nblk, stream), "edge bwd dz")
             dg2, db2, c0, c1 = bn_.backward_consts(part, nblk, float(E), st2, stream)
             if fused_bwd:
                 # conv2 + LReLU/BN1 backward in one pass: gE, BN1 partials, dW2 slabs

@@ -157,6 +157,14 @@ int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel,
                         const float* shift, const float* mean,
                         const float* invstd, float slope, float* dz,
                         float* partials, int nrows, void* stream);
+/* dgx_edge_bwd_dz_f32 for a channel-major dY (B x Co x N, the layout of the
+ * gradient of a (B, C, N) module output): same dz (M x Co, point-major) and
+ * partials, nrows = dgx_edge_bwd_dz_cm_rows(B, N). */
+int dgx_edge_bwd_dz_cm_rows(int B, int N);
+int dgx_edge_bwd_dz_cm_f32(const float* dY, const float* ysel, int B, int N, int Co,
+                           const float* scale, const float* shift, const float* mean,
+                           const float* invstd, float slope, float* dz, float* partials,
+                           int nrows, void* stream);
 int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co,
                             double count, const float* scale, const float* mean,
                             const float* invstd, float* dgamma, float* dbeta,
