@@ -88,9 +88,12 @@ class _EdgeMLP2(torch.autograd.Function):
                     nat.ptr(H1, nat.BF16), stream), "edge mlp fused forward")
                 st2 = (bn_.batch_stats(part2, rows2, float(E), bn2, g2, b2, stream) if use2
                        else bn_.running_stats(bn2, g2, b2, stream))
-                out = torch.empty((M, C2), dtype=torch.float32, device=dev)
-                nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, C2, nat.f32(st2.scale), nat.f32(st2.shift),
-                                                   float(slope2), nat.f32(out), C2, None, stream), "bn apply")
+                # LReLU(BN2) of the selected values, written (B, C2, N) contiguous as the
+                # reference's max over k returns it (LDS-transposed apply)
+                out = torch.empty((B, C2, N), dtype=torch.float32, device=dev)
+                nat.check(L.dgx_pointconv_apply_f32(nat.f32(ysel), C2, B, N, C2, nat.f32(st2.scale),
+                                                    nat.f32(st2.shift), float(slope2), nat.f32(out), stream),
+                          "bn apply")
                 ctx.dims = (B, C, N, k, C1, C2)
                 ctx.slopes = (float(slope1), float(slope2))
                 ctx.st = (st1, st2)
@@ -98,7 +101,7 @@ class _EdgeMLP2(torch.autograd.Function):
                 ctx.bf16 = bf16
                 if need_grad:
                     ctx.save_for_backward(X, idx, PQ, sumP1, H1, None, ysel, arg, w1, w2)
-                return out.view(B, N, C2).permute(0, 2, 1)
+                return out
             h16 = bf16 and C1 % 64 == 0
             H1 = torch.empty((E, C1), dtype=torch.bfloat16 if h16 else torch.float32, device=dev)
             nat.check(L.dgx_edge_mlp_h1_f32(nat.f32(PQ), 2 * C1, nat.i32(idx), B, N, k, C1, nat.f32(st1.scale),
@@ -132,9 +135,9 @@ class _EdgeMLP2(torch.autograd.Function):
             arg = torch.empty((M, C2), dtype=torch.uint8, device=dev)
             nat.check(L.dgx_edge_mlp_max_f32(nat.ptr(Z2, nat.F32, nat.BF16), int(z16), B, N, k, C2, nat.f32(st2.scale),
                                              nat.f32(ysel), nat.u8(arg), stream), "edge max")
-            out = torch.empty((M, C2), dtype=torch.float32, device=dev)
-            nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, C2, nat.f32(st2.scale), nat.f32(st2.shift),
-                                               float(slope2), nat.f32(out), C2, None, stream), "bn apply")
+            out = torch.empty((B, C2, N), dtype=torch.float32, device=dev)
+            nat.check(L.dgx_pointconv_apply_f32(nat.f32(ysel), C2, B, N, C2, nat.f32(st2.scale), nat.f32(st2.shift),
+                                                float(slope2), nat.f32(out), stream), "bn apply")
         ctx.dims = (B, C, N, k, C1, C2)
         ctx.slopes = (float(slope1), float(slope2))
         ctx.st = (st1, st2)
@@ -142,7 +145,7 @@ class _EdgeMLP2(torch.autograd.Function):
         ctx.bf16 = bf16
         if need_grad:
             ctx.save_for_backward(X, idx, PQ, sumP1, H1, Z2, ysel, arg, w1, w2)
-        return out.view(B, N, C2).permute(0, 2, 1)
+        return out
 
     @staticmethod
     @prec.no_autocast
@@ -267,7 +270,7 @@ def edge_mlp2(x, k, conv1, conv2, training=None, knn_src=None):
     """max_k conv2(conv1(get_graph_feature(x, k))) for conv1/conv2 =
     nn.Sequential(Conv2d(1x1, bias=False), BatchNorm2d, LeakyReLU) as
     PositionEmbedding builds them (reference models/layers.py:17-20, 45-52).
-    Returns (B, C2, N) (a permuted view of a point-major buffer).
+    Returns (B, C2, N) contiguous, as the reference's max over k.
     ``training`` is accepted for call compatibility only (dgx.bn: each BN
     module's own flags decide batch vs running statistics). ``knn_src``:
     optional (B, C', N) tensor the neighbours are searched on instead of x

@@ -74,6 +74,6 @@ def test_fused_backward_skips_h1_store(cuda):
         y = EM.edge_mlp2(x, 20, conv1, conv2, True)
     finally:
         precision.set("fp32")
-    saved = y.grad_fn.saved_tensors  # the engine Function's node (it returns the permuted view)
+    saved = y.grad_fn.saved_tensors  # the engine Function's own node (it returns its output)
     assert len(saved) == 10
     assert all(t is None or t.shape[0] != 2 * 256 * 20 for t in saved)
