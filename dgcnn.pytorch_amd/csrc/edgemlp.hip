@@ -358,112 +358,123 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
 }
 
 // ---- fused forward (bf16 mode): h1 -> conv2 on the MFMA -> max over k + BN2
-// statistics, without writing z2. A pair of waves takes one point at a time,
-// each wave half of the C2 output channels: the point's k edge rows, padded to
-// KT tiles of 16, are the MFMA row tiles. Per row tile a lane builds its A
-// fragment (row = lane & 15, channels 32 ks + 8 g .. +7, g = lane >> 4)
-// straight from the gathered P_j and the point's Q_i (h1 = LReLU(a1 (P_j + Q_i)
-// + b1), rounded to bf16 as the unfused path stores it), multiplies by its half
-// of W2 (B fragments in registers for the whole kernel) and folds the 16 x C2/2
-// result into the point's running max (and first slot) and the per-column sums
-// of z2 and z2^2. W2's rows come pre-multiplied by dir = sign(gamma2) (exact),
-// so the max of dir * z2 is the max (or min) the BN2 + LReLU ordering needs;
-// outputs are multiplied back. Optionally writes h1 (bf16, the backward's
-// operand; the half-0 wave of a pair stores it). Block = 2 pairs x EMF_PPW
-// points; blocks of a cloud stay on one XCD (its P rows are L2-resident);
-// partial-stat row = block.
-constexpr int EMF_PPW = 4;
-constexpr int EMF_PPB = 2 * EMF_PPW;
+// statistics, without writing z2. A block is a pair of waves and takes
+// EMF_PPB points one at a time; wave `half` owns C2 output channels
+// [C2/2 half, C2/2 (half + 1)). The point's k edge rows, padded to KT tiles of
+// 16, are the MFMA row tiles. Per row tile the pair builds h1 = LReLU(a1 (P_j +
+// Q_i) + b1) once (as LReLU(a1 P_j + qb), qb = a1 Q_i + b1 per point, rounded
+// to bf16 as the unfused path stores it): wave `half` gathers rows 8 half ..
+// 8 half + 7, eight lanes per 256-byte P_j row (two whole 128-byte lines per
+// load instruction), and writes its bf16 rows to an LDS tile (double-buffered
+// by tile parity: one barrier per tile). Each wave then reads the A fragments
+// (row = lane & 15, channels 32 ks + 8 g .. +7, g = lane >> 4), multiplies by
+// its half of W2 (B fragments in registers for the whole kernel) and folds the
+// 16 x C2/2 result into the point's running max (and first slot) and the
+// per-column sums of z2 and z2^2. W2's rows come pre-multiplied by dir =
+// sign(gamma2) (exact), so the max of dir * z2 is the max (or min) the BN2 +
+// LReLU ordering needs; outputs are multiplied back. Optionally writes h1
+// (bf16, the unfused backward's operand). Blocks of a cloud stay on one XCD
+// (its P rows are L2-resident); partial-stat row = block. Held to 3 waves per
+// SIMD (168 VGPRs, a few spilled): 191 us at cfg4 against 228 us at the 2 waves
+// the compiler picks unasked (and 298 us for the previous kernel, which built
+// every h1 tile in both waves of a pair).
+constexpr int EMF_PPB = 8;
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ uint2 pack4_bf16(const __bf16* h) {
+    return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16),
+                      (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16));
+}
+
 template <int KT, int NTW>
-__global__ __launch_bounds__(256) void emlp_fwd_kernel(
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void emlp_fwd_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int B, int N, int k, int tiles,
     const float* __restrict__ scale1, const float* __restrict__ shift1, float slope1, const __bf16* __restrict__ W2d,
     const float* __restrict__ dir2, float* __restrict__ ysel, uint8_t* __restrict__ arg, float* __restrict__ part,
     __bf16* __restrict__ H1) {
-    constexpr int C1 = 64, C2 = 32 * NTW;
-    __shared__ float red[2][2][C2];
+    constexpr int C1 = 64, C2 = 32 * NTW, HP = C1 + 8;  // h1 tile pitch: +16 B staggers rows over the banks
+    __shared__ __attribute__((aligned(16))) __bf16 h1s[2][16 * HP];
     int b, tile;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, tiles, b, tile)) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int pair = wave >> 1, half = wave & 1;
+    const int lane = threadIdx.x & 63, half = threadIdx.x >> 6;
     const int g = lane >> 4, r16 = lane & 15;
     const int cb = half * NTW;  // first channel tile of this wave
+    // gather role: tile row R, channels 4m .. 4m+3 and 32 + 4m .. 32 + 4m+3
+    const int R = 8 * half + (lane >> 3), m = lane & 7;
     bf16x8_t wf[NTW][2];
 #pragma unroll
     for (int ct = 0; ct < NTW; ++ct)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
             wf[ct][ks] = *reinterpret_cast<const bf16x8_t*>(W2d + ((cb + ct) * 16 + r16) * C1 + ks * 32 + 8 * g);
-    float a1[2][8];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) ld8(scale1 + ks * 32 + 8 * g, a1[ks]);
+    auto ldrow = [&](const float* row, float* v) {
+        const float4 x = ld4(row + 4 * m), y = ld4(row + 32 + 4 * m);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    };
+    float a1[8];
+    ldrow(scale1, a1);
     float2 s1[NTW], s2[NTW];
 #pragma unroll
     for (int ct = 0; ct < NTW; ++ct) { s1[ct] = make_float2(0.f, 0.f); s2[ct] = make_float2(0.f, 0.f); }
     const int64_t cbase = (int64_t)b * N;
-    const int n0 = tile * EMF_PPB + pair * EMF_PPW;
-    const int np = max(0, min(EMF_PPW, N - n0));
+    const int n0 = tile * EMF_PPB;
+    const int np = max(0, min(EMF_PPB, N - n0));  // block-uniform: both waves meet every barrier
     // Per point its KT row tiles are unrolled with the P_j loads one tile
     // ahead (ids of all tiles up front); the next point's Q_i and ids are issued
     // during the current point. The point loop is not unrolled (I-cache).
     int jv[KT];
-    float qv[2][8];
+    float qv[8];
     auto load_ids = [&](int pp) {
         const int64_t i = cbase + n0 + pp;
 #pragma unroll
-        for (int rt = 0; rt < KT; ++rt) jv[rt] = idx[i * k + min(rt * 16 + r16, k - 1)];
+        for (int rt = 0; rt < KT; ++rt) jv[rt] = idx[i * k + min(rt * 16 + R, k - 1)];
     };
     if (np > 0) {
         load_ids(0);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) ld8(PQ + (cbase + n0) * ldpq + C1 + ks * 32 + 8 * g, qv[ks]);
+        ldrow(PQ + (cbase + n0) * ldpq + C1, qv);
     }
+    int buf = 0;
 #pragma unroll 1
     for (int pp = 0; pp < np; ++pp) {
         const int64_t i = cbase + n0 + pp;
-        float pb[2][2][8];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) ld8(PQ + (cbase + jv[0]) * ldpq + ks * 32 + 8 * g, pb[0][ks]);
-        // h1 = LReLU(a1 (P_j + Q_i) + b1) as LReLU(a1 P_j + qb), qb = a1 Q_i + b1 per point
-        float qb[2][8];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        float pb[2][8];
+        ldrow(PQ + (cbase + jv[0]) * ldpq, pb[0]);
+        float qb[8];
+        {
             float b1[8];
-            ld8(shift1 + ks * 32 + 8 * g, b1);
+            ldrow(shift1, b1);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) qb[ks][u] = fmaf(a1[ks][u], qv[ks][u], b1[u]);
+            for (int u = 0; u < 8; ++u) qb[u] = fmaf(a1[u], qv[u], b1[u]);
         }
-        if (pp + 1 < np) {
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) ld8(PQ + (i + 1) * ldpq + C1 + ks * 32 + 8 * g, qv[ks]);
-        }
+        if (pp + 1 < np) ldrow(PQ + (i + 1) * ldpq + C1, qv);
         float best[NTW];
         int barg[NTW];
 #pragma unroll
         for (int ct = 0; ct < NTW; ++ct) { best[ct] = -INFINITY; barg[ct] = 0; }
 #pragma unroll
         for (int rt = 0; rt < KT; ++rt) {
-            if (rt + 1 < KT) {
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-                    ld8(PQ + (cbase + jv[rt + 1]) * ldpq + ks * 32 + 8 * g, pb[(rt + 1) & 1][ks]);
-            } else if (pp + 1 < np) {
+            if (rt + 1 < KT)
+                ldrow(PQ + (cbase + jv[rt + 1]) * ldpq, pb[(rt + 1) & 1]);
+            else if (pp + 1 < np)
                 load_ids(pp + 1);
+            __bf16 hv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) hv[u] = (__bf16)lrelu(fmaf(a1[u], pb[rt & 1][u], qb[u]), slope1);
+            const uint2 lo = pack4_bf16(hv), hi = pack4_bf16(hv + 4);
+            const int sR = rt * 16 + R;
+            if (H1 && sR < k) {
+                *reinterpret_cast<uint2*>(H1 + (i * k + sR) * C1 + 4 * m) = lo;
+                *reinterpret_cast<uint2*>(H1 + (i * k + sR) * C1 + 32 + 4 * m) = hi;
             }
-            const int s = rt * 16 + r16;
+            __bf16* hrow = h1s[buf] + R * HP;
+            *reinterpret_cast<uint2*>(hrow + 4 * m) = lo;
+            *reinterpret_cast<uint2*>(hrow + 32 + 4 * m) = hi;
+            __syncthreads();
             bf16x8_t af[2];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    af[ks][u] = (__bf16)lrelu(fmaf(a1[ks][u], pb[rt & 1][ks][u], qb[ks][u]), slope1);
-            if (H1 && half == 0 && s < k) {
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks)
-                    *reinterpret_cast<bf16x8_t*>(H1 + (i * k + s) * C1 + ks * 32 + 8 * g) = af[ks];
-            }
+                af[ks] = *reinterpret_cast<const bf16x8_t*>(h1s[buf] + r16 * HP + ks * 32 + 8 * g);
+            buf ^= 1;
             f32x4_t acc[NTW];
 #pragma unroll
             for (int ct = 0; ct < NTW; ++ct) {
@@ -523,7 +534,9 @@ __global__ __launch_bounds__(256) void emlp_fwd_kernel(
             arg[i * C2 + c2] = (uint8_t)ba;
         }
     }
-    // BN2 partials of this block: lane sums -> over the lane groups -> over pairs
+    // BN2 partials of this block: lane sums -> over the lane groups; the wave
+    // owns its channels, so it writes them directly
+    const int prow = b * tiles + tile;
 #pragma unroll
     for (int ct = 0; ct < NTW; ++ct) {
         float t1 = s1[ct].x + s1[ct].y, t2 = s2[ct].x + s2[ct].y;
@@ -532,15 +545,10 @@ __global__ __launch_bounds__(256) void emlp_fwd_kernel(
         t1 += __shfl_xor(t1, 32);
         t2 += __shfl_xor(t2, 32);
         if (g == 0) {
-            red[pair][0][(cb + ct) * 16 + r16] = t1;
-            red[pair][1][(cb + ct) * 16 + r16] = t2;
+            const int c = (cb + ct) * 16 + r16;
+            part[(int64_t)prow * 2 * C2 + c] = dir2[c] * t1;
+            part[(int64_t)prow * 2 * C2 + C2 + c] = t2;
         }
-    }
-    __syncthreads();
-    const int prow = b * tiles + tile;
-    for (int c = threadIdx.x; c < C2; c += 256) {
-        part[(int64_t)prow * 2 * C2 + c] = dir2[c] * (red[0][0][c] + red[1][0][c]);
-        part[(int64_t)prow * 2 * C2 + C2 + c] = red[0][1][c] + red[1][1][c];
     }
 }
 
@@ -912,7 +920,7 @@ int dgx_edge_mlp_fused_fwd_bf16(const float* PQ, int ldpq, const int32_t* idx, i
     hipStream_t st = dgx_stream(stream);
     const int kt = (k + 15) / 16;
 #define DGX_EMF(KTV, NTV)                                                                                        \
-    hipLaunchKernelGGL((emlp_fwd_kernel<KTV, NTV / 2>), grid, dim3(256), 0, st, PQ, ldpq, idx, B, N, k, tiles, scale1, \
+    hipLaunchKernelGGL((emlp_fwd_kernel<KTV, NTV / 2>), grid, dim3(128), 0, st, PQ, ldpq, idx, B, N, k, tiles, scale1, \
                        shift1, slope1, w, dir2, ysel, arg, partials, h)
     if (C2 == 128) {
         switch (kt) {

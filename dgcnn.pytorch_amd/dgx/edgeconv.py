@@ -114,7 +114,7 @@ class _EdgeConvStack(torch.autograd.Function):
         # bf16 twin of the concat buffer: the GEMM operand copy, written by the
         # same kernel that writes xcat (precision "bf16" only)
         xcat16 = torch.empty((M, total), dtype=torch.bfloat16, device=dev) if bf16 else None
-        x_pm = x.permute(0, 2, 1).reshape(M, C0)  # point-major input rows (copy only if needed)
+        x_pm = x.permute(0, 2, 1).reshape(M, C0).contiguous()  # point-major rows (B = 1 reshapes to a view)
         saved = []
         off_in = None
         count = float(M * k)

@@ -48,7 +48,7 @@ class _EdgeMLP2(torch.autograd.Function):
         L = nat.lib()
         stream = nat.stream_of(x)
         bf16 = prec.get() == "bf16"
-        X = x.permute(0, 2, 1).reshape(M, C)
+        X = x.permute(0, 2, 1).reshape(M, C).contiguous()  # B = 1 reshapes to a column-major view
         kx = x if knn_src is None else knn_src.float()                            # neighbours found on kx
         idx = knn_raw(kx, k, order=reduction_order(kx), out_dtype=torch.int32)   # layers.py:45 -> dgcnn.py:21
         w1s = split_weight(w1, C, C1)
