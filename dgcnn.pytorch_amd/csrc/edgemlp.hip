@@ -18,6 +18,7 @@
 //   mlp_dz2_kernel       dZ2 = a2 dz [slot] + c0 + c1 z2 (BN2 backward), dense
 //   mlp_h1_bwd_kernel    g = dH1 * LReLU'(z1) in place + BN1-backward partials
 //   mlp_h1_scatter_kernel dP_j / dQ_i from g over the edge rows and the reverse kNN graph
+//   mlp_h1_scatter4_kernel the same for bf16 g and C1 = 64, four points per wave
 #include "common.h"
 
 namespace {
@@ -354,6 +355,104 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter_kernel(
         const float Pp = PQ[p * ldpq + c], Qp = PQ[p * ldpq + C1 + c];
         dPQ[p * 2 * C1 + c] = fmaf(a, ig, fmaf(k0, deg, k1 * fmaf(deg, Pp, iq)));
         dPQ[p * 2 * C1 + C1 + c] = fmaf(a, sg, fmaf(k0, kf, k1 * fmaf(kf, Qp, sumP[p * C1 + c])));
+    }
+}
+
+// bf16 g with C1 = 64: 64 / LPP points per wave (LPP lanes each, CPL = 64 /
+// LPP channels per lane: 2·CPL-byte g loads, 4·CPL-byte Q loads), so one load
+// instruction carries 64 / LPP in-edges instead of one and a wave keeps that
+// many more rows in flight (the one-point-per-wave kernel above is bound by
+// its dependent load latency). In-edge ids are loaded one batch ahead. Sums in
+// a fixed order (batch slot u, then u = 0..EM_U4-1): deterministic.
+template <int EM_U4, int LPP>
+__global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter4_kernel(
+    const __bf16* __restrict__ g, const float* __restrict__ PQ, int ldpq, const float* __restrict__ sumP,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges, int B, int N, int tiles, int k,
+    const float* __restrict__ scale, const float* __restrict__ c0, const float* __restrict__ c1,
+    float* __restrict__ dPQ) {
+    constexpr int C1 = 64, CPL = C1 / LPP, PPW = 64 / LPP;
+    const int lane = threadIdx.x & 63, c = CPL * (lane % LPP);
+    // blocks of a cloud stay on one XCD: its in-edge rows are gathered from its own g rows
+    int b, tile;
+    if (!dgx_xcd_cloud_map(blockIdx.x, B, tiles, b, tile)) return;
+    const int n = tile * (EM_THREADS / LPP) + (threadIdx.x >> 6) * PPW + lane / LPP;
+    const bool live = n < N;
+    const int64_t p = (int64_t)b * N + n;
+    const int64_t pc = live ? p : (int64_t)b * N + N - 1;  // lanes past the end shadow the last point, write nothing
+    const int32_t beg = rowptr[pc], cnt = live ? rowptr[pc + 1] - beg : 0;
+    auto addg = [](float* acc, const __bf16* q) {
+#pragma unroll
+        for (int h = 0; h < CPL / 4; ++h) {
+            const uint2 w = *reinterpret_cast<const uint2*>(q + 4 * h);
+            acc[4 * h + 0] += __uint_as_float(w.x << 16);
+            acc[4 * h + 1] += __uint_as_float(w.x & 0xffff0000u);
+            acc[4 * h + 2] += __uint_as_float(w.y << 16);
+            acc[4 * h + 3] += __uint_as_float(w.y & 0xffff0000u);
+        }
+    };
+    auto addf = [](float* acc, const float* q) {
+#pragma unroll
+        for (int h = 0; h < CPL / 4; ++h) {
+            const float4 v = ld4(q + 4 * h);
+            acc[4 * h + 0] += v.x; acc[4 * h + 1] += v.y; acc[4 * h + 2] += v.z; acc[4 * h + 3] += v.w;
+        }
+    };
+    float sgv[EM_U4][CPL], igv[EM_U4][CPL], iqv[EM_U4][CPL];
+#pragma unroll
+    for (int u = 0; u < EM_U4; ++u)
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) { sgv[u][e] = 0.f; igv[u][e] = 0.f; iqv[u][e] = 0.f; }
+    int32_t idn[EM_U4];
+    auto load_ids = [&](int r) {
+#pragma unroll
+        for (int u = 0; u < EM_U4; ++u) idn[u] = r + u < cnt ? edges[beg + r + u] : -1;
+    };
+    load_ids(0);
+    const __bf16* __restrict__ gp = g + pc * k * C1 + c;
+    int s = 0;
+    for (; s + EM_U4 <= k; s += EM_U4) {
+#pragma unroll
+        for (int u = 0; u < EM_U4; ++u) addg(sgv[u], gp + (int64_t)(s + u) * C1);
+    }
+    for (; s < k; ++s) addg(sgv[0], gp + (int64_t)s * C1);
+    int cmax = cnt;
+#pragma unroll
+    for (int o = LPP; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o));
+    for (int r = 0; r < cmax; r += EM_U4) {
+        int32_t id[EM_U4];
+#pragma unroll
+        for (int u = 0; u < EM_U4; ++u) id[u] = idn[u];
+        load_ids(r + EM_U4);
+#pragma unroll
+        for (int u = 0; u < EM_U4; ++u) {
+            if (id[u] >= 0) {
+                const int64_t src = (int64_t)(id[u] >> 6);
+                addg(igv[u], g + (src * k + (id[u] & 63)) * C1 + c);
+                addf(iqv[u], PQ + src * ldpq + C1 + c);
+            }
+        }
+    }
+    if (!live) return;
+    const float kf = (float)k, deg = (float)cnt;
+#pragma unroll
+    for (int h = 0; h < CPL / 4; ++h) {
+        const int ch = c + 4 * h;
+        const float4 a4 = ld4(scale + ch), k04 = ld4(c0 + ch), k14 = ld4(c1 + ch);
+        const float4 P4 = ld4(PQ + p * ldpq + ch), Q4 = ld4(PQ + p * ldpq + C1 + ch), S4 = ld4(sumP + p * C1 + ch);
+        const float a[4] = {a4.x, a4.y, a4.z, a4.w}, k0[4] = {k04.x, k04.y, k04.z, k04.w};
+        const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, Pp[4] = {P4.x, P4.y, P4.z, P4.w};
+        const float Qp[4] = {Q4.x, Q4.y, Q4.z, Q4.w}, sP[4] = {S4.x, S4.y, S4.z, S4.w};
+        float dP[4], dQ[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float sg = sgv[0][4 * h + e], ig = igv[0][4 * h + e], iq = iqv[0][4 * h + e];
+#pragma unroll
+            for (int u = 1; u < EM_U4; ++u) { sg += sgv[u][4 * h + e]; ig += igv[u][4 * h + e]; iq += iqv[u][4 * h + e]; }
+            dP[e] = fmaf(a[e], ig, fmaf(k0[e], deg, k1[e] * fmaf(deg, Pp[e], iq)));
+            dQ[e] = fmaf(a[e], sg, fmaf(k0[e], kf, k1[e] * fmaf(kf, Qp[e], sP[e])));
+        }
+        *reinterpret_cast<float4*>(dPQ + p * 2 * C1 + ch) = make_float4(dP[0], dP[1], dP[2], dP[3]);
+        *reinterpret_cast<float4*>(dPQ + p * 2 * C1 + C1 + ch) = make_float4(dQ[0], dQ[1], dQ[2], dQ[3]);
     }
 }
 
@@ -1045,7 +1144,14 @@ int dgx_edge_mlp_scatter_f32(const void* g, int g_bf16, const float* PQ, int ldp
     const int64_t M = (int64_t)B * N;
     const int64_t blocks = (M + EM_THREADS / 64 - 1) / (EM_THREADS / 64);
     if (blocks > 0x7fffffff) return DGX_EUNSUPPORTED;
-    if (g_bf16)
+    if (g_bf16 && C1 == 64 && ldpq % 4 == 0 && al16(g) && al16(PQ) && al16(sumP) && al16(scale) && al16(c0) &&
+        al16(c1) && al16(dPQ)) {
+        constexpr int LPP = 16, PPB = EM_THREADS / LPP;
+        const int tiles = (N + PPB - 1) / PPB;
+        hipLaunchKernelGGL((mlp_h1_scatter4_kernel<4, LPP>), dim3(dgx_xcd_cloud_grid(B, tiles)), dim3(EM_THREADS), 0,
+                           dgx_stream(stream), static_cast<const __bf16*>(g), PQ, ldpq, sumP, rowptr, edges, B, N, tiles, k,
+                           scale, c0, c1, dPQ);
+    } else if (g_bf16)
         hipLaunchKernelGGL(mlp_h1_scatter_kernel<__bf16>, dim3((unsigned)blocks), dim3(EM_THREADS), 0,
                            dgx_stream(stream), static_cast<const __bf16*>(g), PQ, ldpq, sumP, rowptr, edges, M, k, C1,
                            scale, c0, c1, dPQ);
