@@ -474,9 +474,10 @@ __global__ __launch_bounds__(EM_THREADS) void mlp_h1_scatter4_kernel(
 // LReLU ordering needs; outputs are multiplied back. Optionally writes h1
 // (bf16, the unfused backward's operand). Blocks of a cloud stay on one XCD
 // (its P rows are L2-resident); partial-stat row = block. Held to 3 waves per
-// SIMD (168 VGPRs, a few spilled): 191 us at cfg4 against 228 us at the 2 waves
-// the compiler picks unasked (and 298 us for the previous kernel, which built
-// every h1 tile in both waves of a pair).
+// SIMD (168 VGPRs; BN1's scale / shift read from LDS where used, not held in
+// registers): 184 us at cfg4, against 228 us at the 2 waves the compiler picks
+// unasked, 303-436 us at 4 waves (spills), and 298 us for the previous kernel,
+// which built every h1 tile in both waves of a pair.
 constexpr int EMF_PPB = 8;
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
@@ -493,8 +494,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void e
     __bf16* __restrict__ H1) {
     constexpr int C1 = 64, C2 = 32 * NTW, HP = C1 + 8;  // h1 tile pitch: +16 B staggers rows over the banks
     __shared__ __attribute__((aligned(16))) __bf16 h1s[2][16 * HP];
+    __shared__ __attribute__((aligned(16))) float cs[2][C1];  // BN1 scale | shift
     int b, tile;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, tiles, b, tile)) return;
+    cs[threadIdx.x >> 6][threadIdx.x & 63] = (threadIdx.x >> 6 ? shift1 : scale1)[threadIdx.x & 63];
+    __syncthreads();
     const int lane = threadIdx.x & 63, half = threadIdx.x >> 6;
     const int g = lane >> 4, r16 = lane & 15;
     const int cb = half * NTW;  // first channel tile of this wave
@@ -510,8 +514,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void e
         const float4 x = ld4(row + 4 * m), y = ld4(row + 32 + 4 * m);
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
     };
-    float a1[8];
-    ldrow(scale1, a1);
+    auto lds8 = [&](const float* row, float* v) {
+        const float4 x = *reinterpret_cast<const float4*>(row + 4 * m), y = *reinterpret_cast<const float4*>(row + 32 + 4 * m);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    };
     float2 s1[NTW], s2[NTW];
 #pragma unroll
     for (int ct = 0; ct < NTW; ++ct) { s1[ct] = make_float2(0.f, 0.f); s2[ct] = make_float2(0.f, 0.f); }
@@ -540,8 +546,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void e
         ldrow(PQ + (cbase + jv[0]) * ldpq, pb[0]);
         float qb[8];
         {
-            float b1[8];
-            ldrow(shift1, b1);
+            float a1[8], b1[8];
+            lds8(cs[0], a1);
+            lds8(cs[1], b1);
 #pragma unroll
             for (int u = 0; u < 8; ++u) qb[u] = fmaf(a1[u], qv[u], b1[u]);
         }
@@ -557,6 +564,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void e
             else if (pp + 1 < np)
                 load_ids(pp + 1);
             __bf16 hv[8];
+            float a1[8];
+            lds8(cs[0], a1);
 #pragma unroll
             for (int u = 0; u < 8; ++u) hv[u] = (__bf16)lrelu(fmaf(a1[u], pb[rt & 1][u], qb[u]), slope1);
             const uint2 lo = pack4_bf16(hv), hi = pack4_bf16(hv + 4);
