@@ -182,6 +182,10 @@ class _EdgeConvStack(torch.autograd.Function):
                     have16 = False
                     saved.append(None)
             off_in = off
+        if dbg is not None:
+            # the blocks' own inputs (tests re-derive each block's kNN and decisions from them)
+            dbg["xcat"] = xcat
+            dbg["xcat16"] = xcat16 if have16 else None
         ctx.k = k
         ctx.layers = layers
         ctx.shape = (B, C0, N)

@@ -22,7 +22,7 @@ from . import _native as nat
 from . import bn as bn_
 from . import gemm as G
 from . import precision as prec
-from .edgeconv import edge_select, split_weight
+from .edgeconv import debug_capture, edge_select, split_weight
 from .ops import knn_raw, reduction_order
 
 # bf16 mode, C1 = 64 / C2 = 128 (PositionEmbedding): one backward kernel for
@@ -34,6 +34,19 @@ FUSED_BWD = True
 
 def _fused_bwd_ok(bf16, C1, C2, k):
     return FUSED_BWD and bf16 and C1 == 64 and C2 == 128 and k <= 64
+
+
+def _capture(idx, PQ, st1, st2, ysel, arg, bf16, fused):
+    """Debug capture (tests): the stage's routing inputs under "emlp" — the kNN
+    graph, conv1's decomposed PQ and BN1 affine (h1's LeakyReLU signs follow
+    from them), conv2's selected pre-BN value / slot and BN2 affine. ``fused``:
+    h1 was built as fma(a1, P_j, fma(a1, Q_i, b1)) and fed to the MFMA in bf16
+    (emlp_fwd_kernel); otherwise as fma(a1, P_j + Q_i, b1) (mlp_h1_kernel)."""
+    dbg = debug_capture()
+    if dbg is not None:
+        dbg["emlp"] = {"idx": idx.clone(), "PQ": PQ.clone(), "a1": st1.scale.clone(), "b1": st1.shift.clone(),
+                       "ysel": ysel.clone(), "arg": arg.clone(), "a2": st2.scale.clone(), "b2": st2.shift.clone(),
+                       "bf16": bf16, "fused": fused}
 
 
 class _EdgeMLP2(torch.autograd.Function):
@@ -94,6 +107,7 @@ class _EdgeMLP2(torch.autograd.Function):
                 nat.check(L.dgx_pointconv_apply_f32(nat.f32(ysel), C2, B, N, C2, nat.f32(st2.scale),
                                                     nat.f32(st2.shift), float(slope2), nat.f32(out), stream),
                           "bn apply")
+                _capture(idx, PQ, st1, st2, ysel, arg, bf16, fused=True)
                 ctx.dims = (B, C, N, k, C1, C2)
                 ctx.slopes = (float(slope1), float(slope2))
                 ctx.st = (st1, st2)
@@ -138,6 +152,7 @@ class _EdgeMLP2(torch.autograd.Function):
             out = torch.empty((B, C2, N), dtype=torch.float32, device=dev)
             nat.check(L.dgx_pointconv_apply_f32(nat.f32(ysel), C2, B, N, C2, nat.f32(st2.scale), nat.f32(st2.shift),
                                                 float(slope2), nat.f32(out), stream), "bn apply")
+        _capture(idx, PQ, st1, st2, ysel, arg, bf16, fused=False)
         ctx.dims = (B, C, N, k, C1, C2)
         ctx.slopes = (float(slope1), float(slope2))
         ctx.st = (st1, st2)

@@ -123,3 +123,23 @@ def dgcnn_routed(x, params, decisions, mask5, slope=0.2, training=(True,) * 5):
     z = F.batch_norm(z, bn["running_mean"], bn["running_var"], bn["weight"], bn["bias"], training[4], 0.1, 1e-5)
     z = z.view(B, -1, N)
     return torch.where(mask5, z, slope * z)
+
+
+def edge_mlp2_routed(x, w1, bn1, w2, bn2, idx, zpos1, arg2, zpos2, slope=0.2, training=(True, True)):
+    """PositionEmbedding's edge stage (reference models/layers.py:45-52:
+    get_graph_feature -> conv1 -> conv2 -> max over k) in x's dtype, routed by
+    the engine's decisions: zpos1 (B,C1,N,k) bool = sign of BN1's output per
+    edge (conv1's LeakyReLU), arg2 (B*N,C2) = the selected k-slot of conv2's
+    max, zpos2 (B*N,C2) bool = sign of BN2's output there. Returns the stage
+    output (B,C2,N) and conv2's BN output z2 (B,C2,N,k)."""
+    e = graph_feature(x, idx=idx)
+    z1 = F.batch_norm(F.conv2d(e, w1), bn1["running_mean"], bn1["running_var"], bn1["weight"], bn1["bias"],
+                      training[0], bn1.get("momentum", 0.1), bn1.get("eps", 1e-5))
+    h1 = torch.where(zpos1, z1, slope * z1)
+    z2 = F.batch_norm(F.conv2d(h1, w2), bn2["running_mean"], bn2["running_var"], bn2["weight"], bn2["bias"],
+                      training[1], bn2.get("momentum", 0.1), bn2.get("eps", 1e-5))
+    B, C2, N, _ = z2.shape
+    a = arg2.long().view(B, N, C2).permute(0, 2, 1).unsqueeze(-1)
+    zsel = torch.gather(z2, 3, a).squeeze(-1)
+    m = zpos2.view(B, N, C2).permute(0, 2, 1)
+    return torch.where(m, zsel, slope * zsel), z2

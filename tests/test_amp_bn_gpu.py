@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import rel_err
+from conftest import rel_err, validate_dgcnn_decisions
 from oracle import reference as R
 
 pytestmark = pytest.mark.gpu
@@ -84,6 +84,8 @@ def test_dgcnn_autocast_cfg4_geometry(cuda):
         assert torch.equal(p.grad, g_amp[n]), n
     for n, b in m.named_buffers():
         assert torch.equal(b, rs_amp[n]), n
+    # every neighbour set (blocks 1-4) and every max slot / sign is the reference's own
+    print("decision check (gap, flip):", validate_dgcnn_decisions(cap, x, k, init))
     ref, params = _routed_oracle(init, pts, _decisions(cap), y.detach() > 0, gout, cuda)
     assert rel_err(y.detach().cpu(), ref.cpu()) < TOL
     for n, p in m.named_parameters():
@@ -227,6 +229,7 @@ def test_dgcnn_frozen_bn_layers(cuda):
     gout = torch.from_numpy(synth.uniform(67, tuple(y.shape)) - 0.5).float()
     y.backward(gout.to(cuda))
     flags = (True, False, True, True, False)
+    validate_dgcnn_decisions(cap, x, k, init, training=flags[:4])
     ref, params = _routed_oracle(init, pts, _decisions(cap), y.detach() > 0, gout, cuda, training=flags)
     assert rel_err(y.detach().cpu(), ref.cpu()) < TOL
     for n, p in m.named_parameters():

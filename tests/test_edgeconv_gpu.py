@@ -7,7 +7,7 @@ import pytest
 import torch
 
 import oracle
-from conftest import rel_err
+from conftest import check_decisions, rel_err, validate_dgcnn_decisions
 from oracle import reference as R
 
 pytestmark = pytest.mark.gpu
@@ -45,22 +45,6 @@ class Capture:
 
     def __exit__(self, *exc):
         self.E.set_debug_capture(None)
-
-
-def check_decisions(z64, arg, zpos, B, N):
-    """Each GPU decision must be valid for the fp64 recomputation: the chosen
-    slot is a max of z over k up to rounding, and the sign of z there may only
-    disagree where |z| is at rounding level."""
-    z = z64.detach()
-    Co = z.shape[1]
-    scale = float(z.abs().max())
-    zmax = z.max(dim=-1)[0]                                                   # (B,Co,N)
-    a = arg.long().cpu().view(B, N, Co).permute(0, 2, 1).unsqueeze(-1)
-    zsel = torch.gather(z, 3, a).squeeze(-1)
-    assert float((zmax - zsel).max()) <= 1e-5 * scale
-    zp = zpos.cpu().view(B, N, Co).permute(0, 2, 1)
-    bad = zp != (zsel > 0)
-    assert float(zsel[bad].abs().max()) <= 1e-5 * scale if bad.any() else True
 
 
 def test_edgeconv_block_golden(golden, cuda):
@@ -174,6 +158,9 @@ def test_dgcnn_train_routed(golden, cuda, emb, N, k, B):
     y.backward(gout.to(cuda))
     decisions = [tuple(t for t in cap[("fwd", l)]) for l in range(4)]
     mask5 = y.detach() > 0
+    # every block's neighbour sets and max slots / signs are the reference's own
+    # (oracle kNN of the block's input, fp64 z), so routing by them is sound
+    print("decision check (gap, flip):", validate_dgcnn_decisions(cap, x, k, init))
 
     def routed(dtype):
         params = {n: (t.to(cuda).to(dtype) if t.is_floating_point() else t.to(cuda)) for n, t in init.items()}
@@ -323,6 +310,7 @@ def test_dgcnn_bf16_headline_cfg2_routed(cuda):
         y.backward(gout.to(cuda))
     finally:
         precision.set("fp32")
+    print("decision check (gap, flip):", validate_dgcnn_decisions(cap, x, k, init, bf16=True))
     dec = [(i.long(), a, z) for (i, a, z) in (cap[("fwd", l)] for l in range(4))]
     params = {n: (t.to(cuda).double() if t.is_floating_point() else t.to(cuda)) for n, t in init.items()}
     for n, t in params.items():
@@ -358,6 +346,7 @@ def test_dgcnn_bf16_mode_routed(cuda):
         y.backward(gout.to(cuda))
     finally:
         precision.set("fp32")
+    validate_dgcnn_decisions(cap, x, k, init, bf16=True)
     decisions = [tuple(t.cpu() for t in cap[("fwd", l)]) for l in range(4)]
     decisions = [(i.long(), a, z) for (i, a, z) in decisions]
     params = {n: (t.double() if t.is_floating_point() else t) for n, t in init.items()}
