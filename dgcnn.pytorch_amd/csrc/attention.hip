@@ -203,7 +203,19 @@ struct AtArgs {
     uint32_t p32;       // dropout threshold (0: no dropout)
     float rdrop;        // 1 / (1 - p)
     uint32_t s0, s1;    // dropout seed
+    const uint64_t* seedp;  // when set: the seed is read here (device-drawn, graph-replay safe)
 };
+
+// the dropout seed of this launch: from device memory when given (a seed drawn
+// by the device generator: every HIP-graph replay reads the new draw)
+__device__ __forceinline__ void at_seed(const AtArgs& a, uint32_t& s0, uint32_t& s1) {
+    if (a.seedp) {
+        const uint64_t v = *a.seedp;
+        s0 = (uint32_t)v, s1 = (uint32_t)(v >> 32);
+    } else {
+        s0 = a.s0, s1 = a.s1;
+    }
+}
 
 template <int D, int NP>
 constexpr int at_lds_bytes_qk() { return 2 * NP * 64 * at_rsw<D>() * 4; }
@@ -211,6 +223,8 @@ constexpr int at_lds_bytes_qk() { return 2 * NP * 64 * at_rsw<D>() * 4; }
 // ---------------------------------------------------------------- forward --
 template <typename T, int D, bool DROP, int NP>
 __global__ __launch_bounds__(AT_THREADS, NP == 2 ? 1 : 2) void attn_fwd_kernel(AtArgs a, void* __restrict__ out) {
+    uint32_t sd0, sd1;
+    at_seed(a, sd0, sd1);
     constexpr int RSW = at_rsw<D>();
     constexpr int KS = D / 32, DB = D / 16, TW = 64 * RSW;
     extern __shared__ __attribute__((aligned(16))) uint32_t at_lds[];
@@ -302,7 +316,7 @@ __global__ __launch_bounds__(AT_THREADS, NP == 2 ? 1 : 2) void attn_fwd_kernel(A
                     rs += p;
                     if constexpr (DROP) {
                         const int key = kv0 + 16 * kt + 4 * g + r;
-                        s[qt][kt][r] = at_keep(row, (uint32_t)key, a.p32, a.s0, a.s1) ? p : 0.f;
+                        s[qt][kt][r] = at_keep(row, (uint32_t)key, a.p32, sd0, sd1) ? p : 0.f;
                     } else {
                         s[qt][kt][r] = p;
                     }
@@ -398,6 +412,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AtArgs a, int B, int fm
 template <typename T, int D, bool DROP, int NP>
 __global__ __launch_bounds__(AT_THREADS, (D == 128 || NP == 2) ? 1 : 2) void attn_bwd_dq_kernel(
     AtArgs a, float* __restrict__ dq, int64_t dsB, int64_t dsN, int64_t dsH) {
+    uint32_t sd0, sd1;
+    at_seed(a, sd0, sd1);
     constexpr int RSW = at_rsw<D>();
     constexpr int KS = D / 32, DB = D / 16, TW = 64 * RSW;
     extern __shared__ __attribute__((aligned(16))) uint32_t at_lds[];
@@ -486,7 +502,7 @@ __global__ __launch_bounds__(AT_THREADS, (D == 128 || NP == 2) ? 1 : 2) void att
                     const int key = kv0 + 16 * kt + 4 * g + r;
                     const float p = key < a.Nk ? __builtin_amdgcn_exp2f(s[qt][kt][r] * a.scale_log2 - lse[qt]) : 0.f;
                     float d = dp[qt][kt][r];
-                    if constexpr (DROP) d = at_keep(row, (uint32_t)key, a.p32, a.s0, a.s1) ? d * a.rdrop : 0.f;
+                    if constexpr (DROP) d = at_keep(row, (uint32_t)key, a.p32, sd0, sd1) ? d * a.rdrop : 0.f;
                     s[qt][kt][r] = p * (d - dl[qt]) * AT_DS_SCALE;
                 }
         }
@@ -525,6 +541,8 @@ template <typename T, int D, bool DROP, int NP>
 __global__ __launch_bounds__(AT_THREADS, NP == 2 ? 1 : 2) void attn_bwd_dkv_kernel(
     AtArgs a, float* __restrict__ dk, int64_t ksB, int64_t ksN, int64_t ksH, float* __restrict__ dv, int64_t vsB,
     int64_t vsN, int64_t vsH) {
+    uint32_t sd0, sd1;
+    at_seed(a, sd0, sd1);
     constexpr int RSW = at_rsw<D>();
     constexpr int KS = D / 32, DB = D / 16, TW = 64 * RSW;
     extern __shared__ __attribute__((aligned(16))) uint32_t at_lds[];
@@ -608,7 +626,7 @@ __global__ __launch_bounds__(AT_THREADS, NP == 2 ? 1 : 2) void attn_bwd_dkv_kern
                 float d = dp[qt][r], pd = p;
                 if constexpr (DROP) {
                     const uint32_t row = (uint32_t)bh * (uint32_t)a.Nq + (uint32_t)(qv0 + qi);
-                    const bool kp = at_keep(row, (uint32_t)key, a.p32, a.s0, a.s1);
+                    const bool kp = at_keep(row, (uint32_t)key, a.p32, sd0, sd1);
                     d = kp ? d * a.rdrop : 0.f;
                     pd = kp ? p : 0.f;
                 }
@@ -703,7 +721,8 @@ extern "C" {
 int dgx_attn_fwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN, int64_t qsH, const void* k,
                  int64_t ksP, int64_t ksB, int64_t ksN, int64_t ksH, const void* v, int64_t vsP, int64_t vsB,
                  int64_t vsN, int64_t vsH, void* o, int64_t osB, int64_t osN, int64_t osH, float* lse, int B, int H,
-                 int Nq, int Nk, int D, float scale, float dropout_p, uint64_t seed, void* stream) {
+                 int Nq, int Nk, int D, float scale, float dropout_p, uint64_t seed, const uint64_t* seed_dev,
+                 void* stream) {
     if (!o || !lse || B < 0 || H < 1 || Nq < 0 || Nk < 1 || !(scale > 0.f)) return DGX_EINVAL;
     if (!(dropout_p >= 0.f && dropout_p < 1.f)) return DGX_EINVAL;
     if (dtype < 0 || dtype > 2 || (D != 64 && D != 128)) return DGX_EUNSUPPORTED;
@@ -720,6 +739,7 @@ int dgx_attn_fwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN
     a.lse = lse, a.H = H, a.Nq = Nq, a.Nk = Nk;
     a.scale_log2 = scale * 1.4426950408889634f, a.scale = scale;
     a.p32 = dr.p32, a.rdrop = dr.rdrop, a.s0 = (uint32_t)seed, a.s1 = (uint32_t)(seed >> 32);
+    a.seedp = seed_dev;
     const dim3 grid((Nq + AT_QB - 1) / AT_QB, B * H);
     hipStream_t st = dgx_stream(stream);
 #define DGX_ATTN_FWD(T, DV, DR, NPV)                                                                      \
@@ -734,7 +754,8 @@ int dgx_attn_bwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN
                  int64_t ksP, int64_t ksB, int64_t ksN, int64_t ksH, const void* v, int64_t vsP, int64_t vsB,
                  int64_t vsN, int64_t vsH, const void* o, const void* dout, int64_t gsP, int64_t osB, int64_t osN,
                  int64_t osH, const float* dout32, const float* lse, float* delta, int B, int H, int Nq, int Nk, int D,
-                 float scale, float dropout_p, uint64_t seed, float* dq, int64_t dqsB, int64_t dqsN, int64_t dqsH,
+                 float scale, float dropout_p, uint64_t seed, const uint64_t* seed_dev, float* dq, int64_t dqsB,
+                 int64_t dqsN, int64_t dqsH,
                  float* dk, int64_t dksB, int64_t dksN, int64_t dksH, float* dv, int64_t dvsB, int64_t dvsN,
                  int64_t dvsH, void* stream) {
     if (!o || !lse || !delta || !dq || !dk || !dv || B < 0 || H < 1 || Nq < 0 || Nk < 1 || !(scale > 0.f))
@@ -760,6 +781,7 @@ int dgx_attn_bwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN
     a.lse = const_cast<float*>(lse), a.delta = delta, a.H = H, a.Nq = Nq, a.Nk = Nk;
     a.scale_log2 = scale * 1.4426950408889634f, a.scale = scale;
     a.p32 = dr.p32, a.rdrop = dr.rdrop, a.s0 = (uint32_t)seed, a.s1 = (uint32_t)(seed >> 32);
+    a.seedp = seed_dev;
     hipStream_t st = dgx_stream(stream);
     const int64_t rows = (int64_t)B * H * Nq;
     const unsigned dblocks = (unsigned)((rows * 16 + 255) / 256);

@@ -85,10 +85,11 @@ _SIGS = {
                             _vp, _i32, _vp],
     "dgx_hog_1x1_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_attn_fwd": [_i32] + [_vp, _i64, _i64, _i64, _i64] * 3 + [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32,
-                                                                   _i32, _i32, _f32, _f32, ctypes.c_uint64, _vp],
+                                                                   _i32, _i32, _f32, _f32, ctypes.c_uint64, _vp,
+                                                                   _vp],
     "dgx_attn_bwd": [_i32] + [_vp, _i64, _i64, _i64, _i64] * 3 + [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp,
                                                                    _i32, _i32, _i32, _i32, _i32, _f32, _f32,
-                                                                   ctypes.c_uint64]
+                                                                   ctypes.c_uint64, _vp]
                     + [_vp, _i64, _i64, _i64] * 3 + [_vp],
     "dgx_attn_dropout_mask": [_i64, _i32, _f32, ctypes.c_uint64, _vp, _vp],
     "dgx_edge_mlp_fused_rows": [_i32, _i32],

@@ -6,6 +6,11 @@ import torch
 
 from . import _native as N
 
+# k range of the device path: csrc/svd3.h restates LAPACK dgesdd's tall-matrix
+# path (QR first), which dgesdd takes for k >= 5 rows (its mnthr = 3*11/6), and
+# the neighbourhood lives in registers up to 64 rows (HOG_MAX_K)
+HOG_K_MIN, HOG_K_MAX = 5, 64
+
 
 def hog_1x1(x, idx):
     """x (B, 3, N) fp32 on the device, idx (B, N, k) int64 local kNN ids ->
@@ -15,6 +20,9 @@ def hog_1x1(x, idx):
     if C != 3:
         raise RuntimeError(f"dgx: compute_hog_1x1 takes (B, 3, N) clouds, got {tuple(x.shape)}")
     k = idx.shape[-1]
+    if not HOG_K_MIN <= k <= HOG_K_MAX:
+        raise NotImplementedError(f"dgx: compute_hog_1x1 on the device supports {HOG_K_MIN} <= k <= {HOG_K_MAX} "
+                                  f"neighbours (got k={k}); the reference's numpy SVD path takes any k")
     if tuple(idx.shape) != (B, P, k):
         raise RuntimeError(f"dgx: kNN ids of shape {tuple(idx.shape)} do not match the cloud {tuple(x.shape)}")
     x = x.contiguous()

@@ -399,11 +399,14 @@ int dgx_hog_1x1_f32(const float* x, const int64_t* idx, int B, int N, int k, flo
  * (B, N, E) in-projection output viewed as (B, N, H, D)). D in {64, 128}.
  * lse: (B*H*Nq) fp32 log2-sum-exp of the scaled scores, kept for the backward.
  * Dropout (0 <= p < 1) on the attention weights from a counter-based hash of
- * (row, key, seed), regenerated by the backward; kept weights scaled 1/(1-p). */
+ * (row, key, seed), regenerated by the backward; kept weights scaled 1/(1-p).
+ * seed_dev: when non-NULL, the seed is read from this device word at run time
+ * instead of `seed` (a device-generator draw: HIP-graph replays see new seeds). */
 int dgx_attn_fwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN, int64_t qsH, const void* k,
                  int64_t ksP, int64_t ksB, int64_t ksN, int64_t ksH, const void* v, int64_t vsP, int64_t vsB,
                  int64_t vsN, int64_t vsH, void* o, int64_t osB, int64_t osN, int64_t osH, float* lse, int B, int H,
-                 int Nq, int Nk, int D, float scale, float dropout_p, uint64_t seed, void* stream);
+                 int Nq, int Nk, int D, float scale, float dropout_p, uint64_t seed, const uint64_t* seed_dev,
+                 void* stream);
 /* Gradients of dgx_attn_fwd (same operands, seed and p). dout: dO in the
  * operand format (planes at +gsP for dtype 2) with O's (sB, sN, sH); dout32:
  * dO in fp32 (dtype 2 only, for delta = rowsum(dO . O)); dq/dk/dv fp32 with
@@ -413,7 +416,8 @@ int dgx_attn_bwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN
                  int64_t ksP, int64_t ksB, int64_t ksN, int64_t ksH, const void* v, int64_t vsP, int64_t vsB,
                  int64_t vsN, int64_t vsH, const void* o, const void* dout, int64_t gsP, int64_t osB, int64_t osN,
                  int64_t osH, const float* dout32, const float* lse, float* delta, int B, int H, int Nq, int Nk, int D,
-                 float scale, float dropout_p, uint64_t seed, float* dq, int64_t dqsB, int64_t dqsN, int64_t dqsH,
+                 float scale, float dropout_p, uint64_t seed, const uint64_t* seed_dev, float* dq, int64_t dqsB,
+                 int64_t dqsN, int64_t dqsH,
                  float* dk, int64_t dksB, int64_t dksN, int64_t dksH, float* dv, int64_t dvsB, int64_t dvsN,
                  int64_t dvsH, void* stream);
 /* The keep mask (rows = B*H*Nq, Nk) the kernels draw for (p, seed), u8 0/1. */

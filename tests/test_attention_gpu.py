@@ -102,7 +102,7 @@ def test_attention_dropout_matches_masked_reference(cuda, monkeypatch, p, dt):
     B, H, N, D = 2, 4, 160, 64
     E = H * D
     seed = 0x1234_5678_9ABC
-    monkeypatch.setattr(A, "new_seed", lambda: seed)
+    monkeypatch.setattr(A, "new_seed", lambda dev: torch.tensor([seed], dtype=torch.int64, device=dev))
     q, k, v = _inputs(B, N, N, E, dt, cuda, 21)
     for t in (q, k, v):
         t.requires_grad_(True)
@@ -215,3 +215,53 @@ def test_net_attention_on_engine(cuda):
     out.square().mean().backward()
     for n, p in net.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
+def test_dropout_seed_is_device_drawn_and_graph_safe(cuda):
+    """The dropout seed comes from the device generator (dgx.attention.new_seed):
+    the host RNG stream that shuffles / augmentations draw from is untouched, and
+    a captured graph draws a new mask on every replay instead of baking one in."""
+    from dgx.attention import attention
+    B, H, N, D = 1, 2, 128, 64
+    q, k, v = _inputs(B, N, N, H * D, torch.float16, cuda, 31)
+    torch.manual_seed(0)
+    host = torch.random.get_rng_state()
+    o1 = attention(q, k, v, H, dropout_p=0.5)
+    o2 = attention(q, k, v, H, dropout_p=0.5)
+    assert torch.equal(torch.random.get_rng_state(), host)
+    assert not torch.equal(o1, o2)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        attention(q, k, v, H, dropout_p=0.5)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = attention(q, k, v, H, dropout_p=0.5)
+    g.replay()
+    a = out.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(a, out)
+
+
+@pytest.mark.parametrize("batch_first", [True, False])
+def test_mha_projection_form_follows_operand_identity(cuda, monkeypatch, batch_first):
+    """Self-attention is one (B, N, 3E) in-projection and cross-attention over one
+    memory one (B, M, 2E) projection, whatever batch_first is (the identity of
+    the operands is taken before the sequence-first transpose)."""
+    import dgx.attention as A
+    m = A.EngineMultiheadAttention(128, 2, batch_first=batch_first).to(cuda).eval()
+    calls = []
+    lin = A.F.linear
+    monkeypatch.setattr(A.F, "linear", lambda x, w, b=None: calls.append(tuple(w.shape)) or lin(x, w, b))
+    x = torch.randn(2, 64, 128, device=cuda)
+    mem = torch.randn(2, 96, 128, device=cuda)
+    if not batch_first:
+        x, mem = x.transpose(0, 1), mem.transpose(0, 1)
+    with torch.no_grad():
+        m(x, x, x, need_weights=False)
+        assert calls[0] == (384, 128) and len(calls) == 2, calls
+        calls.clear()
+        m(x, mem, mem, need_weights=False)
+        assert calls[:2] == [(128, 128), (256, 128)] and len(calls) == 3, calls

@@ -46,8 +46,10 @@ def test_models_construct_with_upstream_names():
     assert tuple(pn(torch.randn(2, 3, 64)).shape) == (2, 40)  # PointNet is stock torch: runs on CPU
 
 
-def test_datasets_synthetic_items():
+def test_datasets_synthetic_items(monkeypatch, tmp_path):
     import data
+    monkeypatch.setattr(data, "DATA_DIR", str(tmp_path))
+    monkeypatch.setenv("DGX_SYNTHETIC_DATA", "1")
     mn = data.ModelNet40(1024, "train")
     pc, label = mn[3]
     assert mn.SYNTHETIC and len(mn) == 9840
@@ -84,3 +86,44 @@ def test_augmentations_accept_numpy_and_tensors():
     r = data.rotate_pointcloud(pc.copy())
     assert np.allclose(r[:, 1], pc[:, 1])
     assert np.allclose(np.hypot(r[:, 0], r[:, 2]), np.hypot(pc[:, 0], pc[:, 2]), atol=1e-5)
+
+
+def test_datasets_fail_loudly_without_files(monkeypatch, tmp_path):
+    """No data files and no opt-in: every dataset raises, naming what is missing
+    (the reference would download them, data.py:31-77)."""
+    import pytest
+    import data
+    monkeypatch.setattr(data, "DATA_DIR", str(tmp_path))
+    monkeypatch.delenv("DGX_SYNTHETIC_DATA", raising=False)
+    for make in (lambda: data.ModelNet40(1024), lambda: data.ShapeNetPart(2048), lambda: data.S3DIS(4096),
+                 lambda: data.ShapeNetPart_Augmented("train")):
+        with pytest.raises(FileNotFoundError, match="DGX_SYNTHETIC_DATA"):
+            make()
+
+
+def test_augmented_refuses_pickled_dataset(monkeypatch, tmp_path):
+    """The reference's shapenetpart_<p>_dataset.pt is a pickled TensorDataset: the
+    safe loader refuses it, and the dataset raises naming the file instead of
+    silently switching to synthetic items; a tensors-tuple file loads."""
+    import pytest
+    import data
+    monkeypatch.setattr(data, "DATA_DIR", str(tmp_path))
+    monkeypatch.delenv("DGX_TRUST_PICKLE", raising=False)
+    tensors = (torch.rand(3, 2048, 3), torch.arange(3).view(3, 1), torch.zeros(3, 2048, dtype=torch.int64))
+    torch.save(torch.utils.data.TensorDataset(*tensors), tmp_path / "shapenetpart_train_dataset.pt")
+    with pytest.raises(RuntimeError, match="shapenetpart_train_dataset.pt"):
+        data.ShapeNetPart_Augmented("train")
+    torch.save(tensors, tmp_path / "shapenetpart_test_dataset.pt")
+    ds = data.ShapeNetPart_Augmented("test")
+    assert not ds.SYNTHETIC and len(ds) == 3 and torch.equal(ds[1][0], tensors[0][1])
+
+
+def test_color_palettes_as_scripts_read_them(monkeypatch, tmp_path):
+    """main_partseg.py:164 / main_semseg.py:301 read the datasets' palettes."""
+    import data
+    monkeypatch.setattr(data, "DATA_DIR", str(tmp_path))
+    monkeypatch.setenv("DGX_SYNTHETIC_DATA", "1")
+    pc = data.ShapeNetPart(2048, "test").partseg_colors
+    sc = data.S3DIS(4096, "test").semseg_colors
+    assert pc.shape == (50, 3) and sc.shape == (13, 3)
+    assert pc.min() >= 0 and pc.max() <= 255 and tuple(pc[0]) == (152, 223, 138) and tuple(sc[12]) == (112, 128, 144)

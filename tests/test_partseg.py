@@ -118,6 +118,20 @@ def test_hog_degenerate_neighbourhoods(cuda):
 
 
 @pytest.mark.gpu
+def test_hog_k_range(cuda):
+    """The device HOG's k range is explicit: 5 and 64 run, 4 and 65 raise a clear
+    NotImplementedError naming the range (not a bare C status code)."""
+    from dgx.hog import HOG_K_MAX, HOG_K_MIN
+    from models.model_partseg import compute_hog_1x1
+    x = torch.rand((1, 3, 128), device=cuda)
+    for k in (HOG_K_MIN, HOG_K_MAX):
+        assert compute_hog_1x1(x, k).shape == (1, 128, 18)
+    for k in (HOG_K_MIN - 1, HOG_K_MAX + 1):
+        with pytest.raises(NotImplementedError, match="k <= 64"):
+            compute_hog_1x1(x, k)
+
+
+@pytest.mark.gpu
 def test_hog_use_cpu_places_output(cuda, monkeypatch):
     from models.model_partseg import compute_hog_1x1
     monkeypatch.delenv("LOCAL_RANK", raising=False)
