@@ -581,10 +581,11 @@ def main():
     if not args.no_roofline_leg:
         # the same K steps again with HIP events around ONLY the kNN selection
         # launches (on their launch stream): 8 events per step
-        timing = []
-        dgx_ops.set_knn_timing(timing)
+        timing, seed_timing = [], []
+        dgx_ops.set_knn_timing(timing, seed_timing)
         elapsed_inst = reduce_elapsed(timed_region(step, args.steps, world), world, dev)
         dgx_ops.set_knn_timing(None)
+        seed_ms = sum(e0.elapsed_time(e1) for (e0, e1) in seed_timing) / args.steps
         knn_ms = [e0.elapsed_time(e1) for (e0, e1, _, _) in timing]
         launches = max(1, len(knn_ms))
         avg_ms = sum(knn_ms) / launches
@@ -602,6 +603,7 @@ def main():
             "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "traffic_source": tnote,
             "avg_launch_ms": round(avg_ms, 4), "algorithmic_flops_per_launch": avg_flops,
             "launches_timed": len(knn_ms), "knn_ms_by_layer": per_layer,
+            "seed_ms_per_step": round(seed_ms, 4),
             "timed_region": "second K-step region, events around the kNN selection launches only "
                             "(ms_per_step %.3f)" % (elapsed_inst / args.steps * 1e3)}
     if args.precision != "fp32" and not args.no_fp32_leg:

@@ -398,7 +398,8 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
                                                          const float* __restrict__ xximg,
                                                          const float* __restrict__ xx, int B, int N, int k,
                                                          int nqb, int64_t* __restrict__ idx64,
-                                                         int32_t* __restrict__ idx32, float* __restrict__ vals) {
+                                                         int32_t* __restrict__ idx32, float* __restrict__ vals,
+                                                         const float* __restrict__ seed) {
 #pragma clang fp contract(off)
     constexpr int KL = KnnList<KB>::KL;
     constexpr int RPL = KnnList<KB>::RPL;
@@ -456,7 +457,11 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     float* fv = fval + wave * (KQ_QCAP * 64);
     uint16_t* fj = fidx + wave * (KQ_QCAP * 64);
     int cnt = 0;
-    float thr = -INFINITY;
+    // admission seed (dgx_knn_seed_f32): a lower bound of the row's k-th value
+    // in this kernel's exact arithmetic, so candidates below it can never
+    // enter the top-k; -inf without seeds
+    const float tseed = (seed != nullptr && q < N) ? seed[(int64_t)b * N + q] : -INFINITY;
+    float thr = tseed;
     if (tid < KQ_HALVES * KQ_QPB) pub[tid] = -INFINITY;
     static_assert(KnnList<KB>::KL >= (KB + 3) / 4, "lists must hold the m4-th value");
     __syncthreads();
@@ -493,7 +498,7 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
         t4 = fminf(t4, __shfl_xor(t4, 32));
         if (g == 0) __hip_atomic_store(pub + h * KQ_QPB + qq, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const float tp = __hip_atomic_load(pub + (1 - h) * KQ_QPB + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        thr = fmaxf(fmaxf(t4, fminf(tm, tp)), lv[KL - 1]);
+        thr = fmaxf(fmaxf(fmaxf(t4, fminf(tm, tp)), lv[KL - 1]), tseed);
     };
 
     auto consider = [&](float dot, float xc, int j) {
@@ -628,6 +633,10 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     // exact fix-up pass.
     const float kv = kth[qq];
     if (last != -INFINITY && last >= kv) flg[qq] = 1;
+    // fewer than k candidates reached the seed (the merged k-th is then a -inf
+    // pad): only a seed that is not a value of this kernel's arithmetic does
+    // that; the exact fix-up from T0 = -inf repairs the row
+    if (!(kv >= tseed)) flg[qq] = 1;
     __syncthreads();
     if (q < N && flg[qq] == 0) {  // flagged rows are written by the fix-up below
         const int64_t row = ((int64_t)b * N + q) * k;
@@ -651,6 +660,50 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     }
 }
 
+// ------------------------------------------------------------ seed kernel ----
+// Admission seeds from a candidate subset (e.g. the previous EdgeConv block's
+// neighbours, SURVEY §3.2's dynamic graph): T[q] = min over q's ks seed
+// candidates j of v(q, j), each v in knn_kernel's exact arithmetic — the fmaf
+// chain over c = 0..C-1 of x_j[c] * 2 x_q[c] (what the MFMA chain computes,
+// the zero-padded channels add exact zeros), then (dot - |x_j|^2) - |x_q|^2.
+// ks >= k candidates reach T, so T <= the row's k-th value. G lanes per query,
+// one seed per lane, min over the G lanes.
+template <int G, bool VEC>
+__global__ __launch_bounds__(256) void knn_seed_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
+                                                       int64_t sN, const float* __restrict__ xx, int N, int C,
+                                                       int64_t rows, const int32_t* __restrict__ seeds, int ks,
+                                                       float* __restrict__ T) {
+#pragma clang fp contract(off)
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = t / G;
+    const int s = (int)(t - r * G);
+    float v = INFINITY;
+    if (r < rows && s < ks) {
+        const int b = (int)(r / N), q = (int)(r - (int64_t)b * N);
+        const int j = seeds[r * ks + s];
+        const float* __restrict__ xq = x + b * sB + (int64_t)q * sN;
+        const float* __restrict__ xj = x + b * sB + (int64_t)j * sN;
+        float d = 0.f;
+        if constexpr (VEC) {
+            for (int c = 0; c < C; c += 4) {
+                const float4 a = *reinterpret_cast<const float4*>(xj + c);
+                const float4 e = *reinterpret_cast<const float4*>(xq + c);
+                d = fmaf(a.x, 2.0f * e.x, d);
+                d = fmaf(a.y, 2.0f * e.y, d);
+                d = fmaf(a.z, 2.0f * e.z, d);
+                d = fmaf(a.w, 2.0f * e.w, d);
+            }
+        } else {
+            for (int c = 0; c < C; ++c) d = fmaf(xj[c * sC], 2.0f * xq[c * sC], d);
+        }
+        const float tq = d - xx[(int64_t)b * N + j];
+        v = tq - xx[r];
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) v = fminf(v, __shfl_xor(v, o));
+    if (s == 0 && r < rows) T[r] = v;
+}
+
 // image floats per cloud, then |x|^2 image floats per cloud
 inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
 inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
@@ -668,18 +721,19 @@ int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
 template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
-               hipStream_t st) {
+               const float* seed, hipStream_t st) {
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
-                       xximg, xx, B, N, k, nqb, idx64, idx32, vals);
+                       xximg, xx, B, N, k, nqb, idx64, idx32, vals, seed);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 template <int NSTEP>
 int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, hipStream_t st) {
+               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, const float* seed,
+               hipStream_t st) {
 #define DGX_KNN_K(KBV) \
-    return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st)
+    return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st)
     if (k <= 16) DGX_KNN_K(16);
     if (k <= 20) DGX_KNN_K(20);
     if (k <= 32) DGX_KNN_K(32);
@@ -753,9 +807,9 @@ int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int 
     }
 }
 
-int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                       int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes,
-                       void* stream) {
+int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
+                              int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image,
+                              size_t image_bytes, const float* seed, void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
@@ -766,12 +820,39 @@ int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const
     const float* xximg = img + (size_t)B * knn_image_floats(C, N);
     hipStream_t st = dgx_stream(stream);
     switch (knn_nstep(C)) {
-        case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
-        case 3: return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
-        case 8: return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
-        case 16: return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
-        default: return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
+        case 3: return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
+        case 8: return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
+        case 16: return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
+        default: return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
     }
+}
+
+int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
+                       int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes,
+                       void* stream) {
+    return dgx_knn_select_seeded_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes, nullptr,
+                                     stream);
+}
+
+int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
+                     const int32_t* seeds, int ks, float* T, void* stream) {
+    if (!x || !xx || !seeds || !T || B < 0 || C < 1 || N < 1 || ks < 1 || ks > 64) return DGX_EINVAL;
+    if (C > 128) return DGX_EUNSUPPORTED;
+    if (B == 0) return DGX_OK;
+    const int64_t rows = (int64_t)B * N;
+    const bool vec = sC == 1 && C % 4 == 0 && sN % 4 == 0 && sB % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    hipStream_t st = dgx_stream(stream);
+    if (ks <= 32) {
+        const unsigned grid = (unsigned)((rows * 32 + 255) / 256);
+        if (vec) hipLaunchKernelGGL((knn_seed_kernel<32, true>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
+        else hipLaunchKernelGGL((knn_seed_kernel<32, false>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
+    } else {
+        const unsigned grid = (unsigned)((rows * 64 + 255) / 256);
+        if (vec) hipLaunchKernelGGL((knn_seed_kernel<64, true>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
+        else hipLaunchKernelGGL((knn_seed_kernel<64, false>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
+    }
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int k, int order,

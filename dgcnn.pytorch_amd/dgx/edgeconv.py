@@ -34,6 +34,13 @@ from .ops import knn_raw, reduction_order
 
 _tls = threading.local()
 
+# blocks 2-4: seed each kNN's admission bound with the previous block's graph
+# (dgx_knn_seed_f32). Off: measured at cfg2 the selection kernels gain 18 / 18 /
+# 6 us (C = 64 / 64 / 128, they are bound by the operand stream, not the
+# lists) while the seed pass costs 3 x 58 us (profiles/r03e: a gather of 20
+# neighbour rows per query).
+KNN_SEEDS = False
+
 
 def debug_capture():
     """Per-thread capture dict for tests/tools (None when off): forward stores each
@@ -136,8 +143,12 @@ class _EdgeConvStack(torch.autograd.Function):
                 X = xcat[:, off_in:off_in + cin]
                 # the reference's blocks 2-4 see contiguous (B,C,N) features (max over
                 # dim -1 of a contiguous tensor), hence the strided rounding order
+                # optionally the previous block's neighbours seed the admission bound:
+                # feature-space neighbourhoods of consecutive blocks overlap (~1.3 k
+                # candidates then reach it)
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
-                              strides=(N * total, 1, total), shape=(B, cin, N))
+                              strides=(N * total, 1, total), shape=(B, cin, N),
+                              seeds=idx if KNN_SEEDS else None)
             wprep = None
             if cin <= G.SMALLK_MAX:
                 # raw coordinates (block 1, K = 3): exact fp32 in every mode

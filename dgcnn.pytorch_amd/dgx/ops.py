@@ -30,9 +30,14 @@ def _as_f32(x):
     return x if x.dtype == torch.float32 else x.float()
 
 
-def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False):
+def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False, seeds=None):
     """kNN on a (B,C,N) fp32 view. ``strides``/``shape`` let callers describe a
-    strided slice of a larger buffer (the engine's point-major concat buffer)."""
+    strided slice of a larger buffer (the engine's point-major concat buffer).
+    ``seeds``: optional int32 (B, N, ks >= k) candidate ids per query (e.g. the
+    previous EdgeConv block's neighbours): the min of their distances is a
+    lower bound of each row's k-th value (dgx_knn_seed_f32) that lets the
+    selection skip the candidates below it. The result does not depend on the
+    seeds (a row whose seed were too high is recomputed exactly)."""
     nat.require_device(x)
     B, C, N = shape if shape is not None else x.shape
     sB, sC, sN = strides if strides is not None else x.stride()
@@ -54,13 +59,29 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
         nat.check(L.dgx_knn_prepare_f32(nat.f32(x), sB, sC, sN, B, C, N, order, nat.f32(xx), nat.f32(img),
                                         img_bytes, stream), "knn prepare")
         timing = getattr(_tls, "timing", None)
+        T = None
+        if seeds is not None:
+            if seeds.dtype != torch.int32 or not seeds.is_contiguous() or seeds.shape[:2] != (B, N) \
+                    or not k <= seeds.shape[2] <= 64:
+                raise RuntimeError("knn seeds: int32 contiguous (B, N, ks) with k <= ks <= 64")
+            T = torch.empty((B * N,), dtype=torch.float32, device=x.device)
+            if timing is not None:
+                es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                es0.record()
+            nat.check(L.dgx_knn_seed_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, nat.i32(seeds),
+                                         seeds.shape[2], nat.f32(T), stream), "knn seed")
+            if timing is not None:
+                es1.record()
+                seed_log = getattr(_tls, "seed_timing", None)
+                if seed_log is not None:
+                    seed_log.append((es0, es1))
         if timing is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        rc = L.dgx_knn_select_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
-                                  nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
-                                  nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
-                                  nat.f32(img), img_bytes, stream)
+        rc = L.dgx_knn_select_seeded_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
+                                         nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
+                                         nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
+                                         nat.f32(img), img_bytes, nat.f32(T), stream)
         if timing is not None:
             ev1.record()
             timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
@@ -68,11 +89,13 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     return (idx, vals) if return_values else idx
 
 
-def set_knn_timing(lst):
+def set_knn_timing(lst, seed_lst=None):
     """Optional per-thread instrumentation (tools): when a list, every kNN
     selection launch of this thread appends (start_event, end_event,
-    gram_flops, shape) recorded on the launch stream."""
+    gram_flops, shape) recorded on the launch stream; ``seed_lst`` collects
+    (start_event, end_event) of the admission-seed launches."""
     _tls.timing = lst
+    _tls.seed_timing = seed_lst
 
 
 def knn(x, k):

@@ -78,6 +78,22 @@ int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                        const float* xx, int B, int C, int N, int k,
                        int64_t* idx64, int32_t* idx32, float* vals,
                        const void* image, size_t image_bytes, void* stream);
+/* dgx_knn_select_f32 with admission seeds: seed (B*N fp32, or NULL) holds a
+ * lower bound of each row's k-th value in the selection's exact arithmetic
+ * (dgx_knn_seed_f32); candidates below it are skipped without list work. A
+ * row whose admitted candidates fall short of k is recomputed exactly, so the
+ * output equals dgx_knn_select_f32's for any seed. */
+int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
+                              int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image,
+                              size_t image_bytes, const float* seed, void* stream);
+/* Admission seeds from a candidate subset (reference dgcnn.py:88-98: blocks
+ * 2-4 search a feature space whose neighbourhoods overlap the previous
+ * block's): T[b*N+q] = min over the ks local ids seeds[(b*N+q)*ks + s] of the
+ * negated squared distance (dgcnn.py:7-9) as the selection kernel computes it
+ * (fmaf chain over the channels with the query doubled, xx from
+ * dgx_knn_prepare_f32). ks >= k makes T a lower bound of the k-th value. */
+int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
+                     const int32_t* seeds, int ks, float* T, void* stream);
 
 /* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
  * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in

@@ -160,3 +160,38 @@ def test_knn_prepare_norms_match_sqnorm(cuda, B, C, N, layout):
     np.testing.assert_array_equal(xx0.cpu().numpy().view(np.uint32), xx1.cpu().numpy().view(np.uint32))
     ref = oracle.sqnorm(_cpu_view(pts, layout)).reshape(-1)
     np.testing.assert_array_equal(xx1.cpu().numpy().view(np.uint32), ref.astype(np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("C,N,k,layout", [(64, 1024, 20, "pm"), (128, 2048, 40, "pm"), (64, 777, 20, "bcn"),
+                                          (3, 500, 16, "perm"), (9, 1000, 20, "bcn")])
+def test_knn_seeded_equals_unseeded(cuda, C, N, k, layout):
+    """Admission seeds (dgx_knn_seed_f32 + dgx_knn_select_seeded_f32) never change
+    the result: seeded by the exact kNN itself (the bound equals the k-th
+    value: only the top-k and its ties are admitted), by random distinct ids (a
+    loose bound), by another layer's graph (what EdgeConv blocks 2-4 pass), and
+    by an INVALID seed list (k copies of the query itself: the bound exceeds
+    the k-th value, every row falls short of k admitted candidates and is
+    recomputed exactly by the fix-up) — all bit-identical to the unseeded kNN
+    and to the oracle."""
+    import oracle
+    from dgx import synth
+    from dgx.ops import knn_raw
+    B = 2
+    if C == 3:
+        f = torch.from_numpy(synth.cube_clouds(B, N, 5)).permute(0, 2, 1)
+    else:
+        f = torch.from_numpy(synth.relu_normal(6 + C, (B, C, N)))
+    if layout == "pm":   # point-major memory, as the engine's concat buffer
+        f = f.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+    elif layout == "perm":
+        f = f.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+    x = f.to(cuda)
+    base = knn_raw(x, k, out_dtype=torch.int32)
+    np.testing.assert_array_equal(base.cpu().numpy(), oracle.knn(f, k))
+    g = torch.Generator().manual_seed(C + N)
+    rnd = torch.argsort(torch.rand(B, N, N, generator=g), dim=-1)[..., :k + 3].to(torch.int32)
+    other = knn_raw((x * x).contiguous(), k, out_dtype=torch.int32)        # a different graph of the same points
+    selfs = torch.arange(N, dtype=torch.int32).view(1, N, 1).expand(B, N, k).contiguous()
+    for name, seeds in (("exact", base), ("random", rnd), ("other graph", other), ("invalid", selfs)):
+        got = knn_raw(x, k, out_dtype=torch.int32, seeds=seeds.to(cuda).contiguous())
+        assert torch.equal(got, base), name
