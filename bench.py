@@ -227,7 +227,15 @@ def edgeconv_legs(model, x, reps=10):
     return res
 
 
-def eager_reference_step_ms(x, k, emb, autocast_dtype=None, reps=5):
+def eager_edgeconv_ms(x, k, autocast_dtype=None, reps=5):
+    """The metric's EdgeConv number in stock PyTorch-ROCm eager: the reference's
+    4 EdgeConv blocks (models/dgcnn.py:84-98: get_graph_feature -> Conv2d -> BN
+    -> LeakyReLU -> max over k) fwd+bwd on this GPU, the same work
+    edgeconv_fwd_bwd_ms["chain"] times for the engine."""
+    return eager_reference_step_ms(x, k, None, autocast_dtype=autocast_dtype, reps=reps, chain_only=True)
+
+
+def eager_reference_step_ms(x, k, emb, autocast_dtype=None, reps=5, chain_only=False):
     """The reference's DGCNN op sequence (models/dgcnn.py:6-103: matmul, sum,
     topk, index gather, repeat, cat, permute, conv, BN, LeakyReLU, max) in stock
     PyTorch-ROCm eager on this GPU: the single-GPU denominator of the >=10x
@@ -257,8 +265,8 @@ def eager_reference_step_ms(x, k, emb, autocast_dtype=None, reps=5):
         convs.append(nn.Sequential(nn.Conv2d(2 * c, w, 1, bias=False), nn.BatchNorm2d(w),
                                    nn.LeakyReLU(0.2, inplace=True)).to(dev))
         c = w
-    c5 = nn.Sequential(nn.Conv2d(512, emb, 1, bias=False), nn.BatchNorm2d(emb),
-                       nn.LeakyReLU(0.2, inplace=True)).to(dev)
+    c5 = None if chain_only else nn.Sequential(nn.Conv2d(512, emb, 1, bias=False), nn.BatchNorm2d(emb),
+                                               nn.LeakyReLU(0.2, inplace=True)).to(dev)
     ctx = (torch.autocast("cuda", dtype=autocast_dtype) if autocast_dtype is not None
            else contextlib.nullcontext())
 
@@ -268,7 +276,10 @@ def eager_reference_step_ms(x, k, emb, autocast_dtype=None, reps=5):
             for m in convs:
                 h = m(gf(h)).max(dim=-1, keepdim=False)[0]
                 feats.append(h)
-            y = c5(torch.cat(feats, dim=1).unsqueeze(-1)).view(x.shape[0], -1, x.shape[2])
+            if chain_only:
+                y = torch.cat(feats, dim=1)
+            else:
+                y = c5(torch.cat(feats, dim=1).unsqueeze(-1)).view(x.shape[0], -1, x.shape[2])
         y.backward(upstream_grad(y.shape, dev).to(y.dtype))
     return _ms(step, reps, warm=1)
 
@@ -363,7 +374,14 @@ def cpu_baseline(args, clouds):
     from models.dgcnn import DGCNN
     sys.path.insert(0, REPO)
     from oracle import reference as R
-    threads = torch.get_num_threads()  # honours OMP_NUM_THREADS: the cores this job is given
+    # every host CPU this process may run on (its affinity set: the box's share of
+    # the machine's cores; os.cpu_count() counts the whole machine's)
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
     model = DGCNN(types.SimpleNamespace(emb_dim=args.emb, k=args.k, in_dims=args.in_dims))
     params = {n: t.detach().clone() for n, t in model.state_dict().items()}
@@ -383,12 +401,14 @@ def cpu_baseline(args, clouds):
         times.append(time.perf_counter() - t0)
     times.sort()
     med = times[len(times) // 2]
+    torch.set_num_threads(prev_threads)
     return {"value": round(clouds / med, 3), "unit": "clouds/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(),
             "min_ms": round(times[0] * 1e3, 1), "median_ms": round(med * 1e3, 1), "reps": len(times),
             "sample": f"oracle/reference.py DGCNN(emb={args.emb}) train fwd+bwd on the full {clouds}-cloud batch "
                       f"({args.points} pts, k={args.k}); median of {len(times)} after 1 warm-up; torch CPU with "
-                      f"{threads} threads (OMP_NUM_THREADS share of the box's {os.cpu_count()} CPUs)"}
+                      f"{threads} threads (every CPU in this process's affinity set; the machine has "
+                      f"{os.cpu_count()})"}
 
 
 def make_input(args, clouds, seed):
@@ -455,11 +475,13 @@ def main():
     torch.manual_seed(0)
     model = DGCNN(types.SimpleNamespace(emb_dim=args.emb, k=args.k, in_dims=args.in_dims)).to(dev).train()
     net = model
-    # N > 1 without SyncBN: each rank's fwd + bwd is one HIP graph accumulating
-    # every parameter gradient into ONE flat buffer, then ONE collective
-    # all-reduce of it (sum / N: DDP's averaging) and the fused SGD step; with
-    # --sync-bn (collectives inside the forward / backward) or --no-graph: DDP
-    flat_dp = world > 1 and not args.sync_bn and not args.no_graph
+    # N > 1: each rank's fwd + bwd is one HIP graph accumulating every
+    # parameter gradient into ONE flat buffer, then ONE collective all-reduce
+    # of it (sum / N: DDP's averaging) and the fused SGD step. With --sync-bn
+    # over RCCL the BN-statistics all-reduces (no host synchronisation, dgx.dist)
+    # are captured inside that graph; over gloo (host collectives, not
+    # capturable) or with --no-graph the step runs eagerly under DDP
+    flat_dp = world > 1 and not args.no_graph and (not args.sync_bn or args.backend == "nccl")
     if world > 1:
         if args.sync_bn:
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
@@ -551,7 +573,7 @@ def main():
             reduce_and_step()
         for _ in range(2):
             run()
-        launch = "hip_graph+allreduce"
+        launch = "hip_graph+allreduce" + ("(+syncbn collectives in graph)" if args.sync_bn else "")
     # headline: the timed region runs uninstrumented
     elapsed = reduce_elapsed(timed_region(run, args.steps, world), world, dev)
     result = {
@@ -617,7 +639,19 @@ def main():
         dgx_prec.set(args.precision)
     if rank == 0 and world == 1:
         if not args.no_edgeconv_leg:
-            result["edgeconv_fwd_bwd_ms"] = edgeconv_legs(model, x)
+            legs = edgeconv_legs(model, x)
+            if not args.no_eager_baseline:
+                # the same 4-block chain in stock PyTorch-ROCm eager (the metric's EdgeConv ratio)
+                for name, dt in (("fp32", None), ("bf16_autocast", torch.bfloat16)):
+                    try:
+                        legs[f"torch_eager_{name}"] = round(eager_edgeconv_ms(x, args.k, autocast_dtype=dt), 3)
+                    except RuntimeError as e:
+                        legs[f"torch_eager_{name}"] = {"error": str(e)[:200]}
+                    torch.cuda.empty_cache()
+                ref = legs.get(f"torch_eager_{'fp32' if args.precision == 'fp32' else 'bf16_autocast'}")
+                if isinstance(ref, float):
+                    legs["engine_speedup_vs_eager"] = round(ref / legs["chain"], 2)
+            result["edgeconv_fwd_bwd_ms"] = legs
         if not args.no_posemb_leg:
             result["posemb_edge_mlp"] = posemb_edge_leg(dev)
         if not args.no_attention_leg:

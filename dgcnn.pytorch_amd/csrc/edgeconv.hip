@@ -379,6 +379,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ 
         __syncthreads();
     }
     if (t != 0) return;
+    // count < 0: the element count follows the sums on the device (SyncBatchNorm:
+    // all-reduced with them, never read back to the host)
+    if (count < 0.0) count = (double)partials[(int64_t)nrows * 2 * Co];
     const double mean = r1[0] / count;
     double var = r2[0] / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -561,6 +564,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const T* __restric
     if (t != 0) return;
     s1 = r1[0];
     s2 = r2[0];
+    if (count < 0.0) count = (double)partials[(int64_t)nrows * 2 * Co];   // device-side count, as above
     if (dbeta) dbeta[o] = (float)(accumulate ? (double)dbeta[o] + s1 : s1);
     if (dgamma) dgamma[o] = (float)(accumulate ? (double)dgamma[o] + s2 : s2);
     const double a = scale[o], mu = mean[o], is = invstd[o];
@@ -1047,7 +1051,7 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count, 
 int dgx_bn_finalize_f64(const double* sums, int nrows, int Co, double count, const float* gamma, const float* beta,
                         float* running_mean, float* running_var, double momentum, double eps, float* scale,
                         float* shift, float* mean, float* invstd, int64_t* num_batches_tracked, void* stream) {
-    if (!sums || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
+    if (!sums || nrows < 1 || Co < 1 || count == 0.0 || !scale || !shift) return DGX_EINVAL;
     hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
                        num_batches_tracked);
@@ -1119,7 +1123,7 @@ int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co, double cou
 int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co, double count, const float* scale,
                             const float* mean, const float* invstd, float* dgamma, float* dbeta, float* c0,
                             float* c1, int accumulate, void* stream) {
-    if (!sums || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !mean || !invstd || !c0 || !c1)
+    if (!sums || nrows < 1 || Co < 1 || count == 0.0 || !scale || !mean || !invstd || !c0 || !c1)
         return DGX_EINVAL;
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, scale, mean, invstd, dgamma, dbeta, c0, c1, accumulate);

@@ -399,7 +399,11 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
                                                          const float* __restrict__ xx, int B, int N, int k,
                                                          int nqb, int64_t* __restrict__ idx64,
                                                          int32_t* __restrict__ idx32, float* __restrict__ vals,
-                                                         const float* __restrict__ seed) {
+                                                         const float* __restrict__ seed
+#ifdef DGX_KNN_STATS
+                                                         , uint32_t* __restrict__ stats
+#endif
+                                                         ) {
 #pragma clang fp contract(off)
     constexpr int KL = KnnList<KB>::KL;
     constexpr int RPL = KnnList<KB>::RPL;
@@ -465,7 +469,13 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     if (tid < KQ_HALVES * KQ_QPB) pub[tid] = -INFINITY;
     static_assert(KnnList<KB>::KL >= (KB + 3) / 4, "lists must hold the m4-th value");
     __syncthreads();
+#ifdef DGX_KNN_STATS
+    uint32_t n_rounds = 0, n_flush = 0;
+#endif
     auto flush = [&]() {
+#ifdef DGX_KNN_STATS
+        ++n_flush;
+#endif
         // branch-free rounds: slots past a lane's count read stale entries and
         // are replaced by -inf, so every round is the same straight-line code
         float cv = fv[lane];
@@ -475,6 +485,9 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
 #pragma unroll
         for (int t = 0; t < KQ_QCAP; ++t) {
             if (!__any(t < cnt)) break;
+#ifdef DGX_KNN_STATS
+            ++n_rounds;
+#endif
             const int nx = min(t + 1, KQ_QCAP - 1);
             float nv = fv[nx * 64 + lane];
             const int nj = fj[nx * 64 + lane];
@@ -650,6 +663,16 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
             }
         }
     }
+#ifdef DGX_KNN_STATS
+    {   // diagnostics build only: per (block, wave) insertion rounds, flushes, flagged rows (vector stores)
+        int nf = 0;
+        for (int f = 0; f < KQ_QPB; ++f) nf += (flg[f] != 0 && qb * KQ_QPB + f < N) ? 1 : 0;
+        if (lane == 0 && stats != nullptr) {
+            uint32_t* st = stats + ((int64_t)blockIdx.x * KQ_WAVES + wave) * 4;
+            st[0] = n_rounds; st[1] = n_flush; st[2] = wave == 0 ? (uint32_t)nf : 0u; st[3] = 1u;
+        }
+    }
+#endif
     // the block's flagged rows (rare), one at a time; flg / kth are block-uniform LDS reads
     float* fixa = smem + KQ_HALVES * KQ_QPB * KB * 2 + 2 * KQ_QPB;
     for (int f = 0; f < KQ_QPB; ++f) {
@@ -704,6 +727,133 @@ __global__ __launch_bounds__(256) void knn_seed_kernel(const float* __restrict__
     if (s == 0 && r < rows) T[r] = v;
 }
 
+// ------------------------------------------------------- spatial seeds ----
+// Coordinate clouds (C <= 4: the xyz kNN of DGCNN's first block,
+// PositionEmbedding and compute_hog_1x1): streamed in index order, the
+// selection's lists keep admitting candidates for the whole stream (a random
+// cloud holds no spatial order; 53 insertion rounds per wave at cfg2, 83 at
+// k 40, measured) and the kernel sat at 2.3 % of the MFMA peak. A spatial
+// seed makes the bound tight from the first tile: order the cloud along a
+// Morton curve of an 8^3 cell grid (counting sort), take for each query the 64
+// points around it in that order, and seed the selection with their k-th best
+// value (exact arithmetic, knn_seed_kernel's argument: 64 >= k candidates
+// reach it, so it never exceeds the row's k-th value).
+constexpr int SP_MINN = 256;
+constexpr int SP_MAXN = 4096;
+constexpr int SP_THREADS = 1024;
+constexpr int SP_WIN = 64;
+constexpr int SP_CELLS = 512;   // 8 x 8 x 8
+
+inline bool knn_spatial_ok(int C, int N) { return C <= 4 && N >= SP_MINN && N <= SP_MAXN; }
+
+// 3-bit coordinate -> every third bit of 9
+__device__ __forceinline__ uint32_t spread3b(uint32_t v) {
+    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
+}
+
+// perm[b*N + p] = id of the p-th point along the cell curve (points of one
+// cell in arrival order: the order only shapes the seed windows, never a result)
+__global__ __launch_bounds__(SP_THREADS) void knn_cell_order_kernel(const float* __restrict__ x, int64_t sB,
+                                                                    int64_t sC, int64_t sN, int C, int N,
+                                                                    int32_t* __restrict__ perm) {
+    __shared__ int cnt[SP_CELLS];
+    __shared__ int scan[SP_THREADS];
+    __shared__ unsigned short cellof[SP_MAXN];
+    __shared__ float red[2][3][SP_THREADS / 64];
+    __shared__ float box[2][3];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* __restrict__ xb = x + b * sB;
+    const int D = C < 3 ? C : 3;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int n = tid; n < N; n += SP_THREADS)
+        for (int d = 0; d < D; ++d) {
+            const float v = xb[d * sC + n * sN];
+            lo[d] = fminf(lo[d], v);
+            hi[d] = fmaxf(hi[d], v);
+        }
+    for (int d = 0; d < 3; ++d) {
+        for (int o = 1; o < 64; o <<= 1) {
+            lo[d] = fminf(lo[d], __shfl_xor(lo[d], o));
+            hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], o));
+        }
+        if (lane == 0) { red[0][d][wave] = lo[d]; red[1][d][wave] = hi[d]; }
+    }
+    for (int c = tid; c < SP_CELLS; c += SP_THREADS) cnt[c] = 0;
+    __syncthreads();
+    if (tid < 3) {
+        float l = INFINITY, h = -INFINITY;
+        for (int w = 0; w < SP_THREADS / 64; ++w) { l = fminf(l, red[0][tid][w]); h = fmaxf(h, red[1][tid][w]); }
+        box[0][tid] = l;
+        box[1][tid] = h;
+    }
+    __syncthreads();
+    for (int n = tid; n < N; n += SP_THREADS) {
+        uint32_t code = 0;
+        for (int d = 0; d < D; ++d) {
+            const float l = box[0][d], w = box[1][d] - l;
+            const float t = w > 0.f ? (xb[d * sC + n * sN] - l) * (8.f / w) : 0.f;
+            code |= spread3b((uint32_t)fminf(fmaxf(t, 0.f), 7.f)) << d;
+        }
+        cellof[n] = (unsigned short)code;
+        atomicAdd(&cnt[code], 1);
+    }
+    __syncthreads();
+    // exclusive scan of the cell counts (one cell per thread, Hillis-Steele over the block)
+    int v = tid < SP_CELLS ? cnt[tid] : 0;
+    scan[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < SP_CELLS; o <<= 1) {
+        const int add = tid >= o ? scan[tid - o] : 0;
+        __syncthreads();
+        scan[tid] += add;
+        __syncthreads();
+    }
+    if (tid < SP_CELLS) cnt[tid] = scan[tid] - v;   // start of the cell
+    __syncthreads();
+    for (int n = tid; n < N; n += SP_THREADS) {
+        const int pos = atomicAdd(&cnt[cellof[n]], 1);
+        perm[(int64_t)b * N + pos] = n;
+    }
+}
+
+// T[b*N + q] = the k-th best value over the 64 points around q along the cell
+// curve, each value in knn_kernel's exact arithmetic (the fmaf chain over the
+// C <= 4 channels with the query doubled, then - |x_j|^2 - |x_q|^2). One wave
+// per query: lane = window candidate, a 64-lane bitonic sort, lane 64 - k.
+__global__ __launch_bounds__(256) void knn_window_seed_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
+                                                              int64_t sN, int C, const float* __restrict__ xx,
+                                                              int B, int N, int k, const int32_t* __restrict__ perm,
+                                                              float* __restrict__ T) {
+#pragma clang fp contract(off)
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= (int64_t)B * N) return;   // wave-uniform
+    const int b = (int)(r / N), p = (int)(r - (int64_t)b * N);
+    const int32_t* __restrict__ pb = perm + (int64_t)b * N;
+    const float* __restrict__ xb = x + b * sB;
+    const int q = pb[p];
+    const int w0 = min(max(p - SP_WIN / 2, 0), N - SP_WIN);
+    const int j = pb[w0 + lane];
+    float d = 0.f;
+    for (int c = 0; c < C; ++c) d = fmaf(xb[c * sC + (int64_t)j * sN], 2.0f * xb[c * sC + (int64_t)q * sN], d);
+    const float tq = d - xx[(int64_t)b * N + j];
+    float v = tq - xx[(int64_t)b * N + q];
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const float o = __shfl_xor(v, stride);
+            const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0 || size == 64);
+            v = keep_min ? fminf(v, o) : fmaxf(v, o);
+        }
+    const float tk = __shfl(v, SP_WIN - k);   // ascending: the k-th largest
+    if (lane == 0) T[(int64_t)b * N + q] = tk;
+}
+
+#ifdef DGX_KNN_STATS
+uint32_t* g_knn_stats = nullptr;   // diagnostics build: device buffer set by dgx_knn_stats_buffer
+#endif
+
 // image floats per cloud, then |x|^2 image floats per cloud
 inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
 inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
@@ -724,7 +874,11 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
                const float* seed, hipStream_t st) {
     const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
-                       xximg, xx, B, N, k, nqb, idx64, idx32, vals, seed);
+                       xximg, xx, B, N, k, nqb, idx64, idx32, vals, seed
+#ifdef DGX_KNN_STATS
+                       , g_knn_stats
+#endif
+                       );
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -745,6 +899,12 @@ int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
 }  // namespace
 
 extern "C" {
+
+#ifdef DGX_KNN_STATS
+// diagnostics build only (tools/knn_stats.py): per (block, wave) of the next
+// selection launch, {insertion rounds, flushes, flagged rows, 1} as uint32
+void dgx_knn_stats_buffer(void* dev) { g_knn_stats = static_cast<uint32_t*>(dev); }
+#endif
 
 const char* dgx_knn_kernel_name(int C, int k) {
     // the selection kernel dgx_knn_select_f32 launches for (C, k), as profilers print it
@@ -852,6 +1012,19 @@ int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const f
         if (vec) hipLaunchKernelGGL((knn_seed_kernel<64, true>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
         else hipLaunchKernelGGL((knn_seed_kernel<64, false>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
     }
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_knn_spatial_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
+                             int N, int k, int32_t* perm, float* T, void* stream) {
+    if (!x || !xx || !perm || !T || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
+    if (!knn_spatial_ok(C, N) || k > SP_WIN) return DGX_EUNSUPPORTED;
+    if (B == 0) return DGX_OK;
+    hipStream_t st = dgx_stream(stream);
+    hipLaunchKernelGGL(knn_cell_order_kernel, dim3((unsigned)B), dim3(SP_THREADS), 0, st, x, sB, sC, sN, C, N, perm);
+    DGX_CHECK_LAUNCH();
+    const unsigned grid = (unsigned)(((int64_t)B * N + 3) / 4);
+    hipLaunchKernelGGL(knn_window_seed_kernel, dim3(grid), dim3(256), 0, st, x, sB, sC, sN, C, xx, B, N, k, perm, T);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

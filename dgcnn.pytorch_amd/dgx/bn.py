@@ -85,8 +85,8 @@ def batch_stats(partials, rows, count, bn, gamma, beta, stream):
     sync, group = dist_.sync_group(bn)
     partials, rows = _compact(partials, rows, co, stream)
     if sync:  # SyncBatchNorm: statistics of the global batch, one fp64 all-reduce
-        sums, gcount = dist_.allreduce_sums(partials, count, group)
-        nat.check(L.dgx_bn_finalize_f64(nat.ptr(sums, nat.F64), 1, co, gcount, nat.f32(gamma), nat.f32(beta), rm, rv,
+        sums = dist_.allreduce_sums(partials, count, group)   # (2C + 1) fp64: sums | global count
+        nat.check(L.dgx_bn_finalize_f64(nat.ptr(sums, nat.F64), 1, co, -1.0, nat.f32(gamma), nat.f32(beta), rm, rv,
                                         factor, float(bn.eps), nat.f32(scale), nat.f32(shift), nat.f32(mean),
                                         nat.f32(invstd), nat.ptr(nbt, nat.I64), stream), "bn finalize")
     else:
@@ -129,8 +129,8 @@ def backward_consts(partials, rows, count, st, stream):
             c0.zero_()
             c1.zero_()
     else:  # SyncBatchNorm: input gradient from global sums, gamma/beta grads rank-local
-        sums, gcount = dist_.allreduce_sums(partials, count, st.group)
-        nat.check(L.dgx_bn_bwd_finalize_f64(nat.ptr(sums, nat.F64), 1, co, gcount, *args, None, None, nat.f32(c0),
+        sums = dist_.allreduce_sums(partials, count, st.group)
+        nat.check(L.dgx_bn_bwd_finalize_f64(nat.ptr(sums, nat.F64), 1, co, -1.0, *args, None, None, nat.f32(c0),
                                             nat.f32(c1), 0, stream), "bn bwd finalize")
         loc = partials.double().sum(0)
         dbeta.copy_(loc[0])

@@ -35,11 +35,13 @@ def sync_group(bn):
 
 def allreduce_sums(partials, count, group):
     """partials: (rows, 2, C) fp32 per-block column sums; count: local element
-    count. Returns (global sums (2, C) fp64 contiguous, global count) with ONE
-    all-reduce."""
+    count. Returns the (2C + 1) fp64 buffer [global sums (2, C) | global count]
+    after ONE all-reduce. The count stays on the device: the fp64 finalize
+    kernels read it there (count argument -1), so no host synchronisation sits
+    on the SyncBatchNorm critical path and the step stays graph-capturable."""
     C = partials.shape[-1]
     buf = torch.empty(2 * C + 1, dtype=torch.float64, device=partials.device)
-    buf[:2 * C] = partials.double().sum(0).reshape(-1)
-    buf[2 * C] = float(count)
+    torch.sum(partials.double(), dim=0, out=buf[:2 * C].view(2, C))
+    buf[2 * C:].fill_(float(count))
     dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    return buf[:2 * C].view(2, C), float(buf[2 * C].item())
+    return buf

@@ -4,6 +4,7 @@
 shapes and dtypes; the work is done by libdgx.so on the tensor's own device
 and current stream.
 """
+import contextlib
 import threading
 
 import torch
@@ -11,6 +12,14 @@ import torch
 from . import _native as nat
 
 _tls = threading.local()
+
+# coordinate clouds (C <= 4, 256 <= N <= 4096): seed the selection with the
+# k-th value of each point's 64 neighbours along a Morton curve of the cloud
+# (dgx_knn_spatial_seed_f32). Off: measured (profiles/r03i_knn_seed_stats.log)
+# the seeds cut the insertion rounds per wave 53 -> 15.5 (k 20) and 83 -> 55
+# (k 40) and the selection 56 -> 44 / 208 -> 185 us, but the two seed launches
+# cost 11 + 23 us per call (latency-bound gathers): no net gain yet.
+SPATIAL_SEEDS = False
 
 
 def reduction_order(x):
@@ -47,6 +56,13 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
         raise RuntimeError(f"knn: selected index k out of range (k={k}, N={N})")
     if C > 128 or k > 64:
         raise NotImplementedError(f"dgx knn kernels are built for C <= 128 and k <= 64 (C={C}, k={k})")
+    cache = getattr(_tls, "cache", None)
+    key = None
+    if cache is not None and seeds is None and not return_values:
+        key = (x.device, x.data_ptr(), (B, C, N), (sB, sC, sN), x._version, k, order)
+        hit = cache.get(key)
+        if hit is not None:
+            return hit if hit.dtype == out_dtype else hit.to(out_dtype)
     L = nat.lib()
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
     vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
@@ -60,6 +76,20 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
                                         img_bytes, stream), "knn prepare")
         timing = getattr(_tls, "timing", None)
         T = None
+        spatial = seeds is None and SPATIAL_SEEDS and C <= 4 and 256 <= N <= 4096 and k <= 64
+        if spatial:
+            T = torch.empty((B * N,), dtype=torch.float32, device=x.device)
+            perm = torch.empty((B * N,), dtype=torch.int32, device=x.device)
+            if timing is not None:
+                es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                es0.record()
+            nat.check(L.dgx_knn_spatial_seed_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k, nat.i32(perm),
+                                                 nat.f32(T), stream), "knn spatial seed")
+            if timing is not None:
+                es1.record()
+                seed_log = getattr(_tls, "seed_timing", None)
+                if seed_log is not None:
+                    seed_log.append((es0, es1))
         if seeds is not None:
             if seeds.dtype != torch.int32 or not seeds.is_contiguous() or seeds.shape[:2] != (B, N) \
                     or not k <= seeds.shape[2] <= 64:
@@ -86,7 +116,28 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
             ev1.record()
             timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
     nat.check(rc, "knn")
+    if key is not None:
+        cache[key] = idx
     return (idx, vals) if return_values else idx
+
+
+@contextlib.contextmanager
+def knn_cache():
+    """Scope in which kNN calls on the same view of the same storage (pointer,
+    shape, strides, version counter) with the same k and rounding order share
+    one computation. ``Net.forward`` reaches the kNN of its input cloud three
+    times (reference model_partseg.py:177 -> dgcnn.py:84, :179 -> :26 and
+    :183 -> layers.py:45); the result is a deterministic function
+    of those keys, so the shared result is the one each call would compute.
+    The caller's references keep the input alive for the whole scope, so a
+    storage pointer cannot be reused inside it. Thread-local (DataParallel
+    replicas run in threads)."""
+    prev = getattr(_tls, "cache", None)
+    _tls.cache = {} if prev is None else prev
+    try:
+        yield
+    finally:
+        _tls.cache = prev
 
 
 def set_knn_timing(lst, seed_lst=None):

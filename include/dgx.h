@@ -94,6 +94,15 @@ int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN
  * dgx_knn_prepare_f32). ks >= k makes T a lower bound of the k-th value. */
 int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                      const int32_t* seeds, int ks, float* T, void* stream);
+/* Spatial admission seeds for coordinate clouds (C <= 4, 256 <= N <= 4096,
+ * k <= 64; reference dgcnn.py:6-12 on the xyz input of DGCNN block 1,
+ * layers.py:45 and model_partseg.py:26): the cloud is ordered along a Morton
+ * curve of an 8^3 cell grid (perm: B*N int32 scratch) and T[b*N+q] = the k-th
+ * best value among the 64 points around q in that order, in the selection's
+ * exact arithmetic (a lower bound of q's k-th value). DGX_EUNSUPPORTED
+ * outside that range (select unseeded then). */
+int dgx_knn_spatial_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
+                             int N, int k, int32_t* perm, float* T, void* stream);
 
 /* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
  * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in
@@ -138,7 +147,8 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         int64_t* num_batches_tracked, void* stream);
 /* The same finalize from fp64 column sums (nrows x 2 x Co doubles): the global
  * sums of a SyncBatchNorm all-reduce (main_partseg_dist.py:189), kept in fp64
- * into var = E[y^2] - E[y]^2. */
+ * into var = E[y^2] - E[y]^2. count < 0: the element count is the double that
+ * follows the sums on the device (all-reduced with them; no host read). */
 int dgx_bn_finalize_f64(const double* sums, int nrows, int Co, double count,
                         const float* gamma, const float* beta,
                         float* running_mean, float* running_var,

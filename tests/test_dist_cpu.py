@@ -21,8 +21,10 @@ def _worker(rank, world, port, q):
         import bench
         # per-block partials (rows, 2, C): summed in fp64 locally, then across ranks
         part = torch.arange(12, dtype=torch.float32).view(2, 2, 3) * (rank + 1)
-        tot, cnt = D.allreduce_sums(part, 10 + rank, dist.group.WORLD)
-        assert tot.dtype == torch.float64 and tot.is_contiguous()
+        buf = D.allreduce_sums(part, 10 + rank, dist.group.WORLD)
+        # one fp64 buffer [sums (2, C) | count]: the count stays with the sums (read on the device)
+        assert buf.dtype == torch.float64 and buf.is_contiguous() and buf.shape == (7,)
+        tot, cnt = buf[:6].view(2, 3), float(buf[6])
         bn = torch.nn.SyncBatchNorm(3)
         on, grp = D.sync_group(bn.train())
         off, _ = D.sync_group(bn.eval())

@@ -195,3 +195,32 @@ def test_knn_seeded_equals_unseeded(cuda, C, N, k, layout):
     for name, seeds in (("exact", base), ("random", rnd), ("other graph", other), ("invalid", selfs)):
         got = knn_raw(x, k, out_dtype=torch.int32, seeds=seeds.to(cuda).contiguous())
         assert torch.equal(got, base), name
+
+
+@pytest.mark.parametrize("B,N,k,layout", [(3, 1024, 20, "perm"), (2, 2048, 40, "bcn"), (1, 4096, 64, "perm"),
+                                          (2, 256, 16, "bcn"), (2, 777, 33, "perm")])
+def test_knn_spatial_seeds_change_nothing(cuda, monkeypatch, B, N, k, layout):
+    """Coordinate clouds take spatial admission seeds (dgx_knn_spatial_seed_f32):
+    the result is bit-identical to the unseeded selection and to the oracle,
+    including clouds of duplicated points (exact ties at the seed) and a
+    degenerate flat cloud."""
+    import oracle
+    from dgx import ops, synth
+    from dgx.ops import knn_raw
+    pts = synth.cube_clouds(B, N, N + k)
+    pts[:, N // 2:N // 2 + N // 8] = pts[:, :N // 8]            # duplicated points: ties
+    if B > 1:
+        pts[1, :, 2] = 0.0                                      # a flat cloud (one empty grid axis)
+    f = torch.from_numpy(pts).permute(0, 2, 1)
+    if layout == "bcn":
+        f = f.contiguous()
+    x = f.to(cuda)
+    monkeypatch.setattr(ops, "SPATIAL_SEEDS", True)
+    seeded = knn_raw(x, k)
+    monkeypatch.setattr(ops, "SPATIAL_SEEDS", False)
+    plain = knn_raw(x, k)
+    assert torch.equal(seeded, plain)
+    idx, vals = oracle.knn(f, k, return_values=True)
+    got_idx, got_vals = knn_raw(x, k, return_values=True)
+    from conftest import assert_knn_equivalent
+    assert_knn_equivalent(seeded.cpu().numpy(), got_vals.cpu().numpy(), idx, vals)

@@ -297,3 +297,39 @@ def test_net_cfg4_routed(cuda, amp):
           "worst (engine, stock):", [(n, f"{e:.1e}", f"{e2:.1e}") for n, e, e2 in rows[:6]])
     for n, e, e2 in rows:
         assert e <= max(floor, RATIO * e2), (n, e, e2)
+
+
+@pytest.mark.gpu
+def test_net_knn_computed_once(cuda, monkeypatch):
+    """Net.forward's three kNN of the input cloud (model_partseg.py:177, 179,
+    183) run as ONE selection launch (dgx.ops.knn_cache), and the step is
+    bit-identical to the one that computes them three times."""
+    import contextlib
+    import models.model_partseg as MP
+    from dgx import ops, synth
+    args = types.SimpleNamespace(k=20, emb_dim=64, n_heads=4, n_blocks=1, ff_dims=128, dropout=0.0, nclasses=50)
+    torch.manual_seed(3)
+    net = MP.Net(args).to(cuda).train()
+    init = {n: t.clone() for n, t in net.state_dict().items()}
+    src = torch.from_numpy(synth.cube_clouds(2, 512, 12)).to(cuda).permute(0, 2, 1).contiguous()
+    lbl = torch.nn.functional.one_hot(torch.tensor([3, 7]), 16).float().to(cuda)
+
+    def step():
+        net.load_state_dict(init)
+        net.zero_grad(set_to_none=True)
+        timing = []
+        ops.set_knn_timing(timing)
+        try:
+            out = net(src, lbl)
+        finally:
+            ops.set_knn_timing(None)
+        out.square().mean().backward()
+        return out.detach(), {n: p.grad.clone() for n, p in net.named_parameters()}, \
+            sum(1 for t in timing if t[3][1] == 3)
+    out1, g1, n1 = step()
+    monkeypatch.setattr(MP, "knn_cache", contextlib.nullcontext)
+    out3, g3, n3 = step()
+    assert (n1, n3) == (1, 3)
+    assert torch.equal(out1, out3)
+    for n in g1:
+        assert torch.equal(g1[n], g3[n]), n

@@ -17,14 +17,16 @@ f128 = torch.from_numpy(synth.relu_normal(4, (32, 128, 1024))).to(dev)
 # point-major (B,N,C) memory, as the engine's concat buffer feeds layers 2-4
 p64 = f64.permute(0, 2, 1).contiguous().permute(0, 2, 1)
 p128 = f128.permute(0, 2, 1).contiguous().permute(0, 2, 1)
-for name, x in (("C3", x3), ("C64", f64), ("C128", f128), ("C64pm", p64), ("C128pm", p128)):
+x3b = torch.from_numpy(synth.cube_clouds(32, 2048, 1)).to(dev).permute(0, 2, 1)
+for name, x, k in (("C3", x3, 20), ("C3 N2048 k40", x3b, 40), ("C64", f64, 20), ("C128", f128, 20),
+                   ("C64pm", p64, 20), ("C128pm", p128, 20)):
     for _ in range(3):
-        knn_raw(x, 20, out_dtype=torch.int32)
+        knn_raw(x, k, out_dtype=torch.int32)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(reps):
-        knn_raw(x, 20, out_dtype=torch.int32)
+        knn_raw(x, k, out_dtype=torch.int32)
     ev1.record()
     torch.cuda.synchronize()
     print(name, "%.1f us/call (incl. sqnorm)" % (ev0.elapsed_time(ev1) / reps * 1e3))

@@ -1,0 +1,21 @@
+"""One kNN call per shape (for PMC passes): python tools/knn_once.py [C3|C3k40|...]"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "dgcnn.pytorch_amd")]
+from dgx import synth  # noqa: E402
+from dgx.ops import knn_raw  # noqa: E402
+
+dev = torch.device("cuda:0")
+if "DGX_SPATIAL_SEEDS" in os.environ:
+    from dgx import ops
+    ops.SPATIAL_SEEDS = os.environ["DGX_SPATIAL_SEEDS"] == "1"
+which = sys.argv[1] if len(sys.argv) > 1 else "C3"
+B, N, k = (32, 2048, 40) if which == "C3k40" else (32, 1024, 20)
+x = torch.from_numpy(synth.cube_clouds(B, N, 0)).to(dev).permute(0, 2, 1)
+for _ in range(3):
+    knn_raw(x, k, out_dtype=torch.int32)
+torch.cuda.synchronize()
