@@ -99,6 +99,59 @@ def mm_xwt(x, w, out=None, stats=False):
     return (out, part) if stats else out
 
 
+def _op32(t, contiguous_dim):
+    """(tensor, ic, ld) reading a 2-D fp32 view in place: ``contiguous_dim`` 1
+    means "k" is dim 1 (opA(i,k) = t[i,k]), 0 means "k" is dim 0 (opB(j,k) =
+    t[k,j]); falls back to a contiguous copy for a view with no unit stride."""
+    if t.dtype != torch.float32:
+        t = t.float()
+    kd, od = contiguous_dim, 1 - contiguous_dim
+    if t.stride(kd) == 1 or t.shape[kd] == 1:            # k contiguous: KC, ld = stride of the other dim
+        return t, 0, max(t.stride(od), t.shape[kd], 1) if t.shape[od] > 1 else max(t.shape[kd], 1)
+    if t.stride(od) == 1 or t.shape[od] == 1:            # rows contiguous: IC, ld = stride along k
+        return t, 1, max(t.stride(kd), t.shape[od], 1) if t.shape[kd] > 1 else max(t.shape[od], 1)
+    t = t.contiguous() if kd == 1 else t.t().contiguous().t()
+    return _op32(t, contiguous_dim)
+
+
+def mm32(a, b, out=None, accumulate=False, addend=None):
+    """out (M,N) = a (M,K) @ b (K,N) on the engine's fp32 MFMA GEMM
+    (dgx_gemm_f32, exact fp32 products): the parity mode's GEMMs. Transposed
+    views are read in place; a long reduction (K >= 2048 over few outputs,
+    the weight gradients over B*N rows) is split over workgroups into slabs
+    summed in a fixed order (deterministic). ``accumulate``: out += a @ b;
+    ``addend``: out = addend + a @ b."""
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K:
+        raise RuntimeError(f"dgx mm32: inner dims {K} and {b.shape[0]} differ")
+    ta, aic, lda = _op32(a, 1)
+    tb, bic, ldb = _op32(b, 0)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if out.dtype != torch.float32 or out.dim() != 2 or (out.stride(1) != 1 and N > 1):
+        raise RuntimeError("dgx mm32: output must be a row-major fp32 2-D view")
+    L = nat.lib()
+    S = L.dgx_gemm_f32_splits(M, N, K) if (K >= 2048 and not accumulate and addend is None) else 1
+    st = nat.stream_of(out)
+    with torch.cuda.device(out.device), _Timed(2.0 * M * N * K):
+        if S > 1:
+            kchunk = -(-K // S)
+            kchunk = -(-kchunk // 16) * 16
+            used = -(-K // kchunk)
+            slab = torch.empty((used, M, N), dtype=torch.float32, device=out.device)
+            nat.check(L.dgx_gemm_f32(nat.ptr(ta), aic, lda, nat.ptr(tb), bic, ldb, M, N, K, EPI_SLAB, S,
+                                     nat.ptr(slab), N, None, 0, st), "gemm f32 (split-K)")
+            nat.check(L.dgx_slab_reduce_f32(nat.ptr(slab), used, M, N, M, nat.ptr(out), out.stride(0), st),
+                      "slab reduce")
+        else:
+            epi = EPI_ACCUM if (accumulate or addend is not None) else EPI_STORE
+            nat.check(L.dgx_gemm_f32(nat.ptr(ta), aic, lda, nat.ptr(tb), bic, ldb, M, N, K, epi, 1, nat.ptr(out),
+                                     out.stride(0) if M > 1 else max(N, 1), nat.ptr(addend),
+                                     addend.stride(0) if addend is not None else 0, st), "gemm f32")
+    return out
+
+
 SMALLK_MAX = 16
 
 
@@ -227,26 +280,44 @@ def prep_weight(w, rows, cols, stacked):
     return nt, tn
 
 
-def prep_weights(jobs):
+def prep_layout(shapes):
+    """Layout of prep_weights' shared bf16 buffer for (rows, cols, stacked,
+    split) jobs: (total elements, [(nt offset, nt shape, tn offset, tn shape)])
+    with every view 16-byte aligned."""
+    total, out = 0, []
+    for (r, c, st, sp) in shapes:
+        R = 2 * r if st else r
+        n_tn, n_nt = R * c, (2 if sp else 1) * R * c
+        p_tn, p_nt = -(-n_tn // 8) * 8, -(-n_nt // 8) * 8
+        out.append((total, (R, 2 * c if sp else c), total + p_nt, (c, R)))
+        total += p_nt + p_tn
+    return total, out
+
+
+def prep_views(buf, shapes):
+    """[(nt, tn)] views of a prep_weights buffer (prep_layout's layout)."""
+    _, lay = prep_layout(shapes)
+    return [(buf[o1:o1 + s1[0] * s1[1]].view(s1), buf[o2:o2 + s2[0] * s2[1]].view(s2)) for (o1, s1, o2, s2) in lay]
+
+
+def prep_weights(jobs, buf=None):
     """prep_weight for several (w, rows, cols, stacked[, split]) jobs in one
-    launch; the bf16 copies share one allocation. Returns [(nt, tn), ...].
-    ``split``: nt is (R, 2*cols) = [W_hi | W_lo] for lds_xwt's split-weight
-    form; tn (the backward's operand) is W_hi^T either way."""
+    launch; the bf16 copies share one allocation (``buf``, prep_layout's size,
+    or a fresh one). Returns [(nt, tn), ...]. ``split``: nt is (R, 2*cols) =
+    [W_hi | W_lo] for lds_xwt's split-weight form; tn (the backward's operand)
+    is W_hi^T either way."""
     import ctypes
     if not jobs:
         return []
     jobs = [tuple(j) + (False,) * (5 - len(j)) for j in jobs]
     dev = jobs[0][0].device
-    sizes = [((2 * r if st else r) * c, (2 if sp else 1) * (2 * r if st else r) * c) for (_, r, c, st, sp) in jobs]
-    pads = [(-(-a // 8) * 8, -(-b // 8) * 8) for (a, b) in sizes]  # 16-byte aligned views
-    buf = torch.empty(sum(a + b for a, b in pads), dtype=torch.bfloat16, device=dev)
-    out, off = [], 0
-    for (w, r, c, st, sp), (n_tn, n_nt), (p_tn, p_nt) in zip(jobs, sizes, pads):
-        R = 2 * r if st else r
-        nt = buf[off:off + n_nt].view(R, 2 * c if sp else c)
-        tn = buf[off + p_nt:off + p_nt + n_tn].view(c, R)
-        off += p_nt + p_tn
-        out.append((nt, tn))
+    shapes = [(r, c, st, sp) for (_, r, c, st, sp) in jobs]
+    total, _ = prep_layout(shapes)
+    if buf is None:
+        buf = torch.empty(total, dtype=torch.bfloat16, device=dev)
+    elif buf.numel() != total or buf.dtype != torch.bfloat16:
+        raise RuntimeError("dgx weight prep: buffer does not match the jobs' layout")
+    out = prep_views(buf, shapes)
     n = len(jobs)
     P = ctypes.c_void_p * n
     I = ctypes.c_int * n

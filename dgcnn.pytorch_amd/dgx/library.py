@@ -1,0 +1,490 @@
+"""torch.library op layer of the engine (SURVEY §8(b) "Torch op layer").
+
+The reference's hot path is plain Python over ATen ops (models/dgcnn.py:6,
+15, 47-103). The engine's HIP work is exposed here as ``torch.ops.dgx.*``
+custom ops with device ("cuda" = ROCm) kernels, fake (meta) kernels for
+tracing, autocast rules and autograd formulas, so ``torch.compile`` /
+``torch.export`` / FX see each op as one node instead of an opaque ctypes call
+(the compiled graph has no break at the engine):
+
+  dgx::knn(x, k) -> int64 (B, N, k)                     dgcnn.py:6-12
+  dgx::graph_feature(x, k, mode) -> (edge tensor, idx)  dgcnn.py:15-44
+      (+ dgx::graph_feature_backward)
+  dgx::weight_prep(weights, ...) -> bf16 operand buffer  (bf16 mode)
+  dgx::edgeconv_chain(x, k, conv/BN tensors, ...) -> (concat buffer, its
+      bf16 twin, updated running statistics, saved state)  dgcnn.py:84-100
+      (+ dgx::edgeconv_chain_backward)
+  dgx::pointconv(X, X16, B, N, conv/BN tensors, ...) -> (out, updated
+      running statistics, saved state)                   dgcnn.py:100-102
+      (+ dgx::pointconv_backward)
+
+The ops are functional: BatchNorm running statistics come back as outputs and
+the caller copies them into the module buffers (what a compiled graph does with
+a buffer mutation anyway). Each op's device kernel runs the same code as the
+engine's autograd Functions (dgx.edgeconv, dgx.pointconv), so eager results
+are identical either way; ``models.dgcnn.DGCNN`` takes this path unless a
+BatchNorm is a SyncBatchNorm (process groups cannot cross the op boundary) —
+then the Function path runs, with its collectives.
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from . import bn as bn_
+from . import edgeconv as E
+from . import gemm as G
+from . import ops
+from . import pointconv as PC
+from . import precision as prec
+
+ENABLED = True
+_F32, _BF16, _I32 = torch.float32, torch.bfloat16, torch.int32
+
+
+def _empty(dev, dtype=_F32):
+    return torch.empty(0, dtype=dtype, device=dev)
+
+
+class _Rec:
+    """The autograd-context surface the engine's Functions use, recorded so a
+    custom op can run a Function's forward / backward body."""
+
+    def __init__(self):
+        self.saved_tensors = ()
+        self.needs_input_grad = (True,) * 64
+
+    def save_for_backward(self, *t):
+        self.saved_tensors = t
+
+    def mark_non_differentiable(self, *_):
+        pass
+
+    def set_materialize_grads(self, _):
+        pass
+
+
+class _BNSpec:
+    """The nn.BatchNorm fields dgx.bn reads, rebuilt from tensors that crossed
+    the op boundary (running statistics are the op's private copies)."""
+
+    def __init__(self, training, track, rm, rv, nbt, momentum, eps):
+        self.training = bool(training)
+        self.track_running_stats = bool(track)
+        self.running_mean = rm if rm.numel() else None
+        self.running_var = rv if rv.numel() else None
+        self.num_batches_tracked = nbt if nbt.numel() else None
+        self.momentum = None if momentum < 0 else float(momentum)
+        self.eps = float(eps)
+
+
+def _use_batch(training, rm):
+    return bool(training) or rm.numel() == 0
+
+
+# ------------------------------------------------------------------- knn ----
+@torch.library.custom_op("dgx::knn", mutates_args=(), device_types="cuda")
+def knn(x: Tensor, k: int) -> Tensor:
+    """int64 (B, N, k) local ids of the k nearest points (reference dgcnn.py:6-12)."""
+    return ops.knn(x, k).clone() if getattr(ops._tls, "cache", None) is not None else ops.knn(x, k)
+
+
+@knn.register_fake
+def _(x, k):
+    B, _, N = x.shape
+    return x.new_empty((B, N, k), dtype=torch.int64)
+
+
+# distances are computed in fp32 whatever autocast says
+torch.library.register_autocast("dgx::knn", "cuda", torch.float32)
+
+
+# --------------------------------------------------------- graph feature ----
+def _gf_shape(x, k, mode):
+    B, C, N = x.shape
+    if mode == ops.nat.GF_CAT:
+        return (B, 2 * C, N, k)
+    if mode == ops.nat.GF_DISP:
+        return (B, C, N, k)
+    return (B, N, k, C)
+
+
+@torch.library.custom_op("dgx::graph_feature", mutates_args=(), device_types="cuda")
+def graph_feature(x: Tensor, k: int, mode: int) -> tuple[Tensor, Tensor]:
+    """(edge tensor, int32 kNN ids) of reference dgcnn.py:15-44; mode 0 =
+    cat(x_j, x_i) (B,2C,N,k), 1 = x_j - x_i (B,C,N,k), 2 = x_j (B,N,k,C)."""
+    xf = x.float()
+    idx = ops.knn_raw(xf.detach(), k, out_dtype=_I32)
+    return ops._GraphFeature.forward(_Rec(), xf, idx, mode), idx.clone() if idx._base is not None else idx
+
+
+@graph_feature.register_fake
+def _(x, k, mode):
+    B, _, N = x.shape
+    return x.new_empty(_gf_shape(x, k, mode), dtype=_F32), x.new_empty((B, N, k), dtype=_I32)
+
+
+@torch.library.custom_op("dgx::graph_feature_backward", mutates_args=(), device_types="cuda")
+def graph_feature_backward(grad: Tensor, idx: Tensor, C: int, mode: int) -> Tensor:
+    rec = _Rec()
+    rec.saved_tensors = (idx,)
+    rec.mode = mode
+    B, N, _ = idx.shape
+    rec.shape = (B, C, N)
+    return ops._GraphFeature.backward(rec, grad)[0]
+
+
+@graph_feature_backward.register_fake
+def _(grad, idx, C, mode):
+    B, N, _ = idx.shape
+    return grad.new_empty((B, C, N), dtype=_F32)
+
+
+def _gf_setup(ctx, inputs, output):
+    ctx.save_for_backward(output[1])
+    ctx.C, ctx.mode = inputs[0].shape[1], inputs[2]
+
+
+def _gf_bwd(ctx, gout, _gidx):
+    (idx,) = ctx.saved_tensors
+    return torch.ops.dgx.graph_feature_backward(gout.contiguous(), idx, ctx.C, ctx.mode), None, None
+
+
+torch.library.register_autograd("dgx::graph_feature", _gf_bwd, setup_context=_gf_setup)
+torch.library.register_autocast("dgx::graph_feature", "cuda", torch.float32)
+
+
+# ------------------------------------------------------------ weight prep ----
+@torch.library.custom_op("dgx::weight_prep", mutates_args=(), device_types="cuda")
+def weight_prep(weights: list[Tensor], rows: list[int], cols: list[int], stacked: list[bool],
+                split: list[bool]) -> Tensor:
+    """One bf16 buffer holding every weight's GEMM operand copies
+    (gemm.prep_layout: [W | W_hi W_lo] and W^T per weight), one launch."""
+    shapes = list(zip(rows, cols, stacked, split))
+    total, _ = G.prep_layout(shapes)
+    buf = torch.empty(total, dtype=_BF16, device=weights[0].device)
+    G.prep_weights([(w.detach(), r, c, st, sp) for w, (r, c, st, sp) in zip(weights, shapes)], buf=buf)
+    return buf
+
+
+@weight_prep.register_fake
+def _(weights, rows, cols, stacked, split):
+    total, _ = G.prep_layout(list(zip(rows, cols, stacked, split)))
+    return weights[0].new_empty((total,), dtype=_BF16)
+
+
+def _dgcnn_prep_shapes(weights5):
+    """(rows, cols, stacked, split) of DGCNN's bf16 copies: conv2-4 stacked and
+    split (edgeconv), conv5 plain (models.dgcnn._bf16_weight_copies)."""
+    shapes = [(w.shape[0], w.shape[1] // 2, True, True) for w in weights5[:3]]
+    shapes.append((weights5[3].shape[0], weights5[3].shape[1], False, False))
+    return shapes
+
+
+# --------------------------------------------------------- edgeconv chain ----
+_PER_LAYER = 9   # idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd
+
+
+def _chain_prep_shapes(weights):
+    """(rows, cols, stacked, split) of blocks 2..n's bf16 copies (split, stacked)."""
+    return [(w.shape[0], w.shape[1] // 2, True, True) for w in weights[1:]]
+
+
+def _chain_layers(weights, specs, slopes):
+    return [E._Layer(w.shape[1] // 2, w.shape[0], s, sl) for w, s, sl in zip(weights, specs, slopes)]
+
+
+def _chain_prep_used(li, bf16, selecting, cin):
+    """Whether block li's GEMMs take the bf16 weight copies (dgx.edgeconv:
+    its input is the bf16 twin written by a selecting block and the operand
+    qualifies for the LDS-DMA path)."""
+    return bf16 and li > 0 and selecting[li - 1] and cin % 64 == 0
+
+
+@torch.library.custom_op("dgx::edgeconv_chain", mutates_args=(), device_types="cuda")
+def edgeconv_chain(x: Tensor, k: int, weights: list[Tensor], gammas: list[Tensor], betas: list[Tensor],
+                   running_means: list[Tensor], running_vars: list[Tensor], nbts: list[Tensor], training: list[bool],
+                   track: list[bool], momentum: list[float], eps: list[float], slopes: list[float], bf16: bool,
+                   need_grad: bool, prep: Optional[Tensor]) -> tuple[Tensor, Tensor, list[Tensor], list[Tensor],
+                                                                     list[Tensor], list[Tensor]]:
+    """DGCNN's EdgeConv blocks (dgcnn.py:84-100) as dgx.edgeconv runs them:
+    returns (concat buffer (B*N, sum Co), its bf16 twin or empty, updated
+    running means / vars / batch counters, the state the backward reads)."""
+    rms = [t.clone() for t in running_means]
+    rvs = [t.clone() for t in running_vars]
+    nbs = [t.clone() for t in nbts]
+    specs = [_BNSpec(*a) for a in zip(training, track, rms, rvs, nbs, momentum, eps)]
+    layers = _chain_layers(weights, specs, slopes)
+    params = [t for trip in zip(weights, gammas, betas) for t in trip]
+    preps = None
+    if prep is not None:   # blocks 2.. : the first entries of the shared bf16 buffer (dgcnn_forward)
+        preps = [None] + G.prep_views(prep, _chain_prep_shapes(weights))
+    rec = _Rec()
+    with prec.mode("bf16" if bf16 else "fp32"):
+        xcat, xcat16 = E._EdgeConvStack.forward(rec, x, k, layers, preps, need_grad, *params)
+    x_pm = rec.saved_tensors[0]
+    if x_pm.untyped_storage().data_ptr() == x.untyped_storage().data_ptr():
+        x_pm = x_pm.clone()
+    saved = [x_pm]
+    selecting = [s is not None for s in rec.layer_state]
+    for li, st in enumerate(rec.layer_state):
+        if st is None:   # distinct placeholders: op outputs may not alias each other
+            saved += [_empty(x.device) for _ in range(_PER_LAYER)]
+            continue
+        idx, PQ, ysel, arg, sumP, stats, wprep = st
+        if (wprep is not None) != _chain_prep_used(li, bf16, selecting, layers[li].cin):
+            raise RuntimeError("dgx::edgeconv_chain: bf16 operand-copy use differs from its static rule")
+        saved += [idx, PQ, ysel, arg, sumP, stats.scale, stats.shift, stats.mean, stats.invstd]
+    return xcat, xcat16, rms, rvs, nbs, saved
+
+
+@edgeconv_chain.register_fake
+def _(x, k, weights, gammas, betas, running_means, running_vars, nbts, training, track, momentum, eps, slopes,
+      bf16, need_grad, prep):
+    B, C0, N = x.shape
+    M = B * N
+    widths = [w.shape[0] for w in weights]
+    total = sum(widths)
+    selecting = [_use_batch(t, rm) or need_grad for t, rm in zip(training, running_means)]
+    xcat = x.new_empty((M, total), dtype=_F32)
+    xcat16 = x.new_empty((M, total), dtype=_BF16) if (bf16 and selecting[-1]) else x.new_empty((0,), dtype=_BF16)
+    saved = [x.new_empty((M, C0), dtype=_F32)]
+    for li, co in enumerate(widths):
+        if not selecting[li]:
+            saved += [x.new_empty((0,), dtype=_F32) for _ in range(_PER_LAYER)]
+            continue
+        saved += [x.new_empty((B, N, k), dtype=_I32), x.new_empty((M, 2 * co), dtype=_F32),
+                  x.new_empty((M, co), dtype=_F32), x.new_empty((M, co), dtype=torch.uint8),
+                  x.new_empty((M, co), dtype=_F32)] + [x.new_empty((co,), dtype=_F32) for _ in range(4)]
+    return (xcat, xcat16, [torch.empty_like(t) for t in running_means], [torch.empty_like(t) for t in running_vars],
+            [torch.empty_like(t) for t in nbts], saved)
+
+
+@torch.library.custom_op("dgx::edgeconv_chain_backward", mutates_args=(), device_types="cuda")
+def edgeconv_chain_backward(dxcat: Tensor, x: Tensor, xcat: Tensor, xcat16: Tensor, saved: list[Tensor],
+                            weights: list[Tensor], gammas: list[Tensor], betas: list[Tensor], prep: Optional[Tensor],
+                            k: int, use_batch: list[bool], slopes: list[float], bf16: bool,
+                            x_needs_grad: bool) -> tuple[Tensor, list[Tensor], list[Tensor], list[Tensor]]:
+    B, C0, N = x.shape
+    rec = _Rec()
+    params = [t for trip in zip(weights, gammas, betas) for t in trip]
+    rec.saved_tensors = (saved[0], xcat, xcat16 if xcat16.numel() else None, *params)
+    rec.k, rec.shape, rec.bf16, rec.x_needs_grad = k, (B, C0, N), bf16, x_needs_grad
+    rec.layers = _chain_layers(weights, [None] * len(weights), slopes)
+    preps = [None] * len(weights)
+    if prep is not None:
+        preps = [None] + G.prep_views(prep, _chain_prep_shapes(weights))
+    state, selecting = [], []
+    for li in range(len(weights)):
+        t = saved[1 + _PER_LAYER * li: 1 + _PER_LAYER * (li + 1)]
+        sel = t[0].numel() > 0
+        selecting.append(sel)
+        if not sel:
+            raise RuntimeError("dgx::edgeconv_chain_backward: a block ran without its backward state")
+        stats = bn_.Stats(t[5], t[6], t[7], t[8], None, not use_batch[li])
+        wprep = preps[li] if _chain_prep_used(li, bf16, selecting, rec.layers[li].cin) else None
+        state.append((t[0], t[1], t[2], t[3], t[4], stats, wprep))
+    rec.layer_state = state
+    with prec.mode("bf16" if bf16 else "fp32"):
+        res = E._EdgeConvStack.backward(rec, dxcat, None)
+    dx = res[0].contiguous() if res[0] is not None else _empty(x.device)
+    grads = res[5:]
+    return dx, [g.contiguous() for g in grads[0::3]], list(grads[1::3]), list(grads[2::3])
+
+
+@edgeconv_chain_backward.register_fake
+def _(dxcat, x, xcat, xcat16, saved, weights, gammas, betas, prep, k, use_batch, slopes, bf16, x_needs_grad):
+    dx = x.new_empty(x.shape, dtype=_F32) if x_needs_grad else x.new_empty((0,), dtype=_F32)
+    return (dx, [torch.empty_like(w, dtype=_F32) for w in weights], [torch.empty_like(g, dtype=_F32) for g in gammas],
+            [torch.empty_like(b, dtype=_F32) for b in betas])
+
+
+def _chain_setup(ctx, inputs, output):
+    (x, k, weights, gammas, betas, rms, rvs, nbts, training, track, momentum, eps, slopes, bf16, need_grad,
+     prep) = inputs
+    xcat, xcat16, _, _, _, saved = output
+    ctx.n, ctx.nsaved, ctx.has_prep = len(weights), len(saved), prep is not None
+    ctx.k, ctx.slopes, ctx.bf16 = k, list(slopes), bf16
+    ctx.use_batch = [_use_batch(t, rm) for t, rm in zip(training, rms)]
+    ctx.save_for_backward(x, xcat, xcat16, *saved, *weights, *gammas, *betas, *([prep] if prep is not None else []))
+
+
+def _chain_bwd(ctx, g_xcat, _g16, _grm, _grv, _gnbt, _gsaved):
+    t = ctx.saved_tensors
+    n, ns = ctx.n, ctx.nsaved
+    x, xcat, xcat16 = t[0], t[1], t[2]
+    saved = list(t[3:3 + ns])
+    ws, gs, bs = list(t[3 + ns:3 + ns + n]), list(t[3 + ns + n:3 + ns + 2 * n]), list(t[3 + ns + 2 * n:3 + ns + 3 * n])
+    prep = t[3 + ns + 3 * n] if ctx.has_prep else None
+    if g_xcat is None:
+        g_xcat = torch.zeros_like(xcat)
+    dx, dws, dgs, dbs = torch.ops.dgx.edgeconv_chain_backward(
+        g_xcat.contiguous(), x, xcat, xcat16, saved, ws, gs, bs, prep, ctx.k, ctx.use_batch, ctx.slopes, ctx.bf16,
+        ctx.needs_input_grad[0])
+    nl = [None] * n   # list-of-tensor inputs take a list of gradients (none for the BN buffers)
+    return ((dx if ctx.needs_input_grad[0] else None), None, dws, dgs, dbs, nl, list(nl), list(nl), None, None, None,
+            None, None, None, None, None)
+
+
+torch.library.register_autograd("dgx::edgeconv_chain", _chain_bwd, setup_context=_chain_setup)
+
+
+# -------------------------------------------------------------- pointconv ----
+def _pc_lds(bf16, X16, K):
+    return bf16 and X16.numel() > 0 and K % 64 == 0
+
+
+@torch.library.custom_op("dgx::pointconv", mutates_args=(), device_types="cuda")
+def pointconv(X: Tensor, X16: Tensor, B: int, N: int, weight: Tensor, gamma: Tensor, beta: Tensor,
+              running_mean: Tensor, running_var: Tensor, nbt: Tensor, training: bool, track: bool, momentum: float,
+              eps: float, slope: float, bf16: bool, prep: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor, Tensor,
+                                                                                    list[Tensor]]:
+    """conv5 -> BN -> LeakyReLU on the concat buffer (dgcnn.py:100-102) as
+    dgx.pointconv runs it: (out (B, Co, N), updated running mean / var /
+    batch counter, saved state [Z, scale, shift, mean, invstd])."""
+    rm, rv, nb = running_mean.clone(), running_var.clone(), nbt.clone()
+    spec = _BNSpec(training, track, rm, rv, nb, momentum, eps)
+    wprep = None
+    if prep is not None:
+        Co, K = weight.shape[0], weight.shape[1]
+        wprep = G.prep_views(prep, [(Co, K, False, False)])[0] if prep.numel() == 2 * Co * K else None
+    rec = _Rec()
+    with prec.mode("bf16" if bf16 else "fp32"):
+        out = PC._PointConvBNLReLU.forward(rec, X, X16 if X16.numel() else None, B, N, spec, slope, wprep, weight,
+                                           gamma, beta)
+    Z = rec.saved_tensors[2]
+    st = rec.st
+    return out, rm, rv, nb, [Z, st.scale, st.shift, st.mean, st.invstd]
+
+
+@pointconv.register_fake
+def _(X, X16, B, N, weight, gamma, beta, running_mean, running_var, nbt, training, track, momentum, eps, slope,
+      bf16, prep):
+    M, K = X.shape
+    Co = weight.shape[0]
+    z16 = _pc_lds(bf16, X16, K) and _use_batch(training, running_mean)
+    Z = X.new_empty((M, Co), dtype=_BF16 if z16 else _F32)
+    return (X.new_empty((B, Co, N), dtype=_F32), torch.empty_like(running_mean), torch.empty_like(running_var),
+            torch.empty_like(nbt), [Z] + [X.new_empty((Co,), dtype=_F32) for _ in range(4)])
+
+
+@torch.library.custom_op("dgx::pointconv_backward", mutates_args=(), device_types="cuda")
+def pointconv_backward(dout: Tensor, X: Tensor, X16: Tensor, weight: Tensor, saved: list[Tensor],
+                       prep: Optional[Tensor], B: int, N: int, slope: float, bf16: bool,
+                       use_batch: bool) -> tuple[Tensor, Tensor, Tensor, Tensor]:
+    Z, scale, shift, mean, invstd = saved
+    M, K = X.shape
+    Co = weight.shape[0]
+    lds = _pc_lds(bf16, X16, K)
+    rec = _Rec()
+    rec.saved_tensors = (X16 if lds else X, weight.reshape(Co, K), Z)
+    rec.st = bn_.Stats(scale, shift, mean, invstd, None, not use_batch)
+    rec.meta = (B, N, float(slope), bf16)
+    rec.wprep = None
+    if lds:
+        rec.wprep = (G.prep_views(prep, [(Co, K, False, False)])[0] if prep is not None and prep.numel() == 2 * Co * K
+                     else G.prep_weight(weight, Co, K, False))
+    rec.wshape = weight.shape
+    with prec.mode("bf16" if bf16 else "fp32"):
+        res = PC._PointConvBNLReLU.backward(rec, dout)
+    return res[0].contiguous(), res[7].contiguous(), res[8], res[9]
+
+
+@pointconv_backward.register_fake
+def _(dout, X, X16, weight, saved, prep, B, N, slope, bf16, use_batch):
+    Co = weight.shape[0]
+    return (X.new_empty(X.shape, dtype=_F32), torch.empty_like(weight, dtype=_F32), X.new_empty((Co,), dtype=_F32),
+            X.new_empty((Co,), dtype=_F32))
+
+
+def _pc_setup(ctx, inputs, output):
+    (X, X16, B, N, weight, gamma, beta, rm, rv, nbt, training, track, momentum, eps, slope, bf16, prep) = inputs
+    ctx.meta = (B, N, slope, bf16, _use_batch(training, rm), prep is not None)
+    ctx.save_for_backward(X, X16, weight, *output[4], *([prep] if prep is not None else []))
+
+
+def _pc_bwd(ctx, g_out, _grm, _grv, _gnb, _gsaved):
+    B, N, slope, bf16, use_batch, has_prep = ctx.meta
+    t = ctx.saved_tensors
+    X, X16, weight = t[0], t[1], t[2]
+    saved = list(t[3:8])
+    prep = t[8] if has_prep else None
+    dX, dW, dg, db = torch.ops.dgx.pointconv_backward(g_out.contiguous(), X, X16, weight, saved, prep, B, N, slope,
+                                                      bf16, use_batch)
+    return dX, None, None, None, dW, dg, db, None, None, None, None, None, None, None, None, None, None
+
+
+torch.library.register_autograd("dgx::pointconv", _pc_bwd, setup_context=_pc_setup)
+
+
+# ------------------------------------------------------------------ DGCNN ----
+def _bn_args(bn, dev):
+    e = _empty(dev)
+    return (bn.running_mean if bn.running_mean is not None else e,
+            bn.running_var if bn.running_var is not None else e,
+            bn.num_batches_tracked if bn.num_batches_tracked is not None else _empty(dev, torch.int64),
+            bn.training, bn.track_running_stats, -1.0 if bn.momentum is None else float(bn.momentum), float(bn.eps))
+
+
+def _store_bn(bn, rm, rv, nb):
+    """Copy the op's updated running statistics into the module (only when
+    nn.BatchNorm would have updated them: training and tracking)."""
+    if not bn_.mode(bn)[1]:
+        return
+    with torch.no_grad():
+        if bn.running_mean is not None:
+            bn.running_mean.copy_(rm)
+        if bn.running_var is not None:
+            bn.running_var.copy_(rv)
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.copy_(nb)
+
+
+def enabled_for(model):
+    """The op path serves a model whose BatchNorms are plain nn.BatchNorm
+    (SyncBatchNorm needs its process group inside the op)."""
+    return ENABLED and not any(isinstance(m, torch.nn.SyncBatchNorm) for m in model.modules())
+
+
+def dgcnn_forward(model, x):
+    """models.dgcnn.DGCNN.forward through torch.ops.dgx (dgcnn.py:80-103)."""
+    ops.nat.require_device(x)   # no CPU fallback: a CPU cloud fails loudly here
+    B, _, N = x.shape
+    x = x.float()
+    dev = x.device
+    bf16 = prec.get() == "bf16"
+    blocks = model.edge_blocks()
+    convs = [b[0] for b in blocks]
+    bns = [b[1] for b in blocks]
+    c5, bn5, act5 = model.conv5[0], model.conv5[1], model.conv5[2]
+    for conv, bn in zip(convs + [c5], bns + [bn5]):
+        if conv.bias is not None or bn.weight is None:
+            raise NotImplementedError("dgx DGCNN expects Conv(bias=False) + affine BatchNorm (dgcnn.py:54-78)")
+    params = [p for c, bn in zip(convs + [c5], bns + [bn5]) for p in (c.weight, bn.weight, bn.bias)]
+    need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+    prep = None
+    if bf16:   # one launch for every bf16 operand copy of the step (blocks 2-4, conv5)
+        ws = [c.weight.detach() for c in convs[1:]] + [c5.weight.detach()]
+        shapes = _dgcnn_prep_shapes(ws)
+        prep = torch.ops.dgx.weight_prep(ws, [s[0] for s in shapes], [s[1] for s in shapes],
+                                         [s[2] for s in shapes], [s[3] for s in shapes])
+    bn_in = [_bn_args(bn, dev) for bn in bns]
+    xcat, xcat16, rms, rvs, nbs, _ = torch.ops.dgx.edgeconv_chain(
+        x, model.k, [c.weight for c in convs], [bn.weight for bn in bns], [bn.bias for bn in bns],
+        [a[0] for a in bn_in], [a[1] for a in bn_in], [a[2] for a in bn_in], [a[3] for a in bn_in],
+        [a[4] for a in bn_in], [a[5] for a in bn_in], [a[6] for a in bn_in],
+        [float(b[2].negative_slope) for b in blocks], bf16, need_grad, prep)
+    for bn, rm, rv, nb in zip(bns, rms, rvs, nbs):
+        _store_bn(bn, rm, rv, nb)
+    a5 = _bn_args(bn5, dev)
+    prep5 = None
+    if prep is not None:
+        # conv5's copies are the last entry of the shared buffer: pass them as their own view
+        _, lay = G.prep_layout(_dgcnn_prep_shapes([c.weight for c in convs[1:]] + [c5.weight]))
+        off = lay[3][0]
+        prep5 = prep[off:]
+    out, rm5, rv5, nb5, _ = torch.ops.dgx.pointconv(xcat, xcat16, B, N, c5.weight, bn5.weight, bn5.bias, a5[0], a5[1],
+                                                     a5[2], a5[3], a5[4], a5[5], a5[6], float(act5.negative_slope),
+                                                     bf16, prep5)
+    _store_bn(bn5, rm5, rv5, nb5)
+    return out

@@ -9,6 +9,7 @@ distances, BN statistics and every elementwise stage stay fp32 either way.
 Set with ``dgx.precision.set("bf16")`` or the environment variable
 ``DGX_PRECISION=bf16``.
 """
+import contextlib
 import functools
 import os
 
@@ -28,6 +29,19 @@ def set(mode):  # noqa: A001 (mirrors get)
     if mode not in ("fp32", "bf16"):
         raise ValueError(mode)
     _mode = mode
+
+
+@contextlib.contextmanager
+def mode(name):
+    """Temporarily run in precision ``name`` ("fp32" / "bf16")."""
+    global _mode
+    if name not in ("fp32", "bf16"):
+        raise ValueError(name)
+    prev, _mode = _mode, name
+    try:
+        yield
+    finally:
+        _mode = prev
 
 
 def operand(t):

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from dgx import gemm as _gemm
+from dgx import library as _library
 from dgx import ops as _ops
 from dgx import precision as _prec
 from dgx.edgeconv import edgeconv_stack_pair
@@ -84,6 +85,9 @@ class DGCNN(nn.Module):
         return [self.conv1, self.conv2, self.conv3, self.conv4]
 
     def forward(self, x):
+        if _library.enabled_for(self):
+            # the same kernels behind torch.ops.dgx custom ops (torch.compile / export see one node each)
+            return _library.dgcnn_forward(self, x)
         batch_size, _, num_points = x.size()
         preps = _bf16_weight_copies(self) if self.training else None
         # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)

@@ -282,6 +282,16 @@ int dgx_gemm_bf16(const void* A, int a_bf16, int a_ic, int64_t lda,
                   const void* B, int b_bf16, int b_ic, int64_t ldb,
                   int M, int N, int K, int epi, int splits,
                   float* C, int64_t ldc, float* partials, void* stream);
+/* fp32 MFMA GEMM of the parity mode (v_mfma_f32_16x16x4_f32, exact products,
+ * fp32 accumulation): the same C[i][j] = sum_k opA(i,k) opB(j,k) contract as
+ * dgx_gemm_bf16 with fp32 operands read in place (a_ic / b_ic: i- / j-
+ * contiguous), epi 0 store, 1 accumulate (C = addend + .. when addend is
+ * given, else C += ..), 3 split-K slabs (C = splits x M x N, summed by
+ * dgx_slab_reduce_f32). Replaces the fp32 Conv(1x1) GEMMs of reference
+ * models/dgcnn.py:54-78 and models/layers.py:17-24 and their dgrad / wgrad. */
+int dgx_gemm_f32(const float* A, int a_ic, int lda, const float* B, int b_ic, int ldb, int M, int N, int K, int epi,
+                 int splits, float* C, int64_t ldc, const float* addend, int64_t ldd, void* stream);
+int dgx_gemm_f32_splits(int M, int N, int K);
 /* Exact fp32 GEMM for a short reduction: C (M x N, row stride ldc) = X W^T,
  * X (M x K, row stride ldx), W (N x K) dense; each output an fmaf chain over
  * k = 0..K-1. K <= 16, N % 4 == 0, 16-byte aligned C rows. The layer-1
