@@ -303,7 +303,7 @@ class _EdgeConvStack(torch.autograd.Function):
                 dwcat = prec.mm(dPQ.t(), X)  # (2Co, C)
                 grads[3 * li] = torch.cat([dwcat[:co], dwcat[co:]], dim=1).reshape(w.shape)
                 if li > 0:
-                    dxcat[:, prev:prev + cin] += prec.mm(dPQ, wcat)
+                    prec.mm(dPQ, wcat, out=dxcat[:, prev:prev + cin], accumulate=True)
                 elif ctx.x_needs_grad:
                     dx_in = prec.mm(dPQ, wcat).view(B, N, C0).permute(0, 2, 1)
         return (dx_in, None, None, None, None, *grads)

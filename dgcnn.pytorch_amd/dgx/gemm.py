@@ -152,6 +152,30 @@ def mm32(a, b, out=None, accumulate=False, addend=None):
     return out
 
 
+def mm16(a, b, out=None, accumulate=False):
+    """out (M,N) (+)= a (M,K) @ b (K,N) on the bf16 MFMA GEMM (dgx_gemm_bf16:
+    fp32 or bf16 operands rounded to bf16 while staged, fp32 accumulation);
+    transposed views read in place; long reductions split-K (deterministic)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if a.stride(1) != 1 and a.stride(0) != 1:
+        a = a.contiguous()
+    if b.stride(1) != 1 and b.stride(0) != 1:
+        b = b.contiguous()
+    a_ic = a.stride(1) != 1           # (M,K) with unit stride along M: pass a^T (K,M) row-major
+    b_ic = b.stride(1) == 1           # (K,N) row-major: opB(j,k) = b[k,j] is j-contiguous
+    A = a.t() if a_ic else a
+    Bv = b if b_ic else b.t()
+    if K >= 2048 and not accumulate and out is None and a_ic and b_ic:
+        # the weight-gradient form (reduction over the B*N rows): split-K slabs
+        o = torch.empty((M, N), dtype=torch.float32, device=a.device)
+        return mm_atb(A, Bv, o)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    gemm(A, a_ic, Bv, b_ic, M, N, K, EPI_ACCUM if accumulate else EPI_STORE, out)
+    return out
+
+
 SMALLK_MAX = 16
 
 

@@ -3,7 +3,8 @@
 Replaces conv5 of reference models/dgcnn.py:74-78, 100-102: the reference
 concatenates x1..x4 into (B,512,N,1) and runs Conv2d -> BatchNorm2d ->
 LeakyReLU -> view(B,emb,N). Here the input is the EdgeConv chain's point-major
-concat buffer (B*N, 512) as is; Z = X W^T is one GEMM (precision.mm), BN
+concat buffer (B*N, 512) as is; Z = X W^T is one engine GEMM (bf16 MFMA with
+the BN statistics in its epilogue, or the fp32 MFMA GEMM in parity mode), BN
 statistics / affine / LeakyReLU and the transpose to the reference's (B,emb,N)
 layout are libdgx passes (pointconv.hip). BN follows nn.BatchNorm rules per
 module (dgx.bn: batch or running statistics by the BN's own flags, biased
@@ -120,9 +121,9 @@ class _PointConvBNLReLU(torch.autograd.Function):
             else:
                 G.mm_atb(dZ, Xop, dW)
                 dX = G.mm_xw(dZ, W)
-        else:
-            dW = torch.mm(dZ.t(), Xop)
-            dX = torch.mm(dZ, W)
+        else:   # fp32 MFMA GEMMs (dW: split-K over the B*N rows)
+            dW = prec.mm(dZ.t(), Xop)
+            dX = prec.mm(dZ, W)
         return dX, None, None, None, None, None, None, dW.view(ctx.wshape), dgamma, dbeta
 
 

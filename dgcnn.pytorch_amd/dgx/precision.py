@@ -1,10 +1,13 @@
 """GEMM operand precision of the engine.
 
-"fp32" (default): every GEMM in fp32 (f32 MFMA, exact f32 products) — the
-parity mode the tests hold to 1e-3 against the reference.
+"fp32" (default): every GEMM on the engine's fp32 MFMA kernel (gemm32.hip,
+v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation) or the exact
+small-K kernel for the 3-channel layer — the parity mode the tests hold to
+1e-3 against the reference.
 "bf16": the per-point and conv5 GEMM operands are rounded to bf16, products
-accumulate in fp32 and outputs stay fp32 (BASELINE.json cfg2 "bf16"). kNN
-distances, BN statistics and every elementwise stage stay fp32 either way.
+accumulate in fp32 and outputs stay fp32 (BASELINE.json cfg2 "bf16"), on the
+engine's bf16 MFMA kernels (gemm.hip). kNN distances, BN statistics and every
+elementwise stage stay fp32 either way.
 
 Set with ``dgx.precision.set("bf16")`` or the environment variable
 ``DGX_PRECISION=bf16``.
@@ -49,11 +52,15 @@ def operand(t):
     return t.to(torch.bfloat16) if _mode == "bf16" else t
 
 
-def mm(a, b):
-    """a @ b with fp32 output; bf16 operands when the mode says so."""
+def mm(a, b, out=None, accumulate=False):
+    """a @ b (fp32 output) on the engine's GEMMs in the current precision:
+    fp32 MFMA (dgx.gemm.mm32) or bf16 operands with fp32 accumulation
+    (dgx.gemm.mm16). Transposed views are read in place. ``accumulate``:
+    out += a @ b."""
+    from . import gemm
     if _mode == "bf16":
-        return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
-    return torch.mm(a, b)
+        return gemm.mm16(a, b, out=out, accumulate=accumulate)
+    return gemm.mm32(a, b, out=out, accumulate=accumulate)
 
 
 def no_autocast(fn):

@@ -239,3 +239,33 @@ def test_lds_xwt_split_weight(cuda, M, N, K):
     e_split = float((z.double() - exact).abs().max())
     e_hi = float((G.lds_xwt(x, nt[:, :K].contiguous()).double() - exact).abs().max())
     assert e_split < 0.25 * e_hi
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [(32768, 128, 64, False, True), (32768, 64, 128, False, False),
+                                         (130, 70, 33, True, False), (1, 5, 17, False, False),
+                                         (256, 512, 32768, True, True), (64, 3, 2048, True, True),
+                                         (4096, 1024, 512, False, True)])
+def test_mm32_fp32_mfma(cuda, M, N, K, ta, tb):
+    """The parity mode's engine GEMM (dgx_gemm_f32, v_mfma_f32_16x16x4_f32):
+    a (M,K) @ b (K,N) for row-major and transposed views read in place,
+    ragged edges and the split-K weight-gradient form, against fp64."""
+    from dgx import gemm as G
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn((K, M) if ta else (M, K), generator=g)
+    b = torch.randn((N, K) if tb else (K, N), generator=g)
+    ad, bd = a.to(cuda), b.to(cuda)
+    av, bv = (ad.t() if ta else ad), (bd.t() if tb else bd)
+    got = G.mm32(av, bv)
+    ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
+    assert rel_err(got.cpu(), ref) < 1e-5
+    # accumulate into a column slice of a wider buffer, and the addend form
+    wide = torch.randn((M, N + 9), device=cuda)
+    base = wide.clone()
+    if K < 2048:
+        G.mm32(av, bv, out=wide[:, 4:4 + N], accumulate=True)
+        assert rel_err(wide[:, 4:4 + N].cpu(), base[:, 4:4 + N].cpu().double() + ref) < 1e-5
+        assert torch.equal(wide[:, :4], base[:, :4]) and torch.equal(wide[:, 4 + N:], base[:, 4 + N:])
+        add = torch.randn((M, N), device=cuda)
+        out = torch.empty((M, N), device=cuda)
+        G.mm32(av, bv, out=out, addend=add)
+        assert rel_err(out.cpu(), add.cpu().double() + ref) < 1e-5
