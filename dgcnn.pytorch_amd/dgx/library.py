@@ -82,6 +82,27 @@ def _use_batch(training, rm):
     return bool(training) or rm.numel() == 0
 
 
+def _copy_many(dsts, srcs):
+    """dst_i <- src_i for many small tensors in one multi-tensor launch per
+    dtype (the BN running statistics cross the functional op boundary as
+    private copies: 2 launches per step instead of one per tensor)."""
+    groups = {}
+    for d, s in zip(dsts, srcs):
+        if d.numel():
+            groups.setdefault(d.dtype, ([], []))
+            groups[d.dtype][0].append(d)
+            groups[d.dtype][1].append(s)
+    for ds, ss in groups.values():
+        torch._foreach_copy_(ds, ss)
+
+
+def _fresh(ts):
+    """Private copies of ``ts`` (distinct storages: op outputs may not alias)."""
+    outs = [torch.empty_like(t) for t in ts]
+    _copy_many(outs, ts)
+    return outs
+
+
 # ------------------------------------------------------------------- knn ----
 @torch.library.custom_op("dgx::knn", mutates_args=(), device_types="cuda")
 def knn(x: Tensor, k: int) -> Tensor:
@@ -141,12 +162,15 @@ def _(grad, idx, C, mode):
 
 
 def _gf_setup(ctx, inputs, output):
+    ctx.set_materialize_grads(False)   # no zero-filled gradients for the idx output
     ctx.save_for_backward(output[1])
     ctx.C, ctx.mode = inputs[0].shape[1], inputs[2]
 
 
 def _gf_bwd(ctx, gout, _gidx):
     (idx,) = ctx.saved_tensors
+    if gout is None:
+        return None, None, None
     return torch.ops.dgx.graph_feature_backward(gout.contiguous(), idx, ctx.C, ctx.mode), None, None
 
 
@@ -210,9 +234,9 @@ def edgeconv_chain(x: Tensor, k: int, weights: list[Tensor], gammas: list[Tensor
     """DGCNN's EdgeConv blocks (dgcnn.py:84-100) as dgx.edgeconv runs them:
     returns (concat buffer (B*N, sum Co), its bf16 twin or empty, updated
     running means / vars / batch counters, the state the backward reads)."""
-    rms = [t.clone() for t in running_means]
-    rvs = [t.clone() for t in running_vars]
-    nbs = [t.clone() for t in nbts]
+    n = len(running_means)
+    fresh = _fresh(list(running_means) + list(running_vars) + list(nbts))
+    rms, rvs, nbs = fresh[:n], fresh[n:2 * n], fresh[2 * n:]
     specs = [_BNSpec(*a) for a in zip(training, track, rms, rvs, nbs, momentum, eps)]
     layers = _chain_layers(weights, specs, slopes)
     params = [t for trip in zip(weights, gammas, betas) for t in trip]
@@ -303,6 +327,9 @@ def _chain_setup(ctx, inputs, output):
     (x, k, weights, gammas, betas, rms, rvs, nbts, training, track, momentum, eps, slopes, bf16, need_grad,
      prep) = inputs
     xcat, xcat16, _, _, _, saved = output
+    # the running statistics and saved-state outputs take no gradient: without
+    # this autograd would zero-fill one gradient per saved tensor every step
+    ctx.set_materialize_grads(False)
     ctx.n, ctx.nsaved, ctx.has_prep = len(weights), len(saved), prep is not None
     ctx.k, ctx.slopes, ctx.bf16 = k, list(slopes), bf16
     ctx.use_batch = [_use_batch(t, rm) for t, rm in zip(training, rms)]
@@ -342,7 +369,7 @@ def pointconv(X: Tensor, X16: Tensor, B: int, N: int, weight: Tensor, gamma: Ten
     """conv5 -> BN -> LeakyReLU on the concat buffer (dgcnn.py:100-102) as
     dgx.pointconv runs it: (out (B, Co, N), updated running mean / var /
     batch counter, saved state [Z, scale, shift, mean, invstd])."""
-    rm, rv, nb = running_mean.clone(), running_var.clone(), nbt.clone()
+    rm, rv, nb = _fresh([running_mean, running_var, nbt])
     spec = _BNSpec(training, track, rm, rv, nb, momentum, eps)
     wprep = None
     if prep is not None:
@@ -399,6 +426,7 @@ def _(dout, X, X16, weight, saved, prep, B, N, slope, bf16, use_batch):
 
 def _pc_setup(ctx, inputs, output):
     (X, X16, B, N, weight, gamma, beta, rm, rv, nbt, training, track, momentum, eps, slope, bf16, prep) = inputs
+    ctx.set_materialize_grads(False)
     ctx.meta = (B, N, slope, bf16, _use_batch(training, rm), prep is not None)
     ctx.save_for_backward(X, X16, weight, *output[4], *([prep] if prep is not None else []))
 
@@ -409,6 +437,8 @@ def _pc_bwd(ctx, g_out, _grm, _grv, _gnb, _gsaved):
     X, X16, weight = t[0], t[1], t[2]
     saved = list(t[3:8])
     prep = t[8] if has_prep else None
+    if g_out is None:
+        g_out = torch.zeros((B, weight.shape[0], N), dtype=torch.float32, device=X.device)
     dX, dW, dg, db = torch.ops.dgx.pointconv_backward(g_out.contiguous(), X, X16, weight, saved, prep, B, N, slope,
                                                       bf16, use_batch)
     return dX, None, None, None, dW, dg, db, None, None, None, None, None, None, None, None, None, None
@@ -426,18 +456,20 @@ def _bn_args(bn, dev):
             bn.training, bn.track_running_stats, -1.0 if bn.momentum is None else float(bn.momentum), float(bn.eps))
 
 
-def _store_bn(bn, rm, rv, nb):
-    """Copy the op's updated running statistics into the module (only when
-    nn.BatchNorm would have updated them: training and tracking)."""
-    if not bn_.mode(bn)[1]:
-        return
+def _store_bn(pairs):
+    """Copy the ops' updated running statistics into the modules (only where
+    nn.BatchNorm would have updated them: training and tracking), all layers in
+    one multi-tensor copy per dtype. ``pairs``: (bn, rm, rv, nbt) per layer."""
+    dsts, srcs = [], []
+    for bn, rm, rv, nb in pairs:
+        if not bn_.mode(bn)[1]:
+            continue
+        for d, s in ((bn.running_mean, rm), (bn.running_var, rv), (bn.num_batches_tracked, nb)):
+            if d is not None:
+                dsts.append(d)
+                srcs.append(s)
     with torch.no_grad():
-        if bn.running_mean is not None:
-            bn.running_mean.copy_(rm)
-        if bn.running_var is not None:
-            bn.running_var.copy_(rv)
-        if bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.copy_(nb)
+        _copy_many(dsts, srcs)
 
 
 def enabled_for(model):
@@ -474,8 +506,6 @@ def dgcnn_forward(model, x):
         [a[0] for a in bn_in], [a[1] for a in bn_in], [a[2] for a in bn_in], [a[3] for a in bn_in],
         [a[4] for a in bn_in], [a[5] for a in bn_in], [a[6] for a in bn_in],
         [float(b[2].negative_slope) for b in blocks], bf16, need_grad, prep)
-    for bn, rm, rv, nb in zip(bns, rms, rvs, nbs):
-        _store_bn(bn, rm, rv, nb)
     a5 = _bn_args(bn5, dev)
     prep5 = None
     if prep is not None:
@@ -486,5 +516,5 @@ def dgcnn_forward(model, x):
     out, rm5, rv5, nb5, _ = torch.ops.dgx.pointconv(xcat, xcat16, B, N, c5.weight, bn5.weight, bn5.bias, a5[0], a5[1],
                                                      a5[2], a5[3], a5[4], a5[5], a5[6], float(act5.negative_slope),
                                                      bf16, prep5)
-    _store_bn(bn5, rm5, rv5, nb5)
+    _store_bn(list(zip(bns, rms, rvs, nbs)) + [(bn5, rm5, rv5, nb5)])
     return out
