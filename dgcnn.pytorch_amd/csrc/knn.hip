@@ -14,15 +14,18 @@
 //   knn_image_kernel  one pass over x: |x|^2 in the reference's order and an
 //                     MFMA A-operand "image" of each cloud (16-candidate tiles,
 //                     lane-ordered so a wave fetches a tile with 16-B loads).
-//   knn_kernel        workgroup = 4 waves = 2 query groups of 16 x 2 candidate
-//                     halves (even / odd tiles). Each wave keeps its 16 queries'
-//                     operands in registers and streams its half of the cloud's
-//                     image straight from L2 through a two-slot register ring;
-//                     no LDS staging, no barrier until the final merge. Each
-//                     query's candidates are dealt over 8 register lists (4 lanes
-//                     x 2 halves) with an admission bound shared through LDS.
-//                     A (rare) row whose list overflowed is recomputed exactly
-//                     by the same block at the end (knn_fix_row).
+//   knn_kernel        workgroup = 4 waves = 2 wave groups x 2 candidate halves
+//                     (even / odd tiles); a wave serves QG groups of 16 queries
+//                     (QG = 2 at C > 64: two independent MFMA chains per image
+//                     tile). Each wave keeps its queries' operands in registers
+//                     and streams its half of the cloud's image straight from L2
+//                     through a two-slot register ring; no LDS staging, no
+//                     barrier until the final merge. Each query's candidates are
+//                     dealt over 8 register lists (4 lanes x 2 halves) with an
+//                     admission bound shared through LDS; 3-channel clouds first
+//                     run a values-only pre-pass that seeds that bound. A (rare)
+//                     row whose list overflowed is recomputed exactly by the
+//                     same block at the end (knn_fix_row).
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -228,16 +231,6 @@ inline int knn_ntile(int N) { return (N + 15) / 16; }
 constexpr int FIX_MAXN = 12288;  // largest N (the fix-up's tie bitmap)
 constexpr int FX_CAP = 256;      // candidates above T0 ranked directly by the fix-up
 
-template <int KB>
-constexpr int knn_smem_floats() {
-    constexpr int stream = KQ_HALVES * KQ_QPB                     // published admission bounds
-                           + KQ_WAVES * KQ_QCAP * 64              // FIFO values
-                           + KQ_WAVES * KQ_QCAP * 32;             // FIFO indices (u16)
-    constexpr int merge = KQ_HALVES * KQ_QPB * KB * 2 + 2 * KQ_QPB;  // half lists | k-th | flags
-    constexpr int fix = merge + 2 * FX_CAP + 8 + FIX_MAXN / 32;      // ... | fix-up candidates, counters, tie bitmap
-    return stream > fix ? stream : fix;
-}
-
 // Canonical order: value descending, then index ascending.
 __device__ __forceinline__ bool canon_better(float av, int aj, float bv, int bj) {
     return av > bv || (av == bv && aj < bj);
@@ -389,140 +382,271 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
 }
 
 // ------------------------------------------------------------ knn kernel ----
-// Block = KQ_GROUPS query groups x 2 candidate halves, one wave each. A wave
-// streams the tiles s = h, h+2, h+4, ... of its cloud's image with its loads
-// two units ahead (see the operand stream below). The only block-wide
+// Block = KQ_GROUPS wave groups x 2 candidate halves, one wave each; a wave
+// serves QG groups of 16 queries (QG = 2: 32 queries per wave, 64 per block).
+// A wave streams the tiles s = h, h+2, h+4, ... of its cloud's image with its
+// loads two units ahead (see the operand stream below). With QG = 2 every
+// image tile feeds two independent MFMA chains (one per query group), so a
+// wave keeps the matrix pipe busy through the f32 MFMA's dependent latency
+// and each tile is fetched once per 32 queries. The only block-wide
 // synchronisation is the final merge.
-template <int NSTEP, int KB>
-__global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const float* __restrict__ img,
-                                                         const float* __restrict__ xximg,
-                                                         const float* __restrict__ xx, int B, int N, int k,
-                                                         int nqb, int64_t* __restrict__ idx64,
-                                                         int32_t* __restrict__ idx32, float* __restrict__ vals,
-                                                         const float* __restrict__ seed
+template <int KB, int QG>
+constexpr int knn_smem_floats_qg() {
+    constexpr int qpb = KQ_GROUPS * KQ_QPW * QG;
+    constexpr int stream = KQ_HALVES * qpb                              // published admission bounds
+                           + KQ_WAVES * QG * KQ_QCAP * 64               // FIFO values
+                           + KQ_WAVES * QG * KQ_QCAP * 32;              // FIFO indices (u16)
+    constexpr int merge = KQ_HALVES * qpb * KB * 2 + 2 * qpb;          // half lists | k-th | flags
+    constexpr int fix = merge + 2 * FX_CAP + 8 + FIX_MAXN / 32;         // ... | fix-up candidates, counters, tie bitmap
+    return stream > fix ? stream : fix;
+}
+
+template <int NSTEP, int KB, int QG>
+__global__ __launch_bounds__(KQ_THREADS, QG == 1 ? (KB <= 40 ? 4 : 2) : (KB <= 40 ? 2 : 1))
+void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, const float* __restrict__ xx, int B,
+                int N, int k, int nqb, int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
+                float* __restrict__ vals, const float* __restrict__ seed
 #ifdef DGX_KNN_STATS
-                                                         , uint32_t* __restrict__ stats
+                , uint32_t* __restrict__ stats
 #endif
-                                                         ) {
+                ) {
 #pragma clang fp contract(off)
     constexpr int KL = KnnList<KB>::KL;
     constexpr int RPL = KnnList<KB>::RPL;
-    __shared__ __attribute__((aligned(16))) float smem[knn_smem_floats<KB>()];
-    float* pub = smem;                            // [KQ_HALVES][KQ_QPB] admission bounds
-    float* fval = smem + KQ_HALVES * KQ_QPB;      // per wave [KQ_QCAP][64] pending values
-    uint16_t* fidx = reinterpret_cast<uint16_t*>(fval + KQ_WAVES * KQ_QCAP * 64);  // ... and indices
+    constexpr int QPW = KQ_QPW * QG;           // queries per wave
+    constexpr int QPB = KQ_GROUPS * QPW;       // queries per block
+    __shared__ __attribute__((aligned(16))) float smem[knn_smem_floats_qg<KB, QG>()];
+    float* pub = smem;                         // [KQ_HALVES][QPB] admission bounds
+    float* fval = smem + KQ_HALVES * QPB;      // per (wave, group) [KQ_QCAP][64] pending values
+    uint16_t* fidx = reinterpret_cast<uint16_t*>(fval + KQ_WAVES * QG * KQ_QCAP * 64);  // ... and indices
 
     int b, qb;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int grp = wave % KQ_GROUPS;  // query group
+    // wave-uniform in a scalar register: the half's tile count and every
+    // "unit is live" test become scalar branches
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave % KQ_GROUPS;  // wave group: queries grp*QPW ..
     const int h = wave / KQ_GROUPS;    // candidate half: tiles h, h + 2, h + 4, ...
     const int g = lane >> 4;           // MFMA output rows 4g..4g+3 of a tile
     const int ql = lane & 15;
-    const int qq = grp * KQ_QPW + ql;  // query within the block
-    const int q = qb * KQ_QPB + qq;
     const int ntile = (N + 15) >> 4;
     const float* __restrict__ ib = img + (int64_t)b * ntile * 64 * NSTEP;
     const float* __restrict__ xib = xximg + (int64_t)b * ntile * 16;
-
-    // B operand (queries) in registers: lane holds x[q][4t + g], read from the
-    // query's own image row (zero channels beyond C; q >= N reads a zero row).
-    float bq[NSTEP];
-    {
-        const int qs = min(q, N - 1);
-        ld_vec<NSTEP>(ib + ((int64_t)(qs >> 4) * 64 + g * 16 + knn_row(qs & 15)) * NSTEP, bq);
-        // 2 x the query operand: every product and partial sum of the fmaf chain
-        // doubles exactly, so the MFMA returns fl(2 * dot) (dgcnn.py:7) directly
-#pragma unroll
-        for (int t = 0; t < NSTEP; ++t) bq[t] *= 2.0f;
-    }
-    const float xxq = q < N ? xx[(int64_t)b * N + q] : 0.f;
-
-    // Each lane keeps the KL best of ITS candidates (sorted, registers, static
-    // indexing). Admission filter thr = max(own KL-th, T) where T = min over
-    // the query's 8 lists of their m-th value, m = ceil(k/8): 8 lists x m
-    // candidates >= T exist, so T never exceeds the row's final k-th value. The
-    // other half's 4 lists contribute through `pub` — a value published at its
-    // last flush; lists only improve, so a stale value is still a lower bound.
-    // '>=' keeps equal values; their order is settled canonically at the merge.
     const int m = (k + KQ_LISTS - 1) / KQ_LISTS;
     const int m4 = (k + 3) / 4;
-    float lv[KL];
-    int li[KL];
-#pragma unroll
-    for (int t = 0; t < KL; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
 
-    // Candidates that pass the filter wait in a per-lane FIFO in LDS and are
-    // inserted in batches, so an insertion round (5*KL VALU ops for the whole
-    // wave) is paid once per admitted candidate of the busiest lane.
-    float* fv = fval + wave * (KQ_QCAP * 64);
-    uint16_t* fj = fidx + wave * (KQ_QCAP * 64);
-    int cnt = 0;
-    // admission seed (dgx_knn_seed_f32): a lower bound of the row's k-th value
-    // in this kernel's exact arithmetic, so candidates below it can never
-    // enter the top-k; -inf without seeds
-    const float tseed = (seed != nullptr && q < N) ? seed[(int64_t)b * N + q] : -INFINITY;
-    float thr = tseed;
-    if (tid < KQ_HALVES * KQ_QPB) pub[tid] = -INFINITY;
+    // Per query group: one struct per group, every access by name (an array
+    // indexed by the group number is not split into registers: its selects
+    // became scratch loads).
+    struct Grp {
+        int qq, q;               // query within the block / within the cloud
+        float bq[NSTEP];         // B operand: x[q][4t + g], doubled
+        float xxq, tseed, thr;
+        float lv[KL];            // the lane's sorted list (value desc, index asc)
+        int li[KL];
+        float* fv;               // the lane's FIFO of admitted candidates (LDS)
+        uint16_t* fj;
+        int cnt;
+        f32x4 acc;
+        float last;
+        float ov[RPL];           // merged ranks 4t + g of the wave's 4 lists
+        int oj[RPL];
+        int rk[RPL];             // final ranks after the half merge
+    };
+    Grp G0, G1;
+    auto each = [&](auto&& fn) {
+        fn(G0, 0);
+        if constexpr (QG == 2) fn(G1, 1);
+    };
+
+    each([&](Grp& S, int e) {
+        S.qq = grp * QPW + e * KQ_QPW + ql;
+        S.q = qb * QPB + S.qq;
+        // B operand from the query's own image row (zero channels beyond C;
+        // q >= N reads a zero row). 2 x the query operand: every product and
+        // partial sum of the fmaf chain doubles exactly, so the MFMA returns
+        // fl(2 * dot) (dgcnn.py:7) directly.
+        const int qs = min(S.q, N - 1);
+        ld_vec<NSTEP>(ib + ((int64_t)(qs >> 4) * 64 + g * 16 + knn_row(qs & 15)) * NSTEP, S.bq);
+#pragma unroll
+        for (int t = 0; t < NSTEP; ++t) S.bq[t] *= 2.0f;
+        S.xxq = S.q < N ? xx[(int64_t)b * N + S.q] : 0.f;
+        // admission seed (dgx_knn_seed_f32): a lower bound of the row's k-th
+        // value in this kernel's exact arithmetic, so candidates below it can
+        // never enter the top-k; -inf without seeds
+        S.tseed = (seed != nullptr && S.q < N) ? seed[(int64_t)b * N + S.q] : -INFINITY;
+        S.thr = S.tseed;
+#pragma unroll
+        for (int t = 0; t < KL; ++t) { S.lv[t] = -INFINITY; S.li[t] = 0x7fffffff; }
+        S.fv = fval + (wave * QG + e) * (KQ_QCAP * 64);
+        S.fj = fidx + (wave * QG + e) * (KQ_QCAP * 64);
+        S.cnt = 0;
+    });
+    // Each lane keeps, per group, the KL best of ITS candidates (sorted,
+    // registers, static indexing). Admission filter thr = max(own KL-th, T)
+    // where T = min over the query's 8 lists of their m-th value, m = ceil(k/8):
+    // 8 lists x m candidates >= T exist, so T never exceeds the row's final k-th
+    // value. The other half's 4 lists contribute through `pub` — a value
+    // published at its last flush; lists only improve, so a stale value is
+    // still a lower bound. '>=' keeps equal values; their order is settled
+    // canonically at the merge. Candidates that pass wait in the lane's FIFO
+    // and are inserted in batches, so an insertion round (5*KL VALU ops for
+    // the whole wave) is paid once per admitted candidate of the busiest lane.
+    if (tid < KQ_HALVES * QPB) pub[tid] = -INFINITY;
     static_assert(KnnList<KB>::KL >= (KB + 3) / 4, "lists must hold the m4-th value");
     __syncthreads();
+    if constexpr (NSTEP == 1 && QG == 1) {
+        // Admission pre-pass (3-channel clouds, where one MFMA makes a whole
+        // tile and the selection VALU is the cost): each lane first streams its
+        // candidates once keeping only the m = ceil(k/8) best VALUES (one
+        // v_med3 per slot, no indices, no FIFO). 8 lists x m candidates reach
+        // T = min over the query's 8 lists of their m-th value, so T is a lower
+        // bound of the row's k-th value in this kernel's own arithmetic — the
+        // main pass then admits only the few candidates above it instead of
+        // inserting everything while its bound climbs from -inf.
+        constexpr int MM = (KB + KQ_LISTS - 1) / KQ_LISTS;
+        float p[MM];
+#pragma unroll
+        for (int t = 0; t < MM; ++t) p[t] = -INFINITY;
+        const int ntl0 = (ntile - h + KQ_HALVES - 1) / KQ_HALVES;
+        auto put = [&](float v) {
+#pragma unroll
+            for (int t = MM - 1; t > 0; --t) p[t] = __builtin_amdgcn_fmed3f(p[t - 1], p[t], v);
+            p[0] = fmaxf(p[0], v);
+        };
+        // tiles in chunks of PC, the next chunk's operands in flight while this
+        // one is selected (one L2 latency per chunk, not per tile); only the
+        // cloud's last tile can hold padding rows (j >= N: excluded)
+        constexpr int PC = 4;
+        float av[2][PC];
+        float4 xv[2][PC];
+        auto fetch = [&](int buf, int tl0) {
+#pragma unroll
+            for (int c = 0; c < PC; ++c) {
+                const int s = h + KQ_HALVES * min(tl0 + c, ntl0 - 1);
+                av[buf][c] = ib[(int64_t)s * 64 + lane];
+                xv[buf][c] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
+            }
+        };
+        if (ntl0 > 0) fetch(0, 0);
+#pragma unroll 1
+        for (int tl0 = 0; tl0 < ntl0; tl0 += 2 * PC) {
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const int base = tl0 + half * PC;
+                fetch(half ^ 1, base + PC);
+                if (base < ntl0) {
+#pragma unroll
+                    for (int c = 0; c < PC; ++c) {
+                        const int tl = base + c;
+                        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(av[half][c], G0.bq[0],
+                                                                             f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                        const float4 xc4 = xv[half][c];
+                        float v0 = (d[0] - xc4.x) - G0.xxq, v1 = (d[1] - xc4.y) - G0.xxq;
+                        float v2 = (d[2] - xc4.z) - G0.xxq, v3 = (d[3] - xc4.w) - G0.xxq;
+                        const int s = h + KQ_HALVES * tl;
+                        if (tl >= ntl0 || (s + 1) * 16 > N) {   // wave-uniform: past the end / the padded tile
+                            const int j0 = tl < ntl0 ? s * 16 + g : N;
+                            v0 = j0 < N ? v0 : -INFINITY;
+                            v1 = j0 + 4 < N ? v1 : -INFINITY;
+                            v2 = j0 + 8 < N ? v2 : -INFINITY;
+                            v3 = j0 + 12 < N ? v3 : -INFINITY;
+                        }
+                        put(v0);
+                        put(v1);
+                        put(v2);
+                        put(v3);
+                    }
+                }
+            }
+        }
+        // (an exact k-th of the 8 lists' values by counting measured slower:
+        // 61 vs 57 us at cfg2, the count costs more than the admissions it saves)
+        float tm = p[0];
+#pragma unroll
+        for (int t = 1; t < MM; ++t) tm = (t == m - 1) ? p[t] : tm;
+        tm = fminf(tm, __shfl_xor(tm, 16));
+        tm = fminf(tm, __shfl_xor(tm, 32));
+        if (g == 0) pub[h * QPB + G0.qq] = tm;
+        __syncthreads();
+        const float T = fminf(tm, pub[(1 - h) * QPB + G0.qq]);
+        if (G0.q < N) G0.tseed = fmaxf(G0.tseed, T);
+        G0.thr = G0.tseed;
+    }
 #ifdef DGX_KNN_STATS
     uint32_t n_rounds = 0, n_flush = 0;
 #endif
+    auto cmax = [&]() { return QG == 2 ? max(G0.cnt, G1.cnt) : G0.cnt; };
     auto flush = [&]() {
 #ifdef DGX_KNN_STATS
         ++n_flush;
 #endif
         // branch-free rounds: slots past a lane's count read stale entries and
-        // are replaced by -inf, so every round is the same straight-line code
-        float cv = fv[lane];
-        int cj = fj[lane];
-        cv = cnt > 0 ? cv : -INFINITY;
+        // are replaced by -inf, so every round is the same straight-line code;
+        // the groups' lists are independent (two interleaved dependency chains)
+        float cv0 = G0.cnt > 0 ? G0.fv[lane] : -INFINITY, cv1 = 0.f;
+        int cj0 = G0.fj[lane], cj1 = 0;
+        if constexpr (QG == 2) {
+            cv1 = G1.cnt > 0 ? G1.fv[lane] : -INFINITY;
+            cj1 = G1.fj[lane];
+        }
+        const int cm = cmax();
         // fully unrolled with an early exit: no loop-carried copies of the list
 #pragma unroll
         for (int t = 0; t < KQ_QCAP; ++t) {
-            if (!__any(t < cnt)) break;
+            if (!__any(t < cm)) break;
 #ifdef DGX_KNN_STATS
             ++n_rounds;
 #endif
             const int nx = min(t + 1, KQ_QCAP - 1);
-            float nv = fv[nx * 64 + lane];
-            const int nj = fj[nx * 64 + lane];
-            nv = t + 1 < cnt ? nv : -INFINITY;
-            list_insert_ordered<KL>(lv, li, cv >= thr ? cv : -INFINITY, cj);
-            cv = nv;
-            cj = nj;
+            float nv0 = G0.fv[nx * 64 + lane];
+            const int nj0 = G0.fj[nx * 64 + lane];
+            nv0 = t + 1 < G0.cnt ? nv0 : -INFINITY;
+            list_insert_ordered<KL>(G0.lv, G0.li, cv0 >= G0.thr ? cv0 : -INFINITY, cj0);
+            cv0 = nv0;
+            cj0 = nj0;
+            if constexpr (QG == 2) {
+                float nv1 = G1.fv[nx * 64 + lane];
+                const int nj1 = G1.fj[nx * 64 + lane];
+                nv1 = t + 1 < G1.cnt ? nv1 : -INFINITY;
+                list_insert_ordered<KL>(G1.lv, G1.li, cv1 >= G1.thr ? cv1 : -INFINITY, cj1);
+                cv1 = nv1;
+                cj1 = nj1;
+            }
         }
-        cnt = 0;
-        // admission bound: max of (own 4 lists' min m4-th value: 4*m4 >= k
-        // candidates reach it) and (all 8 lists' min m-th value: 8*m >= k)
-        float tm = lv[0], t4 = lv[0];
+        each([&](Grp& S, int) {
+            S.cnt = 0;
+            // admission bound: max of (own 4 lists' min m4-th value: 4*m4 >= k
+            // candidates reach it) and (all 8 lists' min m-th value: 8*m >= k)
+            float tm = S.lv[0], t4 = S.lv[0];
 #pragma unroll
-        for (int t = 1; t < KL; ++t) {
-            tm = (t == m - 1) ? lv[t] : tm;
-            t4 = (t == m4 - 1) ? lv[t] : t4;
-        }
-        tm = fminf(tm, __shfl_xor(tm, 16));
-        tm = fminf(tm, __shfl_xor(tm, 32));
-        t4 = fminf(t4, __shfl_xor(t4, 16));
-        t4 = fminf(t4, __shfl_xor(t4, 32));
-        if (g == 0) __hip_atomic_store(pub + h * KQ_QPB + qq, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const float tp = __hip_atomic_load(pub + (1 - h) * KQ_QPB + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        thr = fmaxf(fmaxf(fmaxf(t4, fminf(tm, tp)), lv[KL - 1]), tseed);
+            for (int t = 1; t < KL; ++t) {
+                tm = (t == m - 1) ? S.lv[t] : tm;
+                t4 = (t == m4 - 1) ? S.lv[t] : t4;
+            }
+            tm = fminf(tm, __shfl_xor(tm, 16));
+            tm = fminf(tm, __shfl_xor(tm, 32));
+            t4 = fminf(t4, __shfl_xor(t4, 16));
+            t4 = fminf(t4, __shfl_xor(t4, 32));
+            if (g == 0) __hip_atomic_store(pub + h * QPB + S.qq, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const float tp = __hip_atomic_load(pub + (1 - h) * QPB + S.qq, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            S.thr = fmaxf(fmaxf(fmaxf(t4, fminf(tm, tp)), S.lv[KL - 1]), S.tseed);
+        });
     };
 
-    auto consider = [&](float dot, float xc, int j) {
+    auto consider = [&](Grp& S, float dot, float xc, int j) {
         const float tq = dot - xc;  // dot is already 2 x (query operand doubled)
-        const float v = tq - xxq;
-        const bool pass = j < N && v >= thr;
+        const float v = tq - S.xxq;
+        const bool pass = j < N && v >= S.thr;
         // unconditional store: a rejected candidate's slot is reused by the
         // next one (a tile adds at most 4 entries to a FIFO holding <= QCAP-4)
-        fv[cnt * 64 + lane] = v;
-        fj[cnt * 64 + lane] = (uint16_t)j;
-        cnt += pass ? 1 : 0;
+        S.fv[S.cnt * 64 + lane] = v;
+        S.fj[S.cnt * 64 + lane] = (uint16_t)j;
+        S.cnt += pass ? 1 : 0;
     };
 
     // Operand stream: units of SW MFMA k-steps (a whole tile when NSTEP <= 16,
@@ -537,39 +661,47 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     const int nunits = ntl * SPT;
     float a[2][SW];
     float4 xq[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-    auto load = [&](int slot, int u) {
-        if (u >= nunits) return;
-        const int s = h + KQ_HALVES * (u / SPT), sl = u % SPT;
+    // Every load is unconditional (a unit past the end re-reads this half's
+    // last tile, unused): with a data-dependent skip the compiler cannot count
+    // the loads in flight and drains them all (vmcnt(0)) every trip. sl = u %
+    // SPT is a compile-time constant at every call.
+    auto load = [&](int slot, int u, int sl) {
+        const int s = min(h + KQ_HALVES * (u / SPT), ntile - 1);
         ld_vec<SW>(ib + ((int64_t)s * 64 + lane) * NSTEP + sl * SW, a[slot]);
         if (sl == 0) xq[slot] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
     };
-    load(0, 0);
-    load(1, 1);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    load(0, 0, 0);
+    load(1, 1, 1 % SPT);
     float4 xc = xq[0];
 #pragma unroll 1
     for (int u = 0; u < nunits; u += UB) {
 #pragma unroll
         for (int ub = 0; ub < UB; ++ub) {
             const int slot = ub & 1, sl = ub % SPT;
-            if (SPT > 1 || u + ub < nunits) {
+            const bool live = SPT > 1 || u + ub < nunits;   // wave-uniform
+            if (live) {
                 if (sl == 0) {
-                    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                    each([&](Grp& S, int) { S.acc = f32x4{0.f, 0.f, 0.f, 0.f}; });
                     xc = xq[slot];
                 }
+                // the groups' chains interleaved: independent MFMAs back to back
 #pragma unroll
                 for (int t = 0; t < SW; ++t)
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][t], bq[sl * SW + t], acc, 0, 0, 0);
-                load(slot, u + ub + 2);
-                if (sl == SPT - 1) {
-                    // lane holds rows 4g..4g+3 = candidates g, g+4, g+8, g+12 of the tile
-                    const int j0 = (h + KQ_HALVES * ((u + ub) / SPT)) * 16 + g;
-                    consider(acc[0], xc.x, j0);
-                    consider(acc[1], xc.y, j0 + 4);
-                    consider(acc[2], xc.z, j0 + 8);
-                    consider(acc[3], xc.w, j0 + 12);
-                    if (__any(cnt > KQ_QCAP - 4)) flush();
-                }
+                    each([&](Grp& S, int) {
+                        S.acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][t], S.bq[sl * SW + t], S.acc, 0, 0, 0);
+                    });
+            }
+            load(slot, u + ub + 2, (ub + 2) % SPT);
+            if (live && sl == SPT - 1) {
+                // lane holds rows 4g..4g+3 = candidates g, g+4, g+8, g+12 of the tile
+                const int j0 = (h + KQ_HALVES * ((u + ub) / SPT)) * 16 + g;
+                each([&](Grp& S, int) {
+                    consider(S, S.acc[0], xc.x, j0);
+                    consider(S, S.acc[1], xc.y, j0 + 4);
+                    consider(S, S.acc[2], xc.z, j0 + 8);
+                    consider(S, S.acc[3], xc.w, j0 + 12);
+                });
+                if (__any(cmax() > KQ_QCAP - 4)) flush();
             }
         }
     }
@@ -577,30 +709,31 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
 
     // Merge the wave's 4 lists of each query (lanes ql, ql+16, ql+32, ql+48)
     // by k rounds of a canonical arg-max over the 4 list heads; the winning
-    // lane pops its head. Rank r ends up in lane r % 4.
-    const float last = lv[KL - 1];
-    float ov[RPL];
-    int oj[RPL];
+    // lane pops its head. Rank r ends up in lane r % 4. The groups' merges are
+    // independent and interleaved.
+    each([&](Grp& S, int) { S.last = S.lv[KL - 1]; });
 #pragma unroll
     for (int r = 0; r < KB; ++r) {
         if (r < k) {
-            float hv = lv[0];
-            int hj = li[0];
-            float pv = __shfl_xor(hv, 16);
-            int pj = __shfl_xor(hj, 16);
-            if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
-            pv = __shfl_xor(hv, 32);
-            pj = __shfl_xor(hj, 32);
-            if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
-            const bool pop = li[0] == hj && lv[0] == hv;
+            each([&](Grp& S, int) {
+                float hv = S.lv[0];
+                int hj = S.li[0];
+                float pv = __shfl_xor(hv, 16);
+                int pj = __shfl_xor(hj, 16);
+                if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
+                pv = __shfl_xor(hv, 32);
+                pj = __shfl_xor(hj, 32);
+                if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
+                const bool pop = S.li[0] == hj && S.lv[0] == hv;
 #pragma unroll
-            for (int t = 0; t < KL - 1; ++t) {
-                lv[t] = pop ? lv[t + 1] : lv[t];
-                li[t] = pop ? li[t + 1] : li[t];
-            }
-            lv[KL - 1] = pop ? -INFINITY : lv[KL - 1];
-            li[KL - 1] = pop ? 0x7fffffff : li[KL - 1];
-            if ((r & 3) == g) { ov[r >> 2] = hv; oj[r >> 2] = hj; }
+                for (int t = 0; t < KL - 1; ++t) {
+                    S.lv[t] = pop ? S.lv[t + 1] : S.lv[t];
+                    S.li[t] = pop ? S.li[t + 1] : S.li[t];
+                }
+                S.lv[KL - 1] = pop ? -INFINITY : S.lv[KL - 1];
+                S.li[KL - 1] = pop ? 0x7fffffff : S.li[KL - 1];
+                if ((r & 3) == g) { S.ov[r >> 2] = hv; S.oj[r >> 2] = hj; }
+            });
         }
     }
 
@@ -609,64 +742,71 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     // other list that are canonically better (binary search). The halves hold
     // disjoint candidates, so the ranks 0..k-1 are taken exactly once.
     __syncthreads();  // every wave is done with its FIFO
-    float2* lists = reinterpret_cast<float2*>(smem);         // [KQ_HALVES][KQ_QPB][KB]
-    float* kth = smem + KQ_HALVES * KQ_QPB * KB * 2;         // [KQ_QPB] merged k-th value
-    int* flg = reinterpret_cast<int*>(kth + KQ_QPB);         // [KQ_QPB] row needs the fix-up
+    float2* lists = reinterpret_cast<float2*>(smem);         // [KQ_HALVES][QPB][KB]
+    float* kth = smem + KQ_HALVES * QPB * KB * 2;            // [QPB] merged k-th value
+    int* flg = reinterpret_cast<int*>(kth + QPB);            // [QPB] row needs the fix-up
+    each([&](Grp& S, int) {
 #pragma unroll
-    for (int t = 0; t < RPL; ++t) {
-        const int r = 4 * t + g;
-        if (r < k) lists[(h * KQ_QPB + qq) * KB + r] = make_float2(ov[t], __int_as_float(oj[t]));
-    }
-    if (tid < KQ_QPB) {
+        for (int t = 0; t < RPL; ++t) {
+            const int r = 4 * t + g;
+            if (r < k) lists[(h * QPB + S.qq) * KB + r] = make_float2(S.ov[t], __int_as_float(S.oj[t]));
+        }
+    });
+    if (tid < QPB) {
         kth[tid] = -INFINITY;
         flg[tid] = 0;
     }
     __syncthreads();
-    const float2* other = lists + ((1 - h) * KQ_QPB + qq) * KB;
-    int rk[RPL];
-#pragma unroll
-    for (int t = 0; t < RPL; ++t) {
-        const int r = 4 * t + g;
-        rk[t] = k;
-        if (r < k) {
-            int lo = 0, hi = k;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                const float2 o = other[mid];
-                if (canon_better(o.x, __float_as_int(o.y), ov[t], oj[t])) lo = mid + 1;
-                else hi = mid;
-            }
-            rk[t] = r + lo;
-            if (rk[t] == k - 1) kth[qq] = ov[t];
-        }
-    }
-    __syncthreads();
-    // A lane whose list was full and whose last kept value reaches the merged
-    // k-th may have dropped a member of the true top-k: mark the row for the
-    // exact fix-up pass.
-    const float kv = kth[qq];
-    if (last != -INFINITY && last >= kv) flg[qq] = 1;
-    // fewer than k candidates reached the seed (the merged k-th is then a -inf
-    // pad): only a seed that is not a value of this kernel's arithmetic does
-    // that; the exact fix-up from T0 = -inf repairs the row
-    if (!(kv >= tseed)) flg[qq] = 1;
-    __syncthreads();
-    if (q < N && flg[qq] == 0) {  // flagged rows are written by the fix-up below
-        const int64_t row = ((int64_t)b * N + q) * k;
+    each([&](Grp& S, int) {
+        const float2* other = lists + ((1 - h) * QPB + S.qq) * KB;
 #pragma unroll
         for (int t = 0; t < RPL; ++t) {
-            const int r = rk[t];
+            const int r = 4 * t + g;
+            S.rk[t] = k;
             if (r < k) {
-                if (idx64) idx64[row + r] = oj[t];
-                if (idx32) idx32[row + r] = oj[t];
-                if (vals) vals[row + r] = ov[t];
+                int lo = 0, hi = k;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    const float2 o = other[mid];
+                    if (canon_better(o.x, __float_as_int(o.y), S.ov[t], S.oj[t])) lo = mid + 1;
+                    else hi = mid;
+                }
+                S.rk[t] = r + lo;
+                if (S.rk[t] == k - 1) kth[S.qq] = S.ov[t];
             }
         }
-    }
+    });
+    __syncthreads();
+    each([&](Grp& S, int) {
+        // A lane whose list was full and whose last kept value reaches the merged
+        // k-th may have dropped a member of the true top-k: mark the row for the
+        // exact fix-up pass.
+        const float kv = kth[S.qq];
+        if (S.last != -INFINITY && S.last >= kv) flg[S.qq] = 1;
+        // fewer than k candidates reached the seed (the merged k-th is then a -inf
+        // pad): only a seed that is not a value of this kernel's arithmetic does
+        // that; the exact fix-up from T0 = -inf repairs the row
+        if (!(kv >= S.tseed)) flg[S.qq] = 1;
+    });
+    __syncthreads();
+    each([&](Grp& S, int) {
+        if (S.q < N && flg[S.qq] == 0) {  // flagged rows are written by the fix-up below
+            const int64_t row = ((int64_t)b * N + S.q) * k;
+#pragma unroll
+            for (int t = 0; t < RPL; ++t) {
+                const int r = S.rk[t];
+                if (r < k) {
+                    if (idx64) idx64[row + r] = S.oj[t];
+                    if (idx32) idx32[row + r] = S.oj[t];
+                    if (vals) vals[row + r] = S.ov[t];
+                }
+            }
+        }
+    });
 #ifdef DGX_KNN_STATS
     {   // diagnostics build only: per (block, wave) insertion rounds, flushes, flagged rows (vector stores)
         int nf = 0;
-        for (int f = 0; f < KQ_QPB; ++f) nf += (flg[f] != 0 && qb * KQ_QPB + f < N) ? 1 : 0;
+        for (int f = 0; f < QPB; ++f) nf += (flg[f] != 0 && qb * QPB + f < N) ? 1 : 0;
         if (lane == 0 && stats != nullptr) {
             uint32_t* st = stats + ((int64_t)blockIdx.x * KQ_WAVES + wave) * 4;
             st[0] = n_rounds; st[1] = n_flush; st[2] = wave == 0 ? (uint32_t)nf : 0u; st[3] = 1u;
@@ -674,9 +814,9 @@ __global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 4 : 2) void knn_kernel(const
     }
 #endif
     // the block's flagged rows (rare), one at a time; flg / kth are block-uniform LDS reads
-    float* fixa = smem + KQ_HALVES * KQ_QPB * KB * 2 + 2 * KQ_QPB;
-    for (int f = 0; f < KQ_QPB; ++f) {
-        const int qf = qb * KQ_QPB + f;
+    float* fixa = smem + KQ_HALVES * QPB * KB * 2 + 2 * QPB;
+    for (int f = 0; f < QPB; ++f) {
+        const int qf = qb * QPB + f;
         if (flg[f] != 0 && qf < N)
             knn_fix_row<NSTEP>(fixa, ib, xib, xx + (int64_t)b * N, N, k, qf, kth[f], (int64_t)b * N + qf, idx64,
                                idx32, vals);
@@ -868,12 +1008,18 @@ int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
+#ifndef KNN_QG
+#define KNN_QG 2
+#endif
 template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
                const float* seed, hipStream_t st) {
-    const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
-    hipLaunchKernelGGL((knn_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
+    // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
+    // the lists of two groups fit in registers); one where the selection does
+    constexpr int QG = (NSTEP >= 32 && KB <= 40) ? KNN_QG : 1;
+    const int nqb = (N + KQ_QPB * QG - 1) / (KQ_QPB * QG);
+    hipLaunchKernelGGL((knn_kernel<NSTEP, KB, QG>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
                        xximg, xx, B, N, k, nqb, idx64, idx32, vals, seed
 #ifdef DGX_KNN_STATS
                        , g_knn_stats
@@ -914,7 +1060,8 @@ const char* dgx_knn_kernel_name(int C, int k) {
             static const int NS[5] = {1, 3, 8, 16, 32};
             static const int KBS[5] = {16, 20, 32, 40, 64};
             for (int a = 0; a < 5; ++a)
-                for (int b = 0; b < 5; ++b) snprintf(s[a][b], sizeof(s[a][b]), "knn_kernel<%d, %d>", NS[a], KBS[b]);
+                for (int b = 0; b < 5; ++b) snprintf(s[a][b], sizeof(s[a][b]), "knn_kernel<%d, %d, %d>", NS[a], KBS[b],
+                         (NS[a] >= 32 && KBS[b] <= 40) ? KNN_QG : 1);
         }
     };
     static const Names names;  // thread-safe one-time initialisation

@@ -217,7 +217,7 @@ RATIO = 1.5
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("amp", [False, True])
-def test_net_cfg4_routed(cuda, amp):
+def test_net_cfg4_routed(cuda, amp, monkeypatch):
     """Net train step at cfg4 geometry against the reference's forward over
     stock fp64 modules (oracle.partseg.net_routed) on the same neighbours:
     every EdgeConv kNN / max slot / sign, the edge stage's kNN / conv2 slot /
@@ -232,6 +232,11 @@ def test_net_cfg4_routed(cuda, amp):
     from oracle.partseg import net_routed, stock_copy
     B, N, k, emb = 2, 2048, 40, 512
     args = types.SimpleNamespace(k=k, emb_dim=emb, n_heads=4, n_blocks=1, ff_dims=512, dropout=0.0, nclasses=50)
+    # deterministic MIOpen solvers for the stock layers of both runs, so the
+    # engine-vs-stock error ratio below is a property of the code, not of the
+    # solver each run happened to pick
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
     torch.manual_seed(17)
     net = Net(args)
     net64 = stock_copy(net).double().to(cuda).train()
@@ -308,6 +313,11 @@ def test_net_knn_computed_once(cuda, monkeypatch):
     import models.model_partseg as MP
     from dgx import ops, synth
     args = types.SimpleNamespace(k=20, emb_dim=64, n_heads=4, n_blocks=1, ff_dims=128, dropout=0.0, nclasses=50)
+    # the stock Conv1d layers of Net (grads_emb, head) run on MIOpen, whose
+    # weight-gradient solvers may accumulate in a run-dependent order: pin
+    # deterministic solvers so the comparison isolates the engine path
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
     torch.manual_seed(3)
     net = MP.Net(args).to(cuda).train()
     init = {n: t.clone() for n, t in net.state_dict().items()}
