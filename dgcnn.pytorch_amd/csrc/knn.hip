@@ -381,6 +381,16 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
     __syncthreads();  // the fix-up area is free for the next row
 }
 
+// Admission seeds of a selection launch: a per-row lower bound T of the k-th
+// value (dgx_knn_seed_f32), and/or candidate ids whose exact distances the
+// kernel computes itself (the previous EdgeConv block's graph) — min over ks
+// distinct candidates is a lower bound of the row's k-th value when ks >= k.
+struct KnnSeed {
+    const float* T;        // (B*N) or nullptr
+    const int32_t* sidx;   // (B, N, ks) local ids or nullptr
+    int ks;
+};
+
 // ------------------------------------------------------------ knn kernel ----
 // Block = KQ_GROUPS wave groups x 2 candidate halves, one wave each; a wave
 // serves QG groups of 16 queries (QG = 2: 32 queries per wave, 64 per block).
@@ -405,7 +415,7 @@ template <int NSTEP, int KB, int QG>
 __global__ __launch_bounds__(KQ_THREADS, QG == 1 ? (KB <= 40 ? 4 : 2) : (KB <= 40 ? 2 : 1))
 void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, const float* __restrict__ xx, int B,
                 int N, int k, int nqb, int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
-                float* __restrict__ vals, const float* __restrict__ seed
+                float* __restrict__ vals, const KnnSeed sd
 #ifdef DGX_KNN_STATS
                 , uint32_t* __restrict__ stats
 #endif
@@ -477,7 +487,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         // admission seed (dgx_knn_seed_f32): a lower bound of the row's k-th
         // value in this kernel's exact arithmetic, so candidates below it can
         // never enter the top-k; -inf without seeds
-        S.tseed = (seed != nullptr && S.q < N) ? seed[(int64_t)b * N + S.q] : -INFINITY;
+        S.tseed = (sd.T != nullptr && S.q < N) ? sd.T[(int64_t)b * N + S.q] : -INFINITY;
         S.thr = S.tseed;
 #pragma unroll
         for (int t = 0; t < KL; ++t) { S.lv[t] = -INFINITY; S.li[t] = 0x7fffffff; }
@@ -575,6 +585,72 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         const float T = fminf(tm, pub[(1 - h) * QPB + G0.qq]);
         if (G0.q < N) G0.tseed = fmaxf(G0.tseed, T);
         G0.thr = G0.tseed;
+    }
+    if constexpr (NSTEP % 4 == 0) {
+        if (sd.sidx != nullptr) {
+            // Graph seeds: the exact distances of ks given candidates (distinct
+            // ids, e.g. the previous block's neighbours) in this kernel's own
+            // arithmetic — the fmaf chain over c = 0..C-1 of x_j[c] * 2 x_q[c]
+            // that the MFMA chain computes (padded channels add exact zeros),
+            // then (dot - |x_j|^2) - |x_q|^2 — so T = their min is a lower bound
+            // of the row's k-th value (ks >= k). The query's 8 lanes (4 here x
+            // 2 halves) take seeds s = 4h + g, 4h + g + 8, ...
+            each([&](Grp& S, int) {
+                float tl = INFINITY;
+                const int qs = min(S.q, N - 1);
+                const int32_t* sj = sd.sidx + ((int64_t)b * N + qs) * sd.ks;
+                constexpr int SPL = 3;   // seeds per lane for ks <= 24
+                int jj[SPL];
+                float dot[SPL];
+#pragma unroll
+                for (int u = 0; u < SPL; ++u) {
+                    const int si = 4 * h + g + 8 * u;
+                    jj[u] = si < sd.ks ? min(max(sj[si], 0), N - 1) : -1;
+                    dot[u] = 0.f;
+                }
+                auto row = [&](int j, int kk) {   // lane-run kk (channels 4t + kk) of candidate j
+                    return ib + ((int64_t)(j >> 4) * 64 + 16 * kk + knn_row(j & 15)) * NSTEP;
+                };
+#pragma unroll 1
+                for (int t0 = 0; t0 < NSTEP; t0 += 4) {
+                    float xq4[4][4];
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const float4 v = *reinterpret_cast<const float4*>(row(qs, kk) + t0);
+                        xq4[kk][0] = 2.f * v.x; xq4[kk][1] = 2.f * v.y; xq4[kk][2] = 2.f * v.z; xq4[kk][3] = 2.f * v.w;
+                    }
+#pragma unroll
+                    for (int u = 0; u < SPL; ++u) {
+                        if (jj[u] < 0) continue;
+                        float xj4[4][4];
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) {
+                            const float4 v = *reinterpret_cast<const float4*>(row(jj[u], kk) + t0);
+                            xj4[kk][0] = v.x; xj4[kk][1] = v.y; xj4[kk][2] = v.z; xj4[kk][3] = v.w;
+                        }
+#pragma unroll
+                        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+                            for (int kk = 0; kk < 4; ++kk) dot[u] = fmaf(xj4[kk][tt], xq4[kk][tt], dot[u]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < SPL; ++u)
+                    if (jj[u] >= 0) tl = fminf(tl, (dot[u] - xx[(int64_t)b * N + jj[u]]) - S.xxq);
+                tl = fminf(tl, __shfl_xor(tl, 16));
+                tl = fminf(tl, __shfl_xor(tl, 32));
+                if (g == 0) pub[h * QPB + S.qq] = tl;
+            });
+            __syncthreads();
+            each([&](Grp& S, int) {
+                const float T = fminf(pub[h * QPB + S.qq], pub[(1 - h) * QPB + S.qq]);
+                if (S.q < N && T != INFINITY) S.tseed = fmaxf(S.tseed, T);
+                S.thr = S.tseed;
+            });
+            __syncthreads();
+            if (tid < KQ_HALVES * QPB) pub[tid] = -INFINITY;
+            __syncthreads();
+        }
     }
 #ifdef DGX_KNN_STATS
     uint32_t n_rounds = 0, n_flush = 0;
@@ -1014,7 +1090,7 @@ int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
 template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
-               const float* seed, hipStream_t st) {
+               KnnSeed seed, hipStream_t st) {
     // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
     // the lists of two groups fit in registers); one where the selection does
     constexpr int QG = (NSTEP >= 32 && KB <= 40) ? KNN_QG : 1;
@@ -1030,7 +1106,7 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
 
 template <int NSTEP>
 int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, const float* seed,
+               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, KnnSeed seed,
                hipStream_t st) {
 #define DGX_KNN_K(KBV) \
     return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st)
@@ -1114,9 +1190,12 @@ int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int 
     }
 }
 
-int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
-                              int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image,
-                              size_t image_bytes, const float* seed, void* stream) {
+}  // extern "C"
+
+namespace {
+int knn_select(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
+               int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes, KnnSeed seed,
+               void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
@@ -1134,12 +1213,31 @@ int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN
         default: return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
     }
 }
+}  // namespace
+
+extern "C" {
+
+int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
+                              int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image,
+                              size_t image_bytes, const float* seed, void* stream) {
+    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes,
+                      KnnSeed{seed, nullptr, 0}, stream);
+}
+
+int dgx_knn_select_graph_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B,
+                                    int C, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
+                                    const void* image, size_t image_bytes, const int32_t* seeds, int ks,
+                                    void* stream) {
+    if (!seeds || ks < k || ks > 24) return DGX_EINVAL;
+    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes,
+                      KnnSeed{nullptr, seeds, ks}, stream);
+}
 
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                        int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes,
                        void* stream) {
-    return dgx_knn_select_seeded_f32(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes, nullptr,
-                                     stream);
+    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes,
+                      KnnSeed{nullptr, nullptr, 0}, stream);
 }
 
 int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,

@@ -37,6 +37,8 @@ _SIGS = {
     "dgx_knn_select_seeded_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp,
                                   _vp],
     "dgx_knn_seed_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp],
+    "dgx_knn_select_graph_seeded_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz,
+                                        _vp, _i32, _vp],
     "dgx_knn_spatial_seed_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],

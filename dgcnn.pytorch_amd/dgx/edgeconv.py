@@ -22,6 +22,7 @@ torch.autocast the op runs in the engine's own precision on fp32 inputs
 (precision.no_autocast): its GEMMs never return autocast-reduced products.
 """
 import ctypes
+import os
 import threading
 
 import torch
@@ -35,11 +36,13 @@ from .ops import knn_raw, reduction_order
 _tls = threading.local()
 
 # blocks 2-4: seed each kNN's admission bound with the previous block's graph
-# (dgx_knn_seed_f32). Off: measured at cfg2 the selection kernels gain 18 / 18 /
-# 6 us (C = 64 / 64 / 128, they are bound by the operand stream, not the
-# lists) while the seed pass costs 3 x 58 us (profiles/r03e: a gather of 20
-# neighbour rows per query).
-KNN_SEEDS = False
+# (the selection kernel computes the seeds' distances itself,
+# dgx_knn_select_graph_seeded_f32). Off: measured at cfg2 the seeded selection
+# launches take 111 / 210 us (C = 64 / 128) against 90 / 139 us unseeded —
+# the per-lane gather of 3 seed rows costs more than the insertion rounds it
+# saves (a separate seed pass, dgx_knn_seed_f32: 87 -> 70 us selection plus
+# 58 us per block for the pass). DGX_KNN_SEEDS=1 turns it on (A/B only).
+KNN_SEEDS = os.environ.get("DGX_KNN_SEEDS", "0") == "1"
 
 
 def debug_capture():

@@ -90,7 +90,8 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
                 seed_log = getattr(_tls, "seed_timing", None)
                 if seed_log is not None:
                     seed_log.append((es0, es1))
-        if seeds is not None:
+        graph_seeded = seeds is not None and C > 12 and seeds.shape[-1] <= 24
+        if seeds is not None and not graph_seeded:
             if seeds.dtype != torch.int32 or not seeds.is_contiguous() or seeds.shape[:2] != (B, N) \
                     or not k <= seeds.shape[2] <= 64:
                 raise RuntimeError("knn seeds: int32 contiguous (B, N, ks) with k <= ks <= 64")
@@ -108,10 +109,21 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
         if timing is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        rc = L.dgx_knn_select_seeded_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
-                                         nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
-                                         nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
-                                         nat.f32(img), img_bytes, nat.f32(T), stream)
+        if graph_seeded:
+            # the selection kernel computes the seeds' distances itself (one launch)
+            if seeds.dtype != torch.int32 or not seeds.is_contiguous() or seeds.shape[:2] != (B, N) \
+                    or not k <= seeds.shape[2]:
+                raise RuntimeError("knn seeds: int32 contiguous (B, N, ks) with k <= ks")
+            rc = L.dgx_knn_select_graph_seeded_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
+                                                   nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
+                                                   nat.i32(idx) if out_dtype == torch.int32 else None,
+                                                   nat.f32(vals), nat.f32(img), img_bytes, nat.i32(seeds),
+                                                   seeds.shape[2], stream)
+        else:
+            rc = L.dgx_knn_select_seeded_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
+                                             nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
+                                             nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
+                                             nat.f32(img), img_bytes, nat.f32(T), stream)
         if timing is not None:
             ev1.record()
             timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))

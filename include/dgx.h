@@ -94,6 +94,17 @@ int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN
  * dgx_knn_prepare_f32). ks >= k makes T a lower bound of the k-th value. */
 int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                      const int32_t* seeds, int ks, float* T, void* stream);
+/* dgx_knn_select_f32 seeded by a candidate subset in ONE launch (reference
+ * dgcnn.py:88-98, blocks 2-4: the previous block's neighbours): the selection
+ * kernel computes the exact distances of the ks (k <= ks <= 24) local ids
+ * seeds[(b*N+q)*ks + s] itself (the arithmetic of dgx_knn_seed_f32) and
+ * admits only candidates at or above their min. The output equals
+ * dgx_knn_select_f32's for any seeds (a row short of k admitted candidates is
+ * recomputed exactly); seeds are ignored for C <= 12. */
+int dgx_knn_select_graph_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B,
+                                    int C, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
+                                    const void* image, size_t image_bytes, const int32_t* seeds, int ks,
+                                    void* stream);
 /* Spatial admission seeds for coordinate clouds (C <= 4, 256 <= N <= 4096,
  * k <= 64; reference dgcnn.py:6-12 on the xyz input of DGCNN block 1,
  * layers.py:45 and model_partseg.py:26): the cloud is ordered along a Morton
