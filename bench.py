@@ -425,7 +425,7 @@ def pmc_traffic(args, shapes):
     whose kernel names do not include every selection kernel this build
     launches for the step's layers is refused."""
     from dgx import _native as nat
-    names = [nat.lib().dgx_knn_kernel_name(c, args.k).decode() for c in shapes]
+    names = [nat.lib().dgx_knn_kernel_name(c, args.k, args.points).decode() for c in shapes]
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{args.config}.json")), reverse=True)
     if not files:
         return None, f"no profiles/*_pmc_{args.config}.json"

@@ -1084,16 +1084,22 @@ int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, in
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
-#ifndef KNN_QG
-#define KNN_QG 2
+#ifndef KNN_QG2_C64_MINN
+#define KNN_QG2_C64_MINN (1 << 30)
 #endif
-template <int NSTEP, int KB>
-int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-               int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
-               KnnSeed seed, hipStream_t st) {
-    // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
-    // the lists of two groups fit in registers); one where the selection does
-    constexpr int QG = (NSTEP >= 32 && KB <= 40) ? KNN_QG : 1;
+// query groups per wave: two where the MFMA chain dominates (C > 64; C = 64
+// only on large clouds), one where the selection does (k <= 40: two groups'
+// lists must fit in registers)
+inline int knn_qg(int nstep, int kb, int N) {
+    if (kb > 40) return 1;
+    if (nstep >= 32) return 2;
+    if (nstep == 16 && N >= KNN_QG2_C64_MINN) return 2;
+    return 1;
+}
+
+template <int NSTEP, int KB, int QG>
+int launch_knn_qg(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
+                  const float* img, const float* xximg, KnnSeed seed, hipStream_t st) {
     const int nqb = (N + KQ_QPB * QG - 1) / (KQ_QPB * QG);
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB, QG>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
                        xximg, xx, B, N, k, nqb, idx64, idx32, vals, seed
@@ -1102,6 +1108,19 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
 #endif
                        );
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+template <int NSTEP, int KB>
+int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
+               int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
+               KnnSeed seed, hipStream_t st) {
+    // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
+    // the lists of two groups fit in registers); one where the selection does
+    if constexpr (KB <= 40 && NSTEP >= 16) {
+        if (knn_qg(NSTEP, KB, N) == 2) return launch_knn_qg<NSTEP, KB, 2>(xx, B, N, k, idx64, idx32, vals, img, xximg,
+                                                                          seed, st);
+    }
+    return launch_knn_qg<NSTEP, KB, 1>(xx, B, N, k, idx64, idx32, vals, img, xximg, seed, st);
 }
 
 template <int NSTEP>
@@ -1128,24 +1147,26 @@ extern "C" {
 void dgx_knn_stats_buffer(void* dev) { g_knn_stats = static_cast<uint32_t*>(dev); }
 #endif
 
-const char* dgx_knn_kernel_name(int C, int k) {
-    // the selection kernel dgx_knn_select_f32 launches for (C, k), as profilers print it
+const char* dgx_knn_kernel_name(int C, int k, int N) {
+    // the selection kernel dgx_knn_select_f32 launches for (C, k, N), as profilers print it
     struct Names {
-        char s[5][5][32];
+        char s[5][5][2][40];
         Names() {
             static const int NS[5] = {1, 3, 8, 16, 32};
             static const int KBS[5] = {16, 20, 32, 40, 64};
             for (int a = 0; a < 5; ++a)
-                for (int b = 0; b < 5; ++b) snprintf(s[a][b], sizeof(s[a][b]), "knn_kernel<%d, %d, %d>", NS[a], KBS[b],
-                         (NS[a] >= 32 && KBS[b] <= 40) ? KNN_QG : 1);
+                for (int b = 0; b < 5; ++b)
+                    for (int q = 0; q < 2; ++q)
+                        snprintf(s[a][b][q], sizeof(s[a][b][q]), "knn_kernel<%d, %d, %d>", NS[a], KBS[b], q + 1);
         }
     };
     static const Names names;  // thread-safe one-time initialisation
-    if (C < 1 || C > 128 || k < 1 || k > 64) return "";
+    if (C < 1 || C > 128 || k < 1 || k > 64 || N < 1) return "";
     const int ns = knn_nstep(C);
     const int a = ns == 1 ? 0 : ns == 3 ? 1 : ns == 8 ? 2 : ns == 16 ? 3 : 4;
     const int b = k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4;
-    return names.s[a][b];
+    static const int KBS[5] = {16, 20, 32, 40, 64};
+    return names.s[a][b][knn_qg(ns, KBS[b], N) - 1];
 }
 
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,

@@ -65,10 +65,10 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
  * prepared image and its xx; vals (B,N,k), nullable, receives the selected pd
  * values (what pd.topk(k)[0] would hold). */
 size_t dgx_knn_image_bytes(int B, int C, int N);
-/* Name of the selection kernel dgx_knn_select_f32 launches for (C, k), as
+/* Name of the selection kernel dgx_knn_select_f32 launches for (C, k, N), as
  * rocprofv3 prints it (host-side query; lets profiles be matched to the
- * kernels that actually ran). "" for unsupported (C, k). */
-const char* dgx_knn_kernel_name(int C, int k);
+ * kernels that actually ran). "" for unsupported (C, k, N). */
+const char* dgx_knn_kernel_name(int C, int k, int N);
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                    int B, int C, int N, int order, float* xx, void* stream);
 int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,

@@ -18,8 +18,16 @@ f128 = torch.from_numpy(synth.relu_normal(4, (32, 128, 1024))).to(dev)
 p64 = f64.permute(0, 2, 1).contiguous().permute(0, 2, 1)
 p128 = f128.permute(0, 2, 1).contiguous().permute(0, 2, 1)
 x3b = torch.from_numpy(synth.cube_clouds(32, 2048, 1)).to(dev).permute(0, 2, 1)
-for name, x, k in (("C3", x3, 20), ("C3 N2048 k40", x3b, 40), ("C64", f64, 20), ("C128", f128, 20),
-                   ("C64pm", p64, 20), ("C128pm", p128, 20)):
+big = os.environ.get("KNN_BENCH_BIG") == "1"
+cases = [("C3", x3, 20), ("C3 N2048 k40", x3b, 40), ("C64", f64, 20), ("C128", f128, 20),
+         ("C64pm", p64, 20), ("C128pm", p128, 20)]
+if big:  # cfg3 / cfg5 layer shapes (point-major, as the concat buffer feeds them)
+    def pm(seed, shape):
+        f = torch.from_numpy(synth.relu_normal(seed, shape)).to(dev)
+        return f.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+    cases = [("C64 N2048 k40", pm(5, (32, 64, 2048)), 40), ("C128 N2048 k40", pm(6, (32, 128, 2048)), 40),
+             ("C64 N4096", pm(7, (24, 64, 4096)), 20), ("C128 N4096", pm(8, (24, 128, 4096)), 20)]
+for name, x, k in cases:
     for _ in range(3):
         knn_raw(x, k, out_dtype=torch.int32)
     torch.cuda.synchronize()
