@@ -181,12 +181,54 @@ __device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float
     }
 }
 
+// BN batch-statistics finalize folded into the gather launch (no separate
+// dgx_bn_finalize launch): each workgroup publishes its partial row with
+// write-through (sc1) stores, drains them, and draws a ticket from its channel
+// slice's counter; the slice's last arriver (ticket B*nparts-1) acquires,
+// reduces the slice's partial rows in one fixed order (fp64, independent of
+// which workgroup arrives last) and writes scale / shift / mean / invstd and
+// the running statistics (cdna_hip_programming.md Guideline 16, counter form).
+// The counters (one int per slice) are zero before the launch and the last
+// arriver resets its own, so they stay zero between launches.
+struct BnFwdFin {
+    int* counter;            // nullptr: partials only (separate finalize)
+    double count;
+    const float* gamma;
+    const float* beta;
+    float* rmean;
+    float* rvar;
+    double momentum;
+    double eps;
+    float* scale;
+    float* shift;
+    float* mean;
+    float* invstd;
+    int64_t* nbt;
+};
+
+__device__ __forceinline__ void bn_finalize_channel(const BnFwdFin& f, int o, double s1, double s2) {
+    const double mean = s1 / f.count;
+    double var = s2 / f.count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const double invstd = 1.0 / sqrt(var + f.eps);
+    const double a = (f.gamma ? (double)f.gamma[o] : 1.0) * invstd;
+    f.scale[o] = (float)a;
+    f.shift[o] = (float)((f.beta ? (double)f.beta[o] : 0.0) - mean * a);
+    if (f.mean) f.mean[o] = (float)mean;
+    if (f.invstd) f.invstd[o] = (float)invstd;
+    if (f.rmean) f.rmean[o] = (float)((1.0 - f.momentum) * (double)f.rmean[o] + f.momentum * mean);
+    if (f.rvar) {
+        const double unbiased = f.count > 1.0 ? var * f.count / (f.count - 1.0) : var;
+        f.rvar[o] = (float)((1.0 - f.momentum) * (double)f.rvar[o] + f.momentum * unbiased);
+    }
+}
+
 template <int CS, bool EVAL>
 __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int B, int N, int k, int Co, int nparts,
     const float* __restrict__ sel_sign, const float* __restrict__ shift, float slope, float* __restrict__ ysel,
     uint8_t* __restrict__ arg, float* __restrict__ sumP, float* __restrict__ partials, float* __restrict__ out,
-    int ldo) {
+    int ldo, BnFwdFin fin) {
     constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V;
     extern __shared__ float lds[];  // [N][CS] slice of P | idx rows of a pass; then the stat reduction
     int b, part, slice;
@@ -347,8 +389,77 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
             r1 += red[(2 * uc) * EC_THREADS + w];
             r2 += red[(2 * uc + 1) * EC_THREADS + w];
         }
-        partials[(int64_t)prow * 2 * Co + o0 + t] = r1;
-        partials[(int64_t)prow * 2 * Co + Co + o0 + t] = r2;
+        // write-through (sc1) stores: the slice's last arriver may sit on another XCD
+        __hip_atomic_store(&partials[(int64_t)prow * 2 * Co + o0 + t], r1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&partials[(int64_t)prow * 2 * Co + Co + o0 + t], r2, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!fin.counter) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
+    __syncthreads();
+    int* last_flag = reinterpret_cast<int*>(lds);
+    if (t == 0) {
+        const int ticket = __hip_atomic_fetch_add(&fin.counter[slice], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == B * nparts - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&fin.counter[slice], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        last_flag[0] = last;
+    }
+    __syncthreads();
+    if (!last_flag[0]) return;
+    // last arriver: rows g, g + G, ... of channel o0 + t % CS per thread (fp64), lanes with
+    // the same channel combined by xor shuffles, then the waves in order
+    {
+        constexpr int G = EC_THREADS / CS;
+        const int c = t % CS, g = t / CS, o = o0 + c;
+        const int R = B * nparts;
+        double s1 = 0.0, s2 = 0.0;
+        if (o < Co) {
+            const float* __restrict__ pp = partials + o;
+            int r = g;
+            for (; r + 3 * G < R; r += 4 * G) {
+                float v1[4], v2[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v1[u] = pp[(int64_t)(r + u * G) * 2 * Co];
+                    v2[u] = pp[(int64_t)(r + u * G) * 2 * Co + Co];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    s1 += (double)v1[u];
+                    s2 += (double)v2[u];
+                }
+            }
+            for (; r < R; r += G) {
+                s1 += (double)pp[(int64_t)r * 2 * Co];
+                s2 += (double)pp[(int64_t)r * 2 * Co + Co];
+            }
+        }
+#pragma unroll
+        for (int m = CS; m < 64; m <<= 1) {
+            s1 += __shfl_xor(s1, m);
+            s2 += __shfl_xor(s2, m);
+        }
+        double* wsum = reinterpret_cast<double*>(lds) + 2;   // [wave][2][CS] (after the flag)
+        const int lane = t & 63, wv = t >> 6;
+        if (lane < CS) {
+            wsum[(wv * 2) * CS + lane] = s1;
+            wsum[(wv * 2 + 1) * CS + lane] = s2;
+        }
+        __syncthreads();
+        if (t < CS && o0 + t < Co) {
+            double r1 = 0.0, r2 = 0.0;
+            for (int w = 0; w < EC_THREADS / 64; ++w) {
+                r1 += wsum[(w * 2) * CS + t];
+                r2 += wsum[(w * 2 + 1) * CS + t];
+            }
+            bn_finalize_channel(fin, o0 + t, r1, r2);
+            if (fin.nbt && slice == 0 && t == 0) *fin.nbt += 1;
+        }
     }
 }
 
@@ -454,7 +565,7 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
     const float* __restrict__ dY, int lddy, const float* __restrict__ ysel, int M, int Co,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
     const float* __restrict__ invstd, float slope, float* __restrict__ dz, float* __restrict__ partials,
-    int rows_per_blk) {
+    int rows_per_blk, const uint8_t* __restrict__ arg) {
     __shared__ float red[2][4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int o = blockIdx.y * 64 + lane;
@@ -468,11 +579,13 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
         constexpr int DZ_U = 4;
         for (int r0 = wave; r0 < rows_per_blk; r0 += 4 * DZ_U) {
             float yv[DZ_U], gv[DZ_U];
+            uint32_t sv[DZ_U];
 #pragma unroll
             for (int u = 0; u < DZ_U; ++u) {
                 const int64_t i = min(i0 + r0 + 4 * u, (int64_t)M - 1);
                 yv[u] = ysel[i * Co + o];
                 gv[u] = dY[i * lddy + o];
+                sv[u] = arg ? arg[i * Co + o] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < DZ_U; ++u) {
@@ -480,7 +593,9 @@ __global__ __launch_bounds__(256) void edge_bwd_dz_kernel(
                 if (r0 + 4 * u >= rows_per_blk || i >= M) break;
                 const float z = fmaf(a, yv[u], sh);
                 const float d = gv[u] * (z > 0.f ? 1.f : slope);
-                dz[i * Co + o] = d;
+                // packed form: the selected slot replaces the low 6 mantissa bits
+                // (18 significant bits left; the scatter reads one word per edge)
+                dz[i * Co + o] = arg ? __uint_as_float((__float_as_uint(d) & ~63u) | sv[u]) : d;
                 acc1 += d;
                 acc2 = fmaf(d, (yv[u] - mu) * is, acc2);
             }
@@ -759,21 +874,42 @@ __device__ __forceinline__ void lds_slots(const uint8_t* __restrict__ p, uint32_
     }
 }
 
-template <int CS, bool OUT16>
+// BN backward finalize folded into the scatter's prologue (no separate
+// dgx_bn_bwd_finalize launch): every workgroup reduces the dz kernel's partial
+// rows for its own CS channels in one fixed order (so all of a slice's
+// workgroups hold bit-identical c0 / c1), the slice's first workgroup writes
+// dgamma, dbeta, c0, c1. partials == nullptr: c0 / c1 are inputs.
+struct BnBwdFin {
+    const float* partials;   // (nrows, 2, Co): sum dz | sum dz*yhat
+    int nrows;
+    double count;
+    const float* mean;
+    const float* invstd;
+    int eval;                // running-statistics forward: c0 = c1 = 0
+    float* dgamma;
+    float* dbeta;
+    float* c0;
+    float* c1;
+};
+constexpr int BW_FIN_LDS = 16 * 2 * 8 * sizeof(double) + 2 * 8 * sizeof(float);   // per-wave sums | c0 c1
+
+template <int CS, bool OUT16, bool PACKED>
 __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
     const float* __restrict__ dz, const uint8_t* __restrict__ arg, const float* __restrict__ sumP, int B, int N,
     int k, int Co, int nparts, const float* __restrict__ scale, const float* __restrict__ c0,
-    const float* __restrict__ c1, void* __restrict__ dPQv) {
+    const float* __restrict__ c1, void* __restrict__ dPQv, BnBwdFin fin) {
     static_assert(CS == 1 || CS == 2 || CS == 4 || CS == 8 || CS == 16, "slice width");
     constexpr int SW = (CS + 3) / 4;  // slot words per row
     float* __restrict__ dPQ = static_cast<float*>(dPQv);
     __bf16* __restrict__ dPQh = static_cast<__bf16*>(dPQv);
-    extern __shared__ float lds[];  // [N][CS] Q | [N][CS] dz | [N][CS] u8 slot | order u16 [per] | buckets
+    // [N][CS] Q | [N][CS] dz | [N][CS] u8 slot (not PACKED) | order u16 [per] | buckets
+    // PACKED: dz words carry the slot in their low 6 bits (dgx_edge_bwd_dz_packed_f32)
+    extern __shared__ float lds[];
     float* qs = lds;
     float* ds = lds + N * CS;
     uint8_t* ss = reinterpret_cast<uint8_t*>(ds + N * CS);
-    uint16_t* order = reinterpret_cast<uint16_t*>(ss + ((N * CS + 15) & ~15));
+    uint16_t* order = reinterpret_cast<uint16_t*>(PACKED ? ss : ss + ((N * CS + 15) & ~15));
     int b, part, slice;
     if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
     const int o0 = slice * CS;
@@ -800,8 +936,9 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             lds_vec<CS>(arr + n * CS, r);
         }
     };
-    const uint8_t* __restrict__ ab = arg + base * Co + o0;
-    if (full && (Co % CS) == 0) {
+    const uint8_t* __restrict__ ab = PACKED ? nullptr : arg + base * Co + o0;
+    if (PACKED) {
+    } else if (full && (Co % CS) == 0) {
         for (int n = t; n < N; n += EC_THREADS) {
             uint32_t w[SW];
             if constexpr (CS == 16) {
@@ -851,12 +988,87 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
         order[atomicAdd(&bucket[BW_BUCKETS - 1 - min(deg, BW_BUCKETS - 1)], 1)] = (uint16_t)r;
     }
     float a[CS], k0[CS], k1[CS];
+    if (fin.partials) {
+        // thread t sums rows g, g + G, ... of channel o0 + t % CS (fp64), lanes of a
+        // wave with the same channel combine by xor shuffles, then the waves in order
+        static_assert(CS <= 8 && EC_THREADS / 64 <= 16, "finalize scratch");
+        double* wsum = reinterpret_cast<double*>(bucket + BW_BUCKETS);   // [wave][2][CS]
+        float* kc = reinterpret_cast<float*>(wsum + 16 * 2 * 8);        // [2][CS]
+        const int c = t % CS, g = t / CS;
+        constexpr int G = EC_THREADS / CS;
+        const int o = o0 + c;
+        double s1 = 0.0, s2 = 0.0;
+        if (o < Co) {
+            const float* __restrict__ pp = fin.partials + o;
+            int r = g;
+            for (; r + 3 * G < fin.nrows; r += 4 * G) {   // 8 independent loads in flight
+                float v1[4], v2[4];
 #pragma unroll
-    for (int u = 0; u < CS; ++u) {
-        const int o = min(o0 + u, Co - 1);
-        a[u] = scale[o];
-        k0[u] = c0[o];
-        k1[u] = c1[o];
+                for (int u = 0; u < 4; ++u) {
+                    v1[u] = pp[(int64_t)(r + u * G) * 2 * Co];
+                    v2[u] = pp[(int64_t)(r + u * G) * 2 * Co + Co];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    s1 += (double)v1[u];
+                    s2 += (double)v2[u];
+                }
+            }
+            for (; r < fin.nrows; r += G) {
+                s1 += (double)pp[(int64_t)r * 2 * Co];
+                s2 += (double)pp[(int64_t)r * 2 * Co + Co];
+            }
+        }
+#pragma unroll
+        for (int m = CS; m < 64; m <<= 1) {
+            s1 += __shfl_xor(s1, m);
+            s2 += __shfl_xor(s2, m);
+        }
+        const int lane = t & 63, wv = t >> 6;
+        if (lane < CS) {
+            wsum[(wv * 2) * CS + lane] = s1;
+            wsum[(wv * 2 + 1) * CS + lane] = s2;
+        }
+        __syncthreads();
+        if (t < CS) {
+            double r1 = 0.0, r2 = 0.0;
+            for (int w = 0; w < EC_THREADS / 64; ++w) {
+                r1 += wsum[(w * 2) * CS + t];
+                r2 += wsum[(w * 2 + 1) * CS + t];
+            }
+            float v0 = 0.f, v1 = 0.f;
+            if (o0 + t < Co) {
+                const double av = scale[o0 + t], mu = fin.mean[o0 + t], is = fin.invstd[o0 + t];
+                const double g1 = r1 / fin.count, g2 = r2 / fin.count;
+                if (!fin.eval) {
+                    v0 = (float)(av * (-g1 + g2 * mu * is));
+                    v1 = (float)(-av * g2 * is);
+                }
+                if (b == 0 && part == 0) {
+                    if (fin.dbeta) fin.dbeta[o0 + t] = (float)r1;
+                    if (fin.dgamma) fin.dgamma[o0 + t] = (float)r2;
+                    fin.c0[o0 + t] = v0;
+                    fin.c1[o0 + t] = v1;
+                }
+            }
+            kc[t] = v0;
+            kc[CS + t] = v1;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            a[u] = scale[min(o0 + u, Co - 1)];
+            k0[u] = kc[u];
+            k1[u] = kc[CS + u];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            const int o = min(o0 + u, Co - 1);
+            a[u] = scale[o];
+            k0[u] = c0[o];
+            k1[u] = c1[o];
+        }
     }
     const bool vec = full && (CS % 4) == 0 && (Co % 4) == 0 && (ldpq % 4) == 0;
     const float kf = (float)k;
@@ -884,15 +1096,23 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             const int il = (e >> 6) - ibase;
             const uint32_t slot = (uint32_t)(e & 63);
             float q[CS];
-            uint32_t w[SW];
             lds_row(qs, il, q);
-            lds_slots<CS>(ss + il * CS, w);
 #pragma unroll
             for (int u = 0; u < CS; ++u) sq[u] += q[u];
             float d[CS];
             lds_row(ds, il, d);
+            if constexpr (PACKED) {
 #pragma unroll
-            for (int u = 0; u < CS; ++u) sd[u] += ((w[u >> 2] >> (8 * (u & 3))) & 0xffu) == slot ? d[u] : 0.f;
+                for (int u = 0; u < CS; ++u) {
+                    const uint32_t wd = __float_as_uint(d[u]);
+                    sd[u] += (wd & 63u) == slot ? __uint_as_float(wd & ~63u) : 0.f;
+                }
+            } else {
+                uint32_t w[SW];
+                lds_slots<CS>(ss + il * CS, w);
+#pragma unroll
+                for (int u = 0; u < CS; ++u) sd[u] += ((w[u >> 2] >> (8 * (u & 3))) & 0xffu) == slot ? d[u] : 0.f;
+            }
         };
         // in-edge ids EB at a time, all loads issued before the first is used
         // (prefetching the next batch as well measured slower)
@@ -908,6 +1128,10 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
         float qn[CS], dn[CS];
         lds_row(qs, n, qn);
         lds_row(ds, n, dn);
+        if constexpr (PACKED) {
+#pragma unroll
+            for (int u = 0; u < CS; ++u) dn[u] = __uint_as_float(__float_as_uint(dn[u]) & ~63u);
+        }
         float dp[CS], dq[CS];
 #pragma unroll
         for (int u = 0; u < CS; ++u) {
@@ -936,11 +1160,12 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     }
 }
 
-// scatter LDS bytes for N points at CS channels (Q | dz | slot | order | buckets)
-inline size_t scatter_lds_bytes(int N, int cs, int parts) {
+// scatter LDS bytes for N points at CS channels (Q | dz | slot | order | buckets;
+// no slot array when the dz words carry the slots)
+inline size_t scatter_lds_bytes(int N, int cs, int parts, bool packed) {
     const int per = (N + parts - 1) / parts;
-    return (size_t)2 * N * cs * sizeof(float) + (((size_t)N * cs + 15) & ~(size_t)15) +
-           (size_t)((per + 7) & ~7) * sizeof(uint16_t) + BW_BUCKETS * sizeof(int);
+    return (size_t)2 * N * cs * sizeof(float) + (packed ? 0 : (((size_t)N * cs + 15) & ~(size_t)15)) +
+           (size_t)((per + 7) & ~7) * sizeof(uint16_t) + BW_BUCKETS * sizeof(int) + BW_FIN_LDS;
 }
 
 inline int grid_for(int64_t total, int block) {
@@ -968,11 +1193,11 @@ template <bool EVAL>
 int launch_gather(int cs, dim3 grid, size_t lds, hipStream_t st, const float* PQ, int ldpq, const int32_t* idx, int B,
                   int N,
                   int k, int Co, int nparts, const float* sel, const float* shift, float slope, float* ysel,
-                  uint8_t* arg, float* sumP, float* partials, float* out, int ldo) {
+                  uint8_t* arg, float* sumP, float* partials, float* out, int ldo, const BnFwdFin& fin = BnFwdFin{}) {
 #define DGX_GATHER_CASE(CSV)                                                                                      \
     case CSV:                                                                                                    \
         hipLaunchKernelGGL((edge_gather_lds_kernel<CSV, EVAL>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, idx, B, \
-                           N, k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo);             \
+                           N, k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo, fin);        \
         break;
     switch (cs) {
         DGX_GATHER_CASE(32)
@@ -1000,7 +1225,9 @@ inline GatherGeom gather_geom(int B, int N, int Co) {
     size_t stage = (size_t)N * g.cs * sizeof(float) + GF_ICAP * sizeof(int);
     const int v = g.cs >= 4 ? g.cs / 4 : 1;
     size_t red = (size_t)2 * v * EC_THREADS * sizeof(float);
+    const size_t fin = 16 + (size_t)(EC_THREADS / 64) * 2 * g.cs * sizeof(double);   // last-arriver scratch
     g.lds = stage > red ? stage : red;
+    if (g.lds < fin) g.lds = fin;
     return g;
 }
 
@@ -1024,6 +1251,29 @@ int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx, int B
     return launch_gather<false>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
                                 ldpq, idx, B, N, k, Co,
                                 g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials, nullptr, 0);
+}
+
+int dgx_edge_fwd_gather_counters(int B, int N, int Co) {
+    if (B < 1 || N < 1 || Co < 1) return DGX_EINVAL;
+    return gather_geom(B, N, Co).slices;
+}
+
+int dgx_edge_fwd_gather_bn_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int Co,
+                               const float* gamma, const float* beta, float* ysel, uint8_t* arg, float* sumP,
+                               float* partials, int nrows, int* counters, double count, float* running_mean,
+                               float* running_var, double momentum, double eps, float* scale, float* shift,
+                               float* mean, float* invstd, int64_t* num_batches_tracked, void* stream) {
+    if (!PQ || !idx || !gamma || !ysel || !arg || !sumP || !partials || !counters || !scale || !shift)
+        return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co || count <= 0.0) return DGX_EINVAL;
+    const GatherGeom g = gather_geom(B, N, Co);
+    if (nrows != B * g.parts) return DGX_EINVAL;
+    if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
+    const BnFwdFin fin{counters, count, gamma, beta, running_mean, running_var, momentum, eps,
+                       scale, shift, mean, invstd, num_batches_tracked};
+    return launch_gather<false>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
+                                ldpq, idx, B, N, k, Co, g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials,
+                                nullptr, 0, fin);
 }
 
 int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int Co,
@@ -1090,7 +1340,18 @@ int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel, int M, int
     if (M < 1 || Co < 1 || lddy < Co || nrows < 1) return DGX_EINVAL;
     const int rows = (M + nrows - 1) / nrows;
     hipLaunchKernelGGL(edge_bwd_dz_kernel, dim3(nrows, (Co + 63) / 64), dim3(256), 0, dgx_stream(stream), dY, lddy,
-                       ysel, M, Co, scale, shift, mean, invstd, slope, dz, partials, rows);
+                       ysel, M, Co, scale, shift, mean, invstd, slope, dz, partials, rows, nullptr);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_edge_bwd_dz_packed_f32(const float* dY, int lddy, const float* ysel, const uint8_t* arg, int M, int Co,
+                               const float* scale, const float* shift, const float* mean, const float* invstd,
+                               float slope, float* dz_packed, float* partials, int nrows, void* stream) {
+    if (!dY || !ysel || !arg || !scale || !shift || !mean || !invstd || !dz_packed || !partials) return DGX_EINVAL;
+    if (M < 1 || Co < 1 || lddy < Co || nrows < 1) return DGX_EINVAL;
+    const int rows = (M + nrows - 1) / nrows;
+    hipLaunchKernelGGL(edge_bwd_dz_kernel, dim3(nrows, (Co + 63) / 64), dim3(256), 0, dgx_stream(stream), dY, lddy,
+                       ysel, M, Co, scale, shift, mean, invstd, slope, dz_packed, partials, rows, arg);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
@@ -1163,33 +1424,41 @@ int dgx_graph_reverse(const int32_t* idx, int B, int N, int k, int32_t* rowptr, 
     return dgx_graph_reverse_multi(1, &idx, B, N, k, &rowptr, &edges, stream);
 }
 
-int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
-                             const float* dz, const uint8_t* arg, const float* sumP, int B, int N, int k, int Co,
-                             const float* scale, const float* c0, const float* c1, void* dPQ, int out_bf16,
-                             void* stream) {
-    if (!PQ || !rowptr || !edges || !dz || !arg || !sumP || !scale || !c0 || !c1 || !dPQ) return DGX_EINVAL;
+namespace {
+int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges, const float* dz,
+                   const uint8_t* arg, const float* sumP, int B, int N, int k, int Co, const float* scale,
+                   const float* c0, const float* c1, void* dPQ, int out_bf16, bool packed, void* stream,
+                   const BnBwdFin& fin = BnBwdFin{}) {
+    if (!PQ || !rowptr || !edges || !dz || (!packed && !arg) || !sumP || !scale || !c0 || !c1 || !dPQ)
+        return DGX_EINVAL;
+    if (fin.partials && (fin.nrows < 1 || fin.count <= 0.0 || !fin.mean || !fin.invstd)) return DGX_EINVAL;
     if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
     if (N > 65535) return DGX_EUNSUPPORTED;
-    int cs = 8;  // slice channels: 9 bytes per (point, channel) within BW_LDS_BYTES
+    // slice channels: 9 (8 packed) bytes per (point, channel) within BW_LDS_BYTES
     // (16 measured slower: one workgroup per CU; 4 slower: per-edge work over fewer channels)
-    while (cs > 1 && (size_t)9 * N * cs > (size_t)BW_LDS_BYTES) cs >>= 1;
-    if ((size_t)9 * N * cs > (size_t)BW_LDS_BYTES) return DGX_EUNSUPPORTED;
+    const size_t per_pc = packed ? 8 : 9;
+    int cs = 8;
+    while (cs > 1 && per_pc * N * cs > (size_t)BW_LDS_BYTES) cs >>= 1;
+    if (per_pc * N * cs > (size_t)BW_LDS_BYTES) return DGX_EUNSUPPORTED;
     const int slices = (Co + cs - 1) / cs;
     const int parts = point_parts(B, slices, N);
     const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
-    const size_t lds = scatter_lds_bytes(N, cs, parts);
+    const size_t lds = scatter_lds_bytes(N, cs, parts, packed);
     hipStream_t st = dgx_stream(stream);
-#define DGX_SCATTER_CASE(CSV)                                                                                  \
-    case CSV:                                                                                                 \
-        if (out_bf16)                                                                                         \
-            hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, true>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq,   \
-                               rowptr, edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);          \
-        else                                                                                                  \
-            hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, false>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq,  \
-                               rowptr, edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ);          \
+#define DGX_SCATTER_LAUNCH(CSV, O16, PK)                                                                      \
+    hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
+                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin)
+#define DGX_SCATTER_CASE(CSV)                                       \
+    case CSV:                                                      \
+        if (packed) {                                              \
+            if (out_bf16) DGX_SCATTER_LAUNCH(CSV, true, true);     \
+            else DGX_SCATTER_LAUNCH(CSV, false, true);             \
+        } else {                                                   \
+            if (out_bf16) DGX_SCATTER_LAUNCH(CSV, true, false);    \
+            else DGX_SCATTER_LAUNCH(CSV, false, false);            \
+        }                                                          \
         break;
     switch (cs) {
-        DGX_SCATTER_CASE(16)
         DGX_SCATTER_CASE(8)
         DGX_SCATTER_CASE(4)
         DGX_SCATTER_CASE(2)
@@ -1197,7 +1466,36 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, c
         default: return DGX_EUNSUPPORTED;
     }
 #undef DGX_SCATTER_CASE
+#undef DGX_SCATTER_LAUNCH
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+}  // namespace
+
+int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
+                             const float* dz, const uint8_t* arg, const float* sumP, int B, int N, int k, int Co,
+                             const float* scale, const float* c0, const float* c1, void* dPQ, int out_bf16,
+                             void* stream) {
+    return launch_scatter(PQ, ldpq, rowptr, edges, dz, arg, sumP, B, N, k, Co, scale, c0, c1, dPQ, out_bf16, false,
+                          stream);
+}
+
+int dgx_edge_bwd_scatter_fin_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
+                                 const float* dz, const uint8_t* arg, const float* sumP, int B, int N, int k, int Co,
+                                 const float* partials, int nrows, double count, const float* scale,
+                                 const float* mean, const float* invstd, int eval, float* dgamma, float* dbeta,
+                                 float* c0, float* c1, void* dPQ, int out_bf16, int packed, void* stream) {
+    if (!partials) return DGX_EINVAL;
+    const BnBwdFin fin{partials, nrows, count, mean, invstd, eval, dgamma, dbeta, c0, c1};
+    return launch_scatter(PQ, ldpq, rowptr, edges, dz, packed ? nullptr : arg, sumP, B, N, k, Co, scale, c0, c1, dPQ,
+                          out_bf16, packed != 0, stream, fin);
+}
+
+int dgx_edge_bwd_scatter_packed_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
+                                    const float* dz_packed, const float* sumP, int B, int N, int k, int Co,
+                                    const float* scale, const float* c0, const float* c1, void* dPQ, int out_bf16,
+                                    void* stream) {
+    return launch_scatter(PQ, ldpq, rowptr, edges, dz_packed, nullptr, sumP, B, N, k, Co, scale, c0, c1, dPQ,
+                          out_bf16, true, stream);
 }
 
 }  // extern "C"

@@ -44,6 +44,9 @@ _SIGS = {
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_edge_partials_rows": [_i32, _i32, _i32],
     "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dgx_edge_fwd_gather_counters": [_i32, _i32, _i32],
+    "dgx_edge_fwd_gather_bn_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                                   _f64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_bn_finalize_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -51,6 +54,7 @@ _SIGS = {
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
     "dgx_bn_lrelu_apply_f32": [_vp, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp],
     "dgx_edge_bwd_dz_f32": [_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
+    "dgx_edge_bwd_dz_packed_f32": [_vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_edge_bwd_dz_cm_rows": [_i32, _i32],
     "dgx_edge_bwd_dz_cm_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _i32, _vp],
     "dgx_bn_bwd_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
@@ -58,6 +62,10 @@ _SIGS = {
     "dgx_graph_reverse_multi": [_i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_edge_bwd_scatter_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
                                  _i32, _vp],
+    "dgx_edge_bwd_scatter_fin_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _i32, _f64,
+                                     _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp],
+    "dgx_edge_bwd_scatter_packed_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
+                                        _i32, _vp],
     "dgx_colstats_rows": [_i64],
     "dgx_colstats_f32": [_vp, _i32, _i64, _i32, _vp, _i32, _vp],
     "dgx_pointconv_apply_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],

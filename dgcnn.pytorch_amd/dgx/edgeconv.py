@@ -43,6 +43,18 @@ _tls = threading.local()
 # saves (a separate seed pass, dgx_knn_seed_f32: 87 -> 70 us selection plus
 # 58 us per block for the pass). DGX_KNN_SEEDS=1 turns it on (A/B only).
 KNN_SEEDS = os.environ.get("DGX_KNN_SEEDS", "0") == "1"
+# bf16 mode: the backward scatter reads packed dz|slot words (DGX_SCATTER_PACKED=0:
+# separate dz and slot arrays, A/B only; cfg2 step 1.4178 -> 1.4131 ms)
+SCATTER_PACKED = os.environ.get("DGX_SCATTER_PACKED", "1") == "1"
+# BN backward finalize folded into the scatter's prologue (DGX_FOLD_BN_BWD=0: a
+# separate finalize launch, A/B only; cfg2 step 1.4131 -> 1.4065 ms)
+FOLD_BN_BWD = os.environ.get("DGX_FOLD_BN_BWD", "1") == "1"
+# forward BN finalize inside the gather launch (last arriver per channel slice,
+# dgx_edge_fwd_gather_bn_f32). Off: measured at cfg2 (tools/ab_step.py --graph)
+# 1.4065 -> 1.4118 ms/step with it on — every workgroup's drain of its stores
+# before the ticket costs more than the finalize launch it removes.
+# DGX_FOLD_BN_FWD=1 turns it on (A/B only).
+FOLD_BN_FWD = os.environ.get("DGX_FOLD_BN_FWD", "0") == "1"
 
 
 def debug_capture():
@@ -105,6 +117,34 @@ def edge_select(PQ, idx, B, N, k, co, gamma, stream):
                                         nat.f32(ysel), nat.u8(arg), nat.f32(sumP), nat.f32(partials), prow, stream),
               "edge gather")
     return ysel, arg, sumP, partials, prow
+
+
+def edge_select_stats(PQ, idx, B, N, k, co, bn, gamma, beta, count, stream):
+    """edge_select + the BN batch-statistics finalize in one launch
+    (dgx_edge_fwd_gather_bn_f32). Returns (ysel, arg, sumP, Stats) or None when
+    the layer needs the separate path (SyncBatchNorm, no counters under capture)."""
+    L = nat.lib()
+    dev = PQ.device
+    if not FOLD_BN_FWD:
+        return None
+    fa = bn_.fused_finalize_args(bn, gamma, beta, co, count, dev)
+    if fa is None:
+        return None
+    ctr = bn_.launch_counters(dev, L.dgx_edge_fwd_gather_counters(B, N, co))
+    if ctr is None:
+        return None
+    args, st = fa
+    M = B * N
+    ysel = torch.empty((M, co), dtype=torch.float32, device=dev)
+    arg = torch.empty((M, co), dtype=torch.uint8, device=dev)
+    sumP = torch.empty((M, co), dtype=torch.float32, device=dev)
+    prow = L.dgx_edge_partials_rows(B, N, co)
+    partials = torch.empty((prow, 2, co), dtype=torch.float32, device=dev)
+    nat.check(L.dgx_edge_fwd_gather_bn_f32(nat.f32(PQ), PQ.stride(0), nat.i32(idx), B, N, k, co, nat.f32(gamma),
+                                           nat.f32(beta), nat.f32(ysel), nat.u8(arg), nat.f32(sumP),
+                                           nat.f32(partials), prow, nat.ptr(ctr, nat.I32), *args, stream),
+              "edge gather + bn finalize")
+    return ysel, arg, sumP, st
 
 
 class _EdgeConvStack(torch.autograd.Function):
@@ -171,12 +211,16 @@ class _EdgeConvStack(torch.autograd.Function):
             bn = ly.bn
             use_batch, _ = bn_.mode(bn)
             with torch.cuda.device(dev):
-                if use_batch or need_grad:
+                fused = edge_select_stats(PQ, idx, B, N, k, co, bn, gamma, beta, count, stream) if use_batch else None
+                if fused is not None:
+                    ysel, arg, sumP, st = fused
+                if fused is None and (use_batch or need_grad):
                     ysel, arg, sumP, partials, prow = edge_select(PQ, idx, B, N, k, co, gamma, stream)
                     if use_batch:
                         st = bn_.batch_stats(partials, prow, count, bn, gamma, beta, stream)
                     else:  # running statistics, output differentiated: keep the selection
                         st = bn_.running_stats(bn, gamma, beta, stream)
+                if use_batch or need_grad:
                     out16 = xcat16[:, off:off + co] if bf16 else None
                     nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, co, nat.f32(st.scale), nat.f32(st.shift),
                                                        float(ly.slope), nat.f32(out), total, nat.ptr(out16, nat.BF16),
@@ -265,15 +309,38 @@ class _EdgeConvStack(torch.autograd.Function):
             # dPQ only feeds the GEMMs: bf16 (what the GEMM would round it to) in bf16 mode
             dPQ = torch.empty((M, 2 * co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
             with torch.cuda.device(dev):
-                nat.check(L.dgx_edge_bwd_dz_f32(
-                    nat.f32(dY), ldy, nat.f32(ysel), M, co, nat.f32(st.scale), nat.f32(st.shift),
-                    nat.f32(st.mean), nat.f32(st.invstd), float(ly.slope), nat.f32(dz), nat.f32(partials), nblk,
-                    stream), "edge bwd dz")
-                dgamma, dbeta, c0, c1 = bn_.backward_consts(partials, nblk, count, st, stream)
-                nat.check(L.dgx_edge_bwd_scatter_f32(
-                    nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.u8(arg), nat.f32(sumP), B, N, k,
-                    co, nat.f32(st.scale), nat.f32(c0), nat.f32(c1), nat.ptr(dPQ, nat.F32, nat.BF16), int(bf16),
-                    stream), "edge bwd scatter")
+                bn_args = (M, co, nat.f32(st.scale), nat.f32(st.shift), nat.f32(st.mean), nat.f32(st.invstd),
+                           float(ly.slope), nat.f32(dz), nat.f32(partials), nblk, stream)
+                packed = bf16 and SCATTER_PACKED
+                if packed:
+                    # dz words carry the selected slot in their 6 low mantissa bits (the
+                    # dPQ they feed is rounded to bf16): one LDS word per in-edge-channel
+                    nat.check(L.dgx_edge_bwd_dz_packed_f32(nat.f32(dY), ldy, nat.f32(ysel), nat.u8(arg), *bn_args),
+                              "edge bwd dz")
+                else:
+                    nat.check(L.dgx_edge_bwd_dz_f32(nat.f32(dY), ldy, nat.f32(ysel), *bn_args), "edge bwd dz")
+                fold = st.group is None and FOLD_BN_BWD
+                if fold:
+                    # BN backward finalize in the scatter's prologue (one launch)
+                    dgamma, dbeta, c0, c1 = (torch.empty(co, dtype=torch.float32, device=dev) for _ in range(4))
+                    nat.check(L.dgx_edge_bwd_scatter_fin_f32(
+                        nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz),
+                        None if packed else nat.u8(arg), nat.f32(sumP), B, N, k, co, nat.f32(partials), nblk,
+                        count, nat.f32(st.scale), nat.f32(st.mean), nat.f32(st.invstd), int(st.eval),
+                        nat.f32(dgamma), nat.f32(dbeta), nat.f32(c0), nat.f32(c1), nat.ptr(dPQ, nat.F32, nat.BF16),
+                        int(bf16), int(packed), stream), "edge bwd scatter")
+                else:   # SyncBatchNorm: the all-reduce sits between the partials and the finalize
+                    dgamma, dbeta, c0, c1 = bn_.backward_consts(partials, nblk, count, st, stream)
+                common = (B, N, k, co, nat.f32(st.scale), nat.f32(c0), nat.f32(c1), nat.ptr(dPQ, nat.F32, nat.BF16),
+                          int(bf16), stream)
+                if not fold and packed:
+                    nat.check(L.dgx_edge_bwd_scatter_packed_f32(
+                        nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.f32(sumP),
+                        *common), "edge bwd scatter")
+                elif not fold:
+                    nat.check(L.dgx_edge_bwd_scatter_f32(
+                        nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.u8(arg),
+                        nat.f32(sumP), *common), "edge bwd scatter")
             if dbg is not None:
                 dbg[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
                            "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.float(), "partials": partials.clone(),

@@ -150,6 +150,20 @@ int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx,
                             int B, int N, int k, int Co, const float* gamma,
                             float* ysel, uint8_t* arg, float* sumP,
                             float* partials, int nrows, void* stream);
+/* dgx_edge_fwd_gather_f32 + dgx_bn_finalize_f32 in ONE launch: the last
+ * workgroup of each channel slice reduces the slice's partial rows (fp64, fixed
+ * order) and writes scale / shift / mean / invstd and the running statistics.
+ * counters: dgx_edge_fwd_gather_counters(B, N, Co) ints, ZERO before the first
+ * call; each launch leaves them zero again. Concurrent launches (other streams)
+ * need their own counters. */
+int dgx_edge_fwd_gather_counters(int B, int N, int Co);
+int dgx_edge_fwd_gather_bn_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N,
+                               int k, int Co, const float* gamma, const float* beta,
+                               float* ysel, uint8_t* arg, float* sumP, float* partials,
+                               int nrows, int* counters, double count,
+                               float* running_mean, float* running_var, double momentum,
+                               double eps, float* scale, float* shift, float* mean,
+                               float* invstd, int64_t* num_batches_tracked, void* stream);
 int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         const float* gamma, const float* beta,
                         float* running_mean, float* running_var,
@@ -194,6 +208,17 @@ int dgx_edge_bwd_dz_f32(const float* dY, int lddy, const float* ysel,
                         const float* shift, const float* mean,
                         const float* invstd, float slope, float* dz,
                         float* partials, int nrows, void* stream);
+/* dgx_edge_bwd_dz_f32 with the forward's selected slot (arg, M x Co u8) packed
+ * into each dz word's low 6 mantissa bits (18 significant bits of dz left):
+ * the input of dgx_edge_bwd_scatter_packed_f32, which then reads one LDS word
+ * per in-edge and channel instead of a dz word plus a slot byte. Used by the
+ * bf16 precision mode (its dPQ is rounded to bf16 afterwards); the fp32 parity
+ * mode keeps exact dz. Partials are from the unpacked dz. */
+int dgx_edge_bwd_dz_packed_f32(const float* dY, int lddy, const float* ysel,
+                               const uint8_t* arg, int M, int Co, const float* scale,
+                               const float* shift, const float* mean, const float* invstd,
+                               float slope, float* dz_packed, float* partials, int nrows,
+                               void* stream);
 /* dgx_edge_bwd_dz_f32 for a channel-major dY (B x Co x N, the layout of the
  * gradient of a (B, C, N) module output): same dz (M x Co, point-major) and
  * partials, nrows = dgx_edge_bwd_dz_cm_rows(B, N). */
@@ -223,6 +248,24 @@ int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
                              int k, int Co, const float* scale, const float* c0,
                              const float* c1, void* dPQ, int out_bf16,
                              void* stream);
+/* dgx_bn_bwd_finalize_f32 + dgx_edge_bwd_scatter_f32 in ONE launch: every
+ * workgroup reduces the dz pass's partial rows (nrows x 2 x Co) for its own
+ * channels in a fixed order (fp64) and the channel slice's first workgroup
+ * writes dgamma, dbeta (not accumulated), c0, c1 (c0 = c1 = 0 when eval != 0).
+ * packed != 0: dz holds dgx_edge_bwd_dz_packed_f32 words (arg unused). */
+int dgx_edge_bwd_scatter_fin_f32(const float* PQ, int ldpq, const int32_t* rowptr,
+                                 const int32_t* edges, const float* dz, const uint8_t* arg,
+                                 const float* sumP, int B, int N, int k, int Co,
+                                 const float* partials, int nrows, double count,
+                                 const float* scale, const float* mean, const float* invstd,
+                                 int eval, float* dgamma, float* dbeta, float* c0, float* c1,
+                                 void* dPQ, int out_bf16, int packed, void* stream);
+/* The same dPQ from packed dz|slot words (dgx_edge_bwd_dz_packed_f32). */
+int dgx_edge_bwd_scatter_packed_f32(const float* PQ, int ldpq, const int32_t* rowptr,
+                                    const int32_t* edges, const float* dz_packed,
+                                    const float* sumP, int B, int N, int k, int Co,
+                                    const float* scale, const float* c0, const float* c1,
+                                    void* dPQ, int out_bf16, void* stream);
 
 /* ---- a4: pointwise Conv1x1 + BatchNorm + LeakyReLU, replaces conv5 of
  * models/dgcnn.py:74-78, 100-102 (cat(x1..x4) -> Conv2d(512,emb,1) -> BN ->

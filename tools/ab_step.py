@@ -14,7 +14,20 @@ for p in (REPO, os.path.join(REPO, "dgcnn.pytorch_amd")):
     sys.path.insert(0, p)
 
 
-def apply(spec):
+_DEFAULTS = {}
+
+
+def apply(spec, all_specs=()):
+    """Set the variant's switches; every switch named by any variant is first
+    reset to its shipped value (so "" really is the shipped configuration)."""
+    for sp in all_specs:
+        for item in filter(None, sp.split(",")):
+            mod, rest = item.split(":")
+            attr = rest.split("=")[0]
+            m = importlib.import_module(mod)
+            _DEFAULTS.setdefault((mod, attr), getattr(m, attr))
+    for (mod, attr), val in _DEFAULTS.items():
+        setattr(importlib.import_module(mod), attr, val)
     for item in filter(None, spec.split(",")):
         mod, rest = item.split(":")
         attr, val = rest.split("=")
@@ -52,7 +65,7 @@ def main():
     res = {v: [] for v in a.variants}
     runs = {}
     for v in a.variants:  # warm every variant (and capture its graph)
-        apply(v)
+        apply(v, a.variants)
         for _ in range(5):
             step()
         runs[v] = step
@@ -70,7 +83,7 @@ def main():
             runs[v] = g.replay
     for r in range(a.rounds):
         for v in a.variants:
-            apply(v)
+            apply(v, a.variants)
             step = runs[v]
             step()
             torch.cuda.synchronize()
