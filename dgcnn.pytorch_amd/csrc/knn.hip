@@ -36,6 +36,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
+// knn3_kernel (VALU 3-channel selection) off by default: measured against the
+// MFMA selection kernel (tools/knn3_ab.py, identical outputs) at 53.8 vs 53.4 us
+// (B 32 N 1024 k 20), 235 vs 185 us (N 2048 k 40), 145 vs 127 us (N 2048 k 20);
+// PMC at cfg2: 16.9 M VALU instructions per launch (old 24.7 M) but 57 % VALU
+// issue — pass 1's v_med3 lists and ~38 insertion rounds per wave dominate.
+bool g_knn3_enabled = false;                     // dgx_knn_set_variant (A/B tools only)
 constexpr int KQ_GROUPS = 2;                    // query groups of 16 per block
 constexpr int KQ_HALVES = 2;                    // candidate halves: waves per query group
 constexpr int KQ_WAVES = KQ_GROUPS * KQ_HALVES;
@@ -1074,6 +1080,260 @@ uint32_t* g_knn_stats = nullptr;   // diagnostics build: device buffer set by dg
 inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
 inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
 
+// ------------------------------------------------ 3-channel selection ----
+// knn3_kernel<KB>: clouds of C <= 4 channels (the xyz kNN of DGCNN's first
+// block, PositionEmbedding and compute_hog_1x1), N <= K3_MAXN. No MFMA: a
+// 3-term dot is three packed-fp32 VALU ops per two candidates, cheaper than
+// feeding a 16x16x4 MFMA and dealing its outputs over 8 lists per query.
+// Lane = query (64 queries per block); wave w of K3_W = 8 = candidate part w
+// (tiles s = w, w+8, ... of 16 candidates: ascending order inside a wave, so a
+// strict '>' keeps canonical tie order).
+//   stage   the cloud's candidates from the operand image into LDS as pairs
+//           {x0 x0' x1 x1'} {x2 x2' xx xx'} (one ds_read_b128 pair feeds packed
+//           math for two candidates); pad candidates get xx = +inf (v = -inf).
+//   pass 1  values only: each lane keeps the M1 = ceil(KB/8) best values of its
+//           part (one v_med3 per slot); T = min over the 8 parts of the M1-th
+//           value is a lower bound of the row's k-th value (the eight lists hold
+//           8*M1 >= k distinct candidates reaching T).
+//   pass 2  the same distances again; v >= T (then v > the list's tail) puts
+//           the candidate id in a per-lane LDS FIFO, drained in insertion rounds
+//           into a sorted register list of KB slots. A part's list keeps its
+//           whole top-KB, so no row can overflow (no fix-up pass).
+//   merge   the 8 part lists through LDS, wave 0: k steps of a canonical
+//           8-way merge per lane.
+// Distances are the MFMA chain's values: d = fmaf(a2, 2q2, fmaf(a1, 2q1,
+// a0 * 2q0)) (the padded 4th channel adds an exact 0), v = (d - xx_j) - xx_q.
+constexpr int K3_MAXN = 4096;
+// candidate parts = waves per block: 8 for k <= 20 (more waves in flight, a
+// shorter pass-1 list), 4 above (the merge holds W x KB list slots in LDS)
+template <int KB>
+constexpr int knn3_w() { return 4; }
+constexpr int K3_QCAP = 24;   // per-lane FIFO slots (drained when any lane passes QCAP - 16)
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int KB>
+constexpr size_t knn3_lds_bytes(int N) {
+    constexpr int K3_W = knn3_w<KB>();
+    const size_t ntile = (size_t)(N + 15) / 16;
+    const size_t stream = ntile * 8 * 32 + K3_W * K3_QCAP * 64 * 4 + K3_W * 64 * 4;
+    const size_t merge = (size_t)K3_W * KB * 64 * 6;   // values | u16 ids
+    return stream > merge ? stream : merge;
+}
+
+__device__ __forceinline__ float knn3_prev_float(float t) {   // largest float below t (-inf stays)
+    if (t == -INFINITY) return t;
+    if (t == 0.f) return -__uint_as_float(1u);
+    const uint32_t u = __float_as_uint(t);
+    return t > 0.f ? __uint_as_float(u - 1u) : __uint_as_float(u + 1u);
+}
+
+template <int KB>
+__global__ __launch_bounds__(64 * knn3_w<KB>()) void knn3_kernel(const float* __restrict__ img,
+                                                         const float* __restrict__ xximg,
+                                                         const float* __restrict__ xx, int B, int N, int k, int nqb,
+                                                         int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
+                                                         float* __restrict__ vals) {
+#pragma clang fp contract(off)
+    constexpr int K3_W = knn3_w<KB>(), K3_THREADS = 64 * K3_W;
+    constexpr int M1 = (KB + K3_W - 1) / K3_W;
+    extern __shared__ float4 k3s[];
+    int b, qb;
+    if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ntile = (N + 15) >> 4;
+    float4* cp = k3s;                                                          // [ntile*8 pairs][2]
+    int* fj = reinterpret_cast<int*>(k3s + ntile * 16);                        // [W][QCAP][64]
+    float* tw = reinterpret_cast<float*>(fj + K3_W * K3_QCAP * 64);           // [W][64]
+    // stage: candidate j = 16 s + c sits at image row knn_row(c) of tile s
+    const float* __restrict__ ib = img + (int64_t)b * ntile * 64;
+    const float* __restrict__ xb = xximg + (int64_t)b * ntile * 16;
+    float* cpf = reinterpret_cast<float*>(cp);
+    for (int j0 = 0; j0 < ntile * 16; j0 += 4 * K3_THREADS) {   // 16 loads in flight per thread
+        float a[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * K3_THREADS + tid;
+            const int st = j >> 4, i = knn_row(j & 15);
+            const bool ok = j < N;
+            a[u][0] = ok ? ib[st * 64 + i] : 0.f;
+            a[u][1] = ok ? ib[st * 64 + 16 + i] : 0.f;
+            a[u][2] = ok ? ib[st * 64 + 32 + i] : 0.f;
+            a[u][3] = ok ? xb[st * 16 + i] : INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * K3_THREADS + tid;
+            if (j < ntile * 16) {
+                const int p = j >> 1, h = j & 1;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) cpf[p * 8 + 2 * c + h] = a[u][c];
+            }
+        }
+    }
+    __syncthreads();
+    const int q = min(qb * 64 + lane, N - 1);
+    const bool live = qb * 64 + lane < N;
+    f32x2 q0, q1, q2, qq;
+    {
+        const float4 u = cp[(q >> 1) * 2], v = cp[(q >> 1) * 2 + 1];
+        const int h = q & 1;
+        const float x0 = h ? u.y : u.x, x1 = h ? u.w : u.z, x2 = h ? v.y : v.x;
+        q0 = 2.0f * x0;
+        q1 = 2.0f * x1;
+        q2 = 2.0f * x2;
+        qq = xx[(int64_t)b * N + q];
+    }
+    auto dist = [&](int p) -> f32x2 {
+        const float4 u = cp[2 * p], v = cp[2 * p + 1];
+        const f32x2 a0 = {u.x, u.y}, a1 = {u.z, u.w}, a2 = {v.x, v.y}, w = {v.z, v.w};
+        const f32x2 d = __builtin_elementwise_fma(a2, q2, __builtin_elementwise_fma(a1, q1, a0 * q0));
+        return (d - w) - qq;
+    };
+    // pass 1: the M1 best values of this quarter
+    float L[M1];
+#pragma unroll
+    for (int m = 0; m < M1; ++m) L[m] = -INFINITY;
+    auto med_insert = [&](float nv) {
+#pragma unroll
+        for (int m = M1 - 1; m > 0; --m) L[m] = __builtin_amdgcn_fmed3f(L[m - 1], L[m], nv);
+        L[0] = fmaxf(L[0], nv);
+    };
+    for (int st = wave; st < ntile; st += K3_W) {
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp) {
+            const f32x2 v = dist(st * 8 + pp);
+            med_insert(v.x);
+            med_insert(v.y);
+        }
+    }
+    tw[wave * 64 + lane] = L[M1 - 1];
+    __syncthreads();
+    float T = tw[lane];
+#pragma unroll
+    for (int w = 1; w < K3_W; ++w) T = fminf(T, tw[w * 64 + lane]);
+    // pass 2: admissions v >= T into the FIFO, insertion rounds into the list
+    float lv[KB];
+    int li[KB];
+#pragma unroll
+    for (int m = 0; m < KB; ++m) {
+        lv[m] = -INFINITY;
+        li[m] = 0x7fffffff;
+    }
+    float thr = knn3_prev_float(T);
+    int cnt = 0;
+    int* __restrict__ myf = fj + wave * K3_QCAP * 64 + lane;
+    auto drain = [&]() {
+        for (int r = 0; __any(r < cnt); ++r) {
+            float nv = -INFINITY;
+            int nj = 0x7fffffff;
+            if (r < cnt) {
+                nj = myf[r * 64];
+                const float4 u = cp[2 * (nj >> 1)], v = cp[2 * (nj >> 1) + 1];
+                const int h = nj & 1;
+                const float a0 = h ? u.y : u.x, a1 = h ? u.w : u.z, a2 = h ? v.y : v.x, w = h ? v.w : v.z;
+                const float d = fmaf(a2, q2.x, fmaf(a1, q1.x, a0 * q0.x));
+                nv = (d - w) - qq.x;
+            }
+            list_insert_ordered<KB>(lv, li, nv, nj);
+        }
+        cnt = 0;
+        thr = fmaxf(thr, lv[KB - 1]);
+    };
+    for (int st = wave; st < ntile; st += K3_W) {
+        // the tile's candidate reads all issued before the first FIFO store (the
+        // compiler may not move LDS reads across those stores)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {   // half tiles: 4 pairs of operands in registers
+        float4 U[4], V[4];
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            U[pp] = cp[2 * (st * 8 + 4 * hh + pp)];
+            V[pp] = cp[2 * (st * 8 + 4 * hh + pp) + 1];
+        }
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            const int p = st * 8 + 4 * hh + pp;
+            const f32x2 a0 = {U[pp].x, U[pp].y}, a1 = {U[pp].z, U[pp].w}, a2 = {V[pp].x, V[pp].y};
+            const f32x2 w = {V[pp].z, V[pp].w};
+            const f32x2 d = __builtin_elementwise_fma(a2, q2, __builtin_elementwise_fma(a1, q1, a0 * q0));
+            const f32x2 v = (d - w) - qq;
+            if (v.x > thr) { myf[cnt * 64] = 2 * p; ++cnt; }
+            if (v.y > thr) { myf[cnt * 64] = 2 * p + 1; ++cnt; }
+        }
+        }
+        if (__any(cnt > K3_QCAP - 16)) drain();
+    }
+    drain();
+    // merge the 4 quarter lists (canonical order) in wave 0
+    __syncthreads();   // every wave is done with the candidates and its FIFO
+    float* lvv = reinterpret_cast<float*>(k3s);                          // [W][KB][64] values
+    uint16_t* lvi = reinterpret_cast<uint16_t*>(lvv + K3_W * KB * 64);   // [W][KB][64] ids (N <= 4096)
+#pragma unroll
+    for (int m = 0; m < KB; ++m) {
+        lvv[(wave * KB + m) * 64 + lane] = lv[m];
+        lvi[(wave * KB + m) * 64 + lane] = (uint16_t)min(li[m], 0xffff);
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    int pos[K3_W];
+    float2 hd[K3_W];
+#pragma unroll
+    for (int w = 0; w < K3_W; ++w) {
+        pos[w] = 0;
+        hd[w] = make_float2(lvv[(w * KB) * 64 + lane], __int_as_float((int)lvi[(w * KB) * 64 + lane]));
+    }
+    const int64_t row = ((int64_t)b * N + qb * 64 + lane) * k;
+    for (int r = 0; r < k; ++r) {
+        int bw = 0;
+        float bv = hd[0].x;
+        int bj = __float_as_int(hd[0].y);
+#pragma unroll
+        for (int w = 1; w < K3_W; ++w) {
+            const float v = hd[w].x;
+            const int j = __float_as_int(hd[w].y);
+            if (canon_better(v, j, bv, bj)) { bv = v; bj = j; bw = w; }
+        }
+        if (live) {
+            if (idx64) idx64[row + r] = bj;
+            if (idx32) idx32[row + r] = bj;
+            if (vals) vals[row + r] = bv;
+        }
+#pragma unroll
+        for (int w = 0; w < K3_W; ++w) {
+            if (w == bw) {
+                ++pos[w];
+                hd[w] = pos[w] < KB ? make_float2(lvv[(w * KB + pos[w]) * 64 + lane],
+                                                  __int_as_float((int)lvi[(w * KB + pos[w]) * 64 + lane]))
+                                    : make_float2(-INFINITY, __int_as_float(0xffff));
+            }
+        }
+    }
+}
+
+template <int KB>
+int launch_knn3(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img,
+                const float* xximg, hipStream_t st) {
+    const int nqb = (N + 63) / 64;
+    const size_t lds = knn3_lds_bytes<KB>(N);
+    hipLaunchKernelGGL((knn3_kernel<KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(64 * knn3_w<KB>()), lds, st, img, xximg, xx,
+                       B, N, k, nqb, idx64, idx32, vals);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dispatch_knn3(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
+                  const float* img, const float* xximg, hipStream_t st) {
+    if (k <= 16) return launch_knn3<16>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
+    if (k <= 20) return launch_knn3<20>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
+    if (k <= 32) return launch_knn3<32>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
+    if (k <= 40) return launch_knn3<40>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
+    return launch_knn3<64>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
+}
+
+// whether dgx_knn_select_f32 takes knn3_kernel for (C, N, k)
+inline bool knn3_ok(int C, int N, int k) { return g_knn3_enabled && C <= 4 && N <= K3_MAXN && k <= 64 && k <= N; }
+
 template <int NSTEP>
 int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,
                    float* img, float* xximg, hipStream_t st) {
@@ -1147,6 +1407,8 @@ extern "C" {
 void dgx_knn_stats_buffer(void* dev) { g_knn_stats = static_cast<uint32_t*>(dev); }
 #endif
 
+void dgx_knn_set_variant(int knn3) { g_knn3_enabled = knn3 != 0; }
+
 const char* dgx_knn_kernel_name(int C, int k, int N) {
     // the selection kernel dgx_knn_select_f32 launches for (C, k, N), as profilers print it
     struct Names {
@@ -1162,6 +1424,11 @@ const char* dgx_knn_kernel_name(int C, int k, int N) {
     };
     static const Names names;  // thread-safe one-time initialisation
     if (C < 1 || C > 128 || k < 1 || k > 64 || N < 1) return "";
+    if (knn3_ok(C, N, k)) {
+        static const char* k3[5] = {"knn3_kernel<16>", "knn3_kernel<20>", "knn3_kernel<32>", "knn3_kernel<40>",
+                                    "knn3_kernel<64>"};
+        return k3[k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4];
+    }
     const int ns = knn_nstep(C);
     const int a = ns == 1 ? 0 : ns == 3 ? 1 : ns == 8 ? 2 : ns == 16 ? 3 : 4;
     const int b = k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4;
@@ -1226,6 +1493,7 @@ int knn_select(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
     const float* img = static_cast<const float*>(image);
     const float* xximg = img + (size_t)B * knn_image_floats(C, N);
     hipStream_t st = dgx_stream(stream);
+    if (!seed.T && !seed.sidx && knn3_ok(C, N, k)) return dispatch_knn3(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
     switch (knn_nstep(C)) {
         case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
         case 3: return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);

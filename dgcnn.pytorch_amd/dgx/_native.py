@@ -30,6 +30,7 @@ _SIGS = {
     "dgx_knn_workspace_bytes": [_i32, _i32, _i32],
     "dgx_knn_image_bytes": [_i32, _i32, _i32],
     "dgx_knn_kernel_name": [_i32, _i32, _i32],
+    "dgx_knn_set_variant": [_i32],
     "dgx_knn_prepare_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp],
     "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
     "dgx_sqnorm_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp],
@@ -120,6 +121,7 @@ _RESTYPES = {
     "dgx_version": ctypes.c_char_p,
     "dgx_strerror": ctypes.c_char_p,
     "dgx_knn_kernel_name": ctypes.c_char_p,
+    "dgx_knn_set_variant": None,
     "dgx_knn_workspace_bytes": _sz,
     "dgx_knn_image_bytes": _sz,
 }

@@ -69,6 +69,10 @@ size_t dgx_knn_image_bytes(int B, int C, int N);
  * rocprofv3 prints it (host-side query; lets profiles be matched to the
  * kernels that actually ran). "" for unsupported (C, k, N). */
 const char* dgx_knn_kernel_name(int C, int k, int N);
+/* A/B tools only: knn3 != 0 lets 3-channel clouds (C <= 4, N <= 4096) take
+ * the VALU selection kernel (knn3_kernel); 0 (default) keeps the MFMA
+ * selection kernel for them. Process-wide; not for concurrent use. */
+void dgx_knn_set_variant(int knn3);
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                    int B, int C, int N, int order, float* xx, void* stream);
 int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,

@@ -224,3 +224,36 @@ def test_knn_spatial_seeds_change_nothing(cuda, monkeypatch, B, N, k, layout):
     got_idx, got_vals = knn_raw(x, k, return_values=True)
     from conftest import assert_knn_equivalent
     assert_knn_equivalent(seeded.cpu().numpy(), got_vals.cpu().numpy(), idx, vals)
+
+
+@pytest.fixture
+def knn3_variant():
+    from dgx import _native as nat
+    nat.lib().dgx_knn_set_variant(1)
+    yield
+    nat.lib().dgx_knn_set_variant(0)
+
+
+@pytest.mark.parametrize("B,N,k,layout", [(2, 77, 1, "perm"), (1, 64, 64, "bcn"), (3, 1024, 20, "perm"),
+                                          (2, 2048, 40, "bcn"), (1, 4096, 20, "perm"), (2, 333, 33, "bcn")])
+def test_knn3_variant_vs_oracle(cuda, knn3_variant, B, N, k, layout):
+    """The VALU 3-channel selection kernel (dgx_knn_set_variant(1), off by
+    default: measured no faster) returns the reference's neighbours too."""
+    from models.dgcnn import knn
+    pts = synth.cube_clouds(B, N, 3 * N + k)
+    idx = knn(_view(pts, layout, cuda), k).cpu().numpy()
+    ref_idx, ref_vals = oracle.knn(_cpu_view(pts, layout), k, return_values=True)
+    if N <= 1024:
+        pd = oracle.pairwise(_cpu_view(pts, layout))
+        assert_knn_equivalent(idx, np.take_along_axis(pd, idx, 2), ref_idx, ref_vals)
+    else:
+        np.testing.assert_array_equal(idx, ref_idx)
+
+
+def test_knn3_variant_ties(golden, cuda, knn3_variant):
+    from models.dgcnn import knn
+    g = golden("knn_cases.npz")
+    pts = g["ties_perm_x"]
+    idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
+    pd = oracle.pairwise(_cpu_view(pts, "perm"))
+    assert_knn_equivalent(idx, np.take_along_axis(pd, idx, 2), g["ties_perm_idx"], g["ties_perm_val"])
