@@ -7,14 +7,19 @@ Reference:
     t  = t.max(dim=-1)[0]                             (B, 128, N)     layers.py:52
 
 Engine: one autograd node. The edge tensor e is never built: conv1 is
-decomposed into PQ = X [W1;W2]^T (y_e = P_j + Q_i, as in the EdgeConv chain),
-its BN statistics come from the EdgeConv gather kernel, and h1 is written once
-per edge row (E = B*N*k rows, point-major) straight in the dtype conv2's GEMM
-consumes. conv2 is one MFMA GEMM over the E edge rows (bf16 with the BN
-statistics fused in its epilogue, or fp32 in the parity mode); the max over k
-keeps the selected value and slot. Backward: BN2 on the selected edges, a dense
-dZ2, the two conv2 GEMMs (dH1, dW2), LReLU/BN1 backward in place and a
-deterministic gather over the kNN graph and its reverse for dP/dQ.
+decomposed into PQ = X [W1;W2]^T (y_e = P_j + Q_i, as in the EdgeConv chain)
+and its BN statistics come from the EdgeConv gather kernel.
+* bf16 mode (the benchmarked path): ONE fused forward kernel per step builds
+  each 16-edge h1 tile from the gathered P_j / Q_i rows in registers / LDS,
+  runs conv2 on the MFMA, and keeps the max over k (value + slot) and the BN2
+  statistics (emlp_fwd_kernel: h1 and z2 never reach HBM); ONE fused backward
+  kernel recomputes h1 and z2, applies the BN2 backward, chains dH1 = W2^T dZ2
+  on the MFMA, applies LReLU'/BN1 and accumulates dW2 (emlp_bwd_kernel: no z2,
+  dZ2 or dH1 in HBM), then the in-edge scatter forms dP / dQ.
+* fp32 parity mode: the unfused kernels — h1 written per edge row (E = B*N*k
+  rows), conv2 on the engine's fp32 MFMA GEMM, max over k, dense dZ2, the two
+  conv2 GEMMs (dH1, dW2), LReLU/BN1 backward in place and the deterministic
+  gather over the kNN graph and its reverse for dP / dQ.
 """
 import torch
 
