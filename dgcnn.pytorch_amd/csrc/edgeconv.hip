@@ -468,15 +468,16 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
 template <typename T>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ partials, int nrows, int Co,
                                                           double count, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* __restrict__ rmean,
-                                                          float* __restrict__ rvar, double momentum, double eps,
+                                                          const float* beta, const float* rmean,
+                                                          const float* rvar, double momentum, double eps,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out,
-                                                          int64_t* __restrict__ nbt) {
+                                                          const int64_t* nbt,
+                                                          float* rmean_new, float* rvar_new, int64_t* nbt_new) {
     __shared__ double r1[256], r2[256];
     const int o = blockIdx.x, t = threadIdx.x;
-    if (nbt && o == 0 && t == 0) *nbt += 1;  // BatchNorm.num_batches_tracked, no extra launch
+    if (nbt && o == 0 && t == 0) *nbt_new = *nbt + 1;  // BatchNorm.num_batches_tracked, no extra launch
     double s1 = 0.0, s2 = 0.0;
     for (int i = t; i < nrows; i += 256) {
         s1 += (double)partials[(int64_t)i * 2 * Co + o];
@@ -502,10 +503,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ 
     shift[o] = (float)((beta ? (double)beta[o] : 0.0) - mean * a);
     if (mean_out) mean_out[o] = (float)mean;
     if (invstd_out) invstd_out[o] = (float)invstd;
-    if (rmean) rmean[o] = (float)((1.0 - momentum) * (double)rmean[o] + momentum * mean);
+    if (rmean) rmean_new[o] = (float)((1.0 - momentum) * (double)rmean[o] + momentum * mean);
     if (rvar) {
         const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-        rvar[o] = (float)((1.0 - momentum) * (double)rvar[o] + momentum * unbiased);
+        rvar_new[o] = (float)((1.0 - momentum) * (double)rvar[o] + momentum * unbiased);
     }
 }
 
@@ -1287,25 +1288,51 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, 
                                g.parts, scale, shift, slope, nullptr, nullptr, nullptr, nullptr, out, ldo);
 }
 
+int dgx_bn_finalize_out_f32(const float* partials, int nrows, int Co, double count, const float* gamma,
+                            const float* beta, const float* running_mean, const float* running_var, double momentum,
+                            double eps, float* scale, float* shift, float* mean, float* invstd,
+                            const int64_t* num_batches_tracked, float* running_mean_new, float* running_var_new,
+                            int64_t* num_batches_tracked_new, void* stream) {
+    if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
+    if ((running_mean && !running_mean_new) || (running_var && !running_var_new) ||
+        (num_batches_tracked && !num_batches_tracked_new))
+        return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
+                       count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
+                       num_batches_tracked, running_mean_new, running_var_new, num_batches_tracked_new);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
 int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, double momentum, double eps,
                         float* scale, float* shift, float* mean, float* invstd, int64_t* num_batches_tracked,
                         void* stream) {
-    if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !shift) return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
+    return dgx_bn_finalize_out_f32(partials, nrows, Co, count, gamma, beta, running_mean, running_var, momentum, eps,
+                                   scale, shift, mean, invstd, num_batches_tracked, running_mean, running_var,
+                                   num_batches_tracked, stream);
+}
+
+int dgx_bn_finalize_out_f64(const double* sums, int nrows, int Co, double count, const float* gamma,
+                            const float* beta, const float* running_mean, const float* running_var, double momentum,
+                            double eps, float* scale, float* shift, float* mean, float* invstd,
+                            const int64_t* num_batches_tracked, float* running_mean_new, float* running_var_new,
+                            int64_t* num_batches_tracked_new, void* stream) {
+    if (!sums || nrows < 1 || Co < 1 || count == 0.0 || !scale || !shift) return DGX_EINVAL;
+    if ((running_mean && !running_mean_new) || (running_var && !running_var_new) ||
+        (num_batches_tracked && !num_batches_tracked_new))
+        return DGX_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
-                       num_batches_tracked);
+                       num_batches_tracked, running_mean_new, running_var_new, num_batches_tracked_new);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_bn_finalize_f64(const double* sums, int nrows, int Co, double count, const float* gamma, const float* beta,
                         float* running_mean, float* running_var, double momentum, double eps, float* scale,
                         float* shift, float* mean, float* invstd, int64_t* num_batches_tracked, void* stream) {
-    if (!sums || nrows < 1 || Co < 1 || count == 0.0 || !scale || !shift) return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
-                       count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
-                       num_batches_tracked);
-    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+    return dgx_bn_finalize_out_f64(sums, nrows, Co, count, gamma, beta, running_mean, running_var, momentum, eps,
+                                   scale, shift, mean, invstd, num_batches_tracked, running_mean, running_var,
+                                   num_batches_tracked, stream);
 }
 
 int dgx_bn_eval_affine_f32(int Co, const float* gamma, const float* beta, const float* running_mean,

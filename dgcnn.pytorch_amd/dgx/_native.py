@@ -50,6 +50,10 @@ _SIGS = {
                                    _f64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dgx_bn_finalize_out_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp, _vp],
+    "dgx_bn_finalize_out_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp, _vp],
     "dgx_bn_finalize_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_bn_bwd_finalize_f64": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_bn_eval_affine_f32": [_i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],

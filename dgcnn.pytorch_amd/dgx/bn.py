@@ -70,29 +70,52 @@ def _compact(partials, rows, co, stream):
     return out, R + left
 
 
+def _update_targets(bn):
+    """Where the updated running statistics go: ``bn.stats_out`` = (mean, var,
+    batch counter) tensors of a functional caller (dgx.library: the module
+    buffers are read, the new values written there — no private copy first),
+    else the module's own buffers, in place."""
+    out = getattr(bn, "stats_out", None)
+    if out is None:
+        return bn.running_mean, bn.running_var, bn.num_batches_tracked
+    return out
+
+
 def batch_stats(partials, rows, count, bn, gamma, beta, stream):
     """Finalize batch statistics from per-block (sum y, sum y^2) partials
     (rows, 2, Co) over ``count`` elements; updates running statistics as
-    nn.BatchNorm would."""
+    nn.BatchNorm would (into ``bn.stats_out`` when the caller gives one)."""
     L = nat.lib()
     dev = partials.device
     co = gamma.shape[0]
     scale, shift, mean, invstd = _vec(co, dev), _vec(co, dev), _vec(co, dev), _vec(co, dev)
     _, update = mode(bn)
-    factor, nbt = _factor(bn) if update else (0.0, None)
+    rm_new, rv_new, nbt_new = _update_targets(bn)
+    if update and getattr(bn, "stats_out", None) is not None and bn.momentum is None:
+        # cumulative average: the counter is bumped on the host side of the op
+        if bn.num_batches_tracked is not None:
+            nbt_new.copy_(bn.num_batches_tracked).add_(1)
+            factor, nbt = 1.0 / float(nbt_new.item()), None
+        else:
+            factor, nbt = 0.0, None
+    else:
+        factor, nbt = _factor(bn) if update else (0.0, None)
     rm = nat.f32(bn.running_mean) if update else None
     rv = nat.f32(bn.running_var) if update else None
+    outs = (nat.f32(rm_new) if update else None, nat.f32(rv_new) if update else None,
+            nat.ptr(nbt_new, nat.I64) if nbt is not None else None)
     sync, group = dist_.sync_group(bn)
     partials, rows = _compact(partials, rows, co, stream)
     if sync:  # SyncBatchNorm: statistics of the global batch, one fp64 all-reduce
         sums = dist_.allreduce_sums(partials, count, group)   # (2C + 1) fp64: sums | global count
-        nat.check(L.dgx_bn_finalize_f64(nat.ptr(sums, nat.F64), 1, co, -1.0, nat.f32(gamma), nat.f32(beta), rm, rv,
-                                        factor, float(bn.eps), nat.f32(scale), nat.f32(shift), nat.f32(mean),
-                                        nat.f32(invstd), nat.ptr(nbt, nat.I64), stream), "bn finalize")
+        nat.check(L.dgx_bn_finalize_out_f64(nat.ptr(sums, nat.F64), 1, co, -1.0, nat.f32(gamma), nat.f32(beta), rm,
+                                            rv, factor, float(bn.eps), nat.f32(scale), nat.f32(shift), nat.f32(mean),
+                                            nat.f32(invstd), nat.ptr(nbt, nat.I64), *outs, stream), "bn finalize")
     else:
-        nat.check(L.dgx_bn_finalize_f32(nat.f32(partials), rows, co, float(count), nat.f32(gamma), nat.f32(beta), rm,
-                                        rv, factor, float(bn.eps), nat.f32(scale), nat.f32(shift), nat.f32(mean),
-                                        nat.f32(invstd), nat.ptr(nbt, nat.I64), stream), "bn finalize")
+        nat.check(L.dgx_bn_finalize_out_f32(nat.f32(partials), rows, co, float(count), nat.f32(gamma), nat.f32(beta),
+                                            rm, rv, factor, float(bn.eps), nat.f32(scale), nat.f32(shift),
+                                            nat.f32(mean), nat.f32(invstd), nat.ptr(nbt, nat.I64), *outs, stream),
+                  "bn finalize")
     return Stats(scale, shift, mean, invstd, group if sync else None, False)
 
 
@@ -125,7 +148,7 @@ def fused_finalize_args(bn, gamma, beta, co, count, dev):
     """(mode arguments of an in-launch finalize, Stats) for a BN layer whose
     batch statistics are local (no SyncBatchNorm), or None."""
     sync, _ = dist_.sync_group(bn)
-    if sync:
+    if sync or getattr(bn, "stats_out", None) is not None:   # in-place updates only
         return None
     scale, shift, mean, invstd = _vec(co, dev), _vec(co, dev), _vec(co, dev), _vec(co, dev)
     _, update = mode(bn)

@@ -18,9 +18,11 @@ tracing, autocast rules and autograd formulas, so ``torch.compile`` /
       running statistics, saved state)                   dgcnn.py:100-102
       (+ dgx::pointconv_backward)
 
-The ops are functional: BatchNorm running statistics come back as outputs and
-the caller copies them into the module buffers (what a compiled graph does with
-a buffer mutation anyway). Each op's device kernel runs the same code as the
+The ops are functional: BatchNorm running statistics come back as outputs (the
+finalize kernels read the module buffers and write the new values straight
+into the outputs: no private copy first) and the caller copies them into the
+module buffers (what a compiled graph does with a buffer mutation anyway;
+torch does not allow an autograd formula on an op that mutates its inputs). Each op's device kernel runs the same code as the
 engine's autograd Functions (dgx.edgeconv, dgx.pointconv), so eager results
 are identical either way; ``models.dgcnn.DGCNN`` takes this path unless a
 BatchNorm is a SyncBatchNorm (process groups cannot cross the op boundary) —
@@ -66,9 +68,10 @@ class _Rec:
 
 class _BNSpec:
     """The nn.BatchNorm fields dgx.bn reads, rebuilt from tensors that crossed
-    the op boundary (running statistics are the op's private copies)."""
+    the op boundary (the running statistics are read from the inputs and the
+    updates written to the op's outputs, ``out``)."""
 
-    def __init__(self, training, track, rm, rv, nbt, momentum, eps):
+    def __init__(self, training, track, rm, rv, nbt, momentum, eps, out=None):
         self.training = bool(training)
         self.track_running_stats = bool(track)
         self.running_mean = rm if rm.numel() else None
@@ -76,6 +79,9 @@ class _BNSpec:
         self.num_batches_tracked = nbt if nbt.numel() else None
         self.momentum = None if momentum < 0 else float(momentum)
         self.eps = float(eps)
+        # (mean, var, counter) outputs the finalize writes the updated statistics
+        # to (dgx.bn._update_targets); the inputs are only read
+        self.stats_out = out
 
 
 def _use_batch(training, rm):
@@ -96,10 +102,20 @@ def _copy_many(dsts, srcs):
         torch._foreach_copy_(ds, ss)
 
 
-def _fresh(ts):
-    """Private copies of ``ts`` (distinct storages: op outputs may not alias)."""
-    outs = [torch.empty_like(t) for t in ts]
-    _copy_many(outs, ts)
+def _stat_outputs(training, track, rms, rvs, nbts):
+    """The ops' running-statistics outputs (distinct storages: op outputs may
+    not alias inputs). A layer that updates them (training and tracking) gets
+    uninitialised tensors the finalize kernel fills from the inputs; the others
+    get copies of the inputs, all in one multi-tensor launch per dtype (none
+    in a training step)."""
+    outs, dsts, srcs = [], [], []
+    for tr, tk, rm, rv, nb in zip(training, track, rms, rvs, nbts):
+        o = (torch.empty_like(rm), torch.empty_like(rv), torch.empty_like(nb))
+        if not (tr and tk and rm.numel()):
+            dsts += list(o)
+            srcs += [rm, rv, nb]
+        outs.append(o)
+    _copy_many(dsts, srcs)
     return outs
 
 
@@ -234,10 +250,10 @@ def edgeconv_chain(x: Tensor, k: int, weights: list[Tensor], gammas: list[Tensor
     """DGCNN's EdgeConv blocks (dgcnn.py:84-100) as dgx.edgeconv runs them:
     returns (concat buffer (B*N, sum Co), its bf16 twin or empty, updated
     running means / vars / batch counters, the state the backward reads)."""
-    n = len(running_means)
-    fresh = _fresh(list(running_means) + list(running_vars) + list(nbts))
-    rms, rvs, nbs = fresh[:n], fresh[n:2 * n], fresh[2 * n:]
-    specs = [_BNSpec(*a) for a in zip(training, track, rms, rvs, nbs, momentum, eps)]
+    outs = _stat_outputs(training, track, running_means, running_vars, nbts)
+    rms, rvs, nbs = [o[0] for o in outs], [o[1] for o in outs], [o[2] for o in outs]
+    specs = [_BNSpec(*a, out=o) for a, o in zip(zip(training, track, running_means, running_vars, nbts, momentum, eps),
+                                                  outs)]
     layers = _chain_layers(weights, specs, slopes)
     params = [t for trip in zip(weights, gammas, betas) for t in trip]
     preps = None
@@ -369,8 +385,8 @@ def pointconv(X: Tensor, X16: Tensor, B: int, N: int, weight: Tensor, gamma: Ten
     """conv5 -> BN -> LeakyReLU on the concat buffer (dgcnn.py:100-102) as
     dgx.pointconv runs it: (out (B, Co, N), updated running mean / var /
     batch counter, saved state [Z, scale, shift, mean, invstd])."""
-    rm, rv, nb = _fresh([running_mean, running_var, nbt])
-    spec = _BNSpec(training, track, rm, rv, nb, momentum, eps)
+    (rm, rv, nb), = _stat_outputs([training], [track], [running_mean], [running_var], [nbt])
+    spec = _BNSpec(training, track, running_mean, running_var, nbt, momentum, eps, out=(rm, rv, nb))
     wprep = None
     if prep is not None:
         Co, K = weight.shape[0], weight.shape[1]

@@ -174,6 +174,24 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         double momentum, double eps,
                         float* scale, float* shift, float* mean, float* invstd,
                         int64_t* num_batches_tracked, void* stream);
+/* dgx_bn_finalize_f32 writing the updated running statistics (and the
+ * incremented batch counter) to separate *_new outputs instead of in place —
+ * the form a functional op (torch.library) needs: no private copy of the
+ * buffers is made first. dgx_bn_finalize_f32 = this with *_new = the inputs. */
+int dgx_bn_finalize_out_f32(const float* partials, int nrows, int Co, double count,
+                            const float* gamma, const float* beta,
+                            const float* running_mean, const float* running_var,
+                            double momentum, double eps, float* scale, float* shift,
+                            float* mean, float* invstd, const int64_t* num_batches_tracked,
+                            float* running_mean_new, float* running_var_new,
+                            int64_t* num_batches_tracked_new, void* stream);
+int dgx_bn_finalize_out_f64(const double* sums, int nrows, int Co, double count,
+                            const float* gamma, const float* beta,
+                            const float* running_mean, const float* running_var,
+                            double momentum, double eps, float* scale, float* shift,
+                            float* mean, float* invstd, const int64_t* num_batches_tracked,
+                            float* running_mean_new, float* running_var_new,
+                            int64_t* num_batches_tracked_new, void* stream);
 /* The same finalize from fp64 column sums (nrows x 2 x Co doubles): the global
  * sums of a SyncBatchNorm all-reduce (main_partseg_dist.py:189), kept in fp64
  * into var = E[y^2] - E[y]^2. count < 0: the element count is the double that
