@@ -1117,15 +1117,22 @@ bool aligned_to(const void* p, int bytes) { return (reinterpret_cast<uintptr_t>(
 // consecutive columns (16-B stores along the row).
 constexpr int SK_ROWS = 64;
 constexpr int SK_MAXK = 16;
+// split != 0: W is a conv weight in the reference layout (N/2, 2K) = [W1 | W2]
+// and row n of the product's weight is W1[n] (n < N/2) or W2[n - N/2]: the
+// EdgeConv block's [W1; W2] without a separate reshuffle (torch.cat) launch.
 __global__ __launch_bounds__(256) void smallk_gemm_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ W, int M, int N, int K,
-                                                          float* __restrict__ C, int64_t ldc) {
+                                                          float* __restrict__ C, int64_t ldc, int split) {
     extern __shared__ float sk[];  // W [N][K] | X [SK_ROWS][K]
     float* ws = sk;
     float* xs = sk + N * K;
     const int r0 = blockIdx.x * SK_ROWS;
     const int rows = min(SK_ROWS, M - r0);
-    for (int e = threadIdx.x; e < N * K; e += 256) ws[e] = W[e];
+    const int half = N >> 1;
+    for (int e = threadIdx.x; e < N * K; e += 256) {
+        const int n = e / K, c = e - n * K;
+        ws[e] = split ? W[(n < half ? n : n - half) * 2 * K + (n < half ? 0 : K) + c] : W[e];
+    }
     for (int e = threadIdx.x; e < rows * K; e += 256) {
         const int r = e / K, c = e - r * K;
         xs[e] = X[(int64_t)(r0 + r) * ldx + c];
@@ -1155,7 +1162,19 @@ int dgx_gemm_smallk_f32(const float* X, int64_t ldx, const float* W, int M, int 
     if ((size_t)(N + SK_ROWS) * K * sizeof(float) > 64 * 1024) return DGX_EUNSUPPORTED;
     const size_t lds = (size_t)(N + SK_ROWS) * K * sizeof(float);
     hipLaunchKernelGGL(smallk_gemm_kernel, dim3((M + SK_ROWS - 1) / SK_ROWS), dim3(256), lds, dgx_stream(stream), X,
-                       ldx, W, M, N, K, C, ldc);
+                       ldx, W, M, N, K, C, ldc, 0);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_gemm_smallk_split_f32(const float* X, int64_t ldx, const float* Wref, int M, int Co, int K, float* C,
+                              int64_t ldc, void* stream) {
+    const int N = 2 * Co;
+    if (!X || !Wref || !C || M < 1 || Co < 2 || K < 1 || ldx < K || ldc < N) return DGX_EINVAL;
+    if (K > SK_MAXK || N % 4 || ldc % 4 || reinterpret_cast<uintptr_t>(C) % 16) return DGX_EUNSUPPORTED;
+    if ((size_t)(N + SK_ROWS) * K * sizeof(float) > 64 * 1024) return DGX_EUNSUPPORTED;
+    const size_t lds = (size_t)(N + SK_ROWS) * K * sizeof(float);
+    hipLaunchKernelGGL(smallk_gemm_kernel, dim3((M + SK_ROWS - 1) / SK_ROWS), dim3(256), lds, dgx_stream(stream), X,
+                       ldx, Wref, M, N, K, C, ldc, 1);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

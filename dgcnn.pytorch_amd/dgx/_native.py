@@ -84,6 +84,7 @@ _SIGS = {
                       _vp],
     "dgx_gemm_f32": [_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp],
     "dgx_gemm_f32_splits": [_i32, _i32, _i32],
+    "dgx_gemm_smallk_split_f32": [_vp, _i64, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_gemm_smallk_f32": [_vp, _i64, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_slab_reduce_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_gemm_lds_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp,

@@ -195,7 +195,7 @@ class _EdgeConvStack(torch.autograd.Function):
             wprep = None
             if cin <= G.SMALLK_MAX:
                 # raw coordinates (block 1, K = 3): exact fp32 in every mode
-                PQ = G.mm_smallk(X, split_weight(w, cin, co))
+                PQ = G.mm_smallk_split(X, w, co)
             elif bf16:
                 X16 = xcat16[:, off_in:off_in + cin] if li > 0 else None
                 if have16 and G.lds_ok_nt(X16, cin):

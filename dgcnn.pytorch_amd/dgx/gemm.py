@@ -194,6 +194,23 @@ def mm_smallk(x, w):
     return out
 
 
+def mm_smallk_split(x, wref, co):
+    """mm_smallk(x, [W1; W2]) for a conv weight wref (Co, 2K[,1,1]) = [W1 | W2]
+    in the reference layout (dgx_gemm_smallk_split_f32): the EdgeConv PQ of the
+    3-channel block, no reshuffled weight copy."""
+    M, K = x.shape
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    w = wref.reshape(co, 2 * K)
+    if not w.is_contiguous():
+        w = w.contiguous()
+    out = torch.empty((M, 2 * co), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device), _Timed(2.0 * M * 2 * co * K):
+        nat.check(nat.lib().dgx_gemm_smallk_split_f32(nat.f32(x), x.stride(0) if M > 1 else K, nat.f32(w), M, co, K,
+                                                      nat.f32(out), 2 * co, nat.stream_of(x)), "gemm small-k")
+    return out
+
+
 def mm_xw(x, w, out=None, accumulate=False):
     """out (M,N) (+)= x (M,K) @ w (K,N)."""
     M, K = x.shape

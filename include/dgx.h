@@ -375,6 +375,11 @@ int dgx_gemm_f32_splits(int M, int N, int K);
  * every precision mode. */
 int dgx_gemm_smallk_f32(const float* X, int64_t ldx, const float* W, int M, int N, int K,
                         float* C, int64_t ldc, void* stream);
+/* dgx_gemm_smallk_f32 with the weight given as the reference's conv weight
+ * (Co, 2K) = [W1 | W2] (models/dgcnn.py:55): C (M, 2Co) = X [W1; W2]^T, the
+ * EdgeConv PQ of the 3-channel block without a reshuffled weight copy. */
+int dgx_gemm_smallk_split_f32(const float* X, int64_t ldx, const float* Wref, int M, int Co,
+                              int K, float* C, int64_t ldc, void* stream);
 /* out[orow][ocol] = sum_s slab[s][r][c] (fixed order: deterministic); rows
  * r >= split land at (r - split, c + cols): the [W1;W2] -> [W1 | W2] weight
  * un-stacking (reference conv weight layout (Co, 2C, 1, 1)). */

@@ -269,3 +269,20 @@ def test_mm32_fp32_mfma(cuda, M, N, K, ta, tb):
         out = torch.empty((M, N), device=cuda)
         G.mm32(av, bv, out=out, addend=add)
         assert rel_err(out.cpu(), add.cpu().double() + ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,Co,K", [(32768, 64, 3), (1000, 24, 3), (77, 8, 9)])
+def test_smallk_split_weight(cuda, M, Co, K):
+    """dgx_gemm_smallk_split_f32 on the reference conv weight (Co, 2K) = [W1 | W2]
+    equals the small-K GEMM on the stacked [W1; W2] bit for bit, and fp64."""
+    from dgx import gemm as G
+    from dgx.edgeconv import split_weight
+    g = torch.Generator().manual_seed(M + Co)
+    x = torch.randn(M, K, generator=g).to(cuda)
+    w = torch.randn(Co, 2 * K, 1, 1, generator=g).to(cuda)
+    ref = G.mm_smallk(x, split_weight(w, K, Co))
+    out = G.mm_smallk_split(x, w, Co)
+    assert torch.equal(out, ref)
+    w2 = w.reshape(Co, 2 * K).double()
+    exact = x.double() @ torch.cat([w2[:, :K], w2[:, K:]], 0).t()
+    assert rel_err(out.cpu(), exact.cpu()) < 1e-6
