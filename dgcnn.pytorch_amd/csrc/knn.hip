@@ -1080,6 +1080,74 @@ uint32_t* g_knn_stats = nullptr;   // diagnostics build: device buffer set by dg
 inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
 inline size_t knn_xximg_floats(int N) { return (size_t)knn_ntile(N) * 16; }
 
+// ------------------------------------- apply + next block's kNN image ----
+// An EdgeConv block's output x_l = LeakyReLU(a ysel + b) (dgcnn.py:84-98) is
+// the next block's kNN input (dgcnn.py:88: knn(x_l) on the contiguous (B,C,N)
+// tensor, ORDER_STRIDED). This kernel writes x_l (fp32 concat slice + its bf16
+// twin, as dgx_bn_lrelu_apply_f32 does) AND what knn_image_kernel would build
+// from it — the MFMA operand image, |x|^2 and the |x|^2 image — so the next
+// kNN skips its image pass. One point per TPP = C/4 lanes (4 channels each);
+// |x|^2 in the reference's cascade order (C a multiple of 16, no tail points:
+// N % 32 == 0): lane 4r gathers run r's 16 squares (channels 16r..16r+15) and
+// sums them in order, lane 0 adds the runs in order (sqnorm_sum's cascade16).
+template <int CO>
+__global__ __launch_bounds__(256) void apply_image_kernel(const float* __restrict__ ysel, int M, int N,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float slope,
+                                                          float* __restrict__ out, int ldo, __bf16* __restrict__ out16,
+                                                          float* __restrict__ xx, float* __restrict__ img,
+                                                          float* __restrict__ xximg) {
+#pragma clang fp contract(off)
+    constexpr int NSTEP = CO / 4, TPP = CO / 4, PPB = 256 / TPP, RUNS = CO / 16;
+    static_assert(CO % 16 == 0 && TPP <= 64, "whole 16-channel runs, one point inside a wave");
+    const int q = threadIdx.x % TPP;
+    const int64_t i = (int64_t)blockIdx.x * PPB + threadIdx.x / TPP;   // point row b*N + n
+    const bool ok = i < M;
+    const int64_t ic = ok ? i : M - 1;
+    const float4 y = *reinterpret_cast<const float4*>(ysel + ic * CO + 4 * q);
+    const float4 a = *reinterpret_cast<const float4*>(scale + 4 * q);
+    const float4 c = *reinterpret_cast<const float4*>(shift + 4 * q);
+    float v[4] = {lrelu(fmaf(a.x, y.x, c.x), slope), lrelu(fmaf(a.y, y.y, c.y), slope),
+                  lrelu(fmaf(a.z, y.z, c.z), slope), lrelu(fmaf(a.w, y.w, c.w), slope)};
+    const int b = (int)(ic / N), n = (int)(ic - (int64_t)b * N);
+    const int ntile = N >> 4, st = n >> 4, ii = knn_row(n & 15);
+    if (ok) {
+        *reinterpret_cast<float4*>(out + i * ldo + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+        if (out16) {
+            typedef __bf16 h4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<h4*>(out16 + i * ldo + 4 * q) = h4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+        }
+        // image lane 16 u + ii of tile st holds channels 4 t + u: here t = q
+        float* __restrict__ ib = img + (((int64_t)b * ntile + st) * 64 + ii) * NSTEP + q;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ib[16 * u * NSTEP] = v[u];
+    }
+    float sq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sq[u] = v[u] * v[u];
+    // run r = lanes 4r .. 4r+3 of the point: lane 4r collects the 16 squares
+    const int lane = threadIdx.x & 63;
+    float g[16];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[4 * h + u] = __shfl(sq[u], lane + h, 64);
+    float run = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) run = run + g[e];
+    float runs[RUNS];
+#pragma unroll
+    for (int r = 0; r < RUNS; ++r) runs[r] = __shfl(run, lane + 4 * r, 64);
+    if (ok && q == 0) {
+        float a1 = 0.f;
+#pragma unroll
+        for (int r = 0; r < RUNS; ++r) a1 = a1 + runs[r];
+        const float w = 0.f + a1;   // cascade16's a0 + a1 (a0 = 0: no partial run)
+        xx[i] = w;
+        xximg[((int64_t)b * ntile + st) * 16 + ii] = w;
+    }
+}
+
 // ------------------------------------------------ 3-channel selection ----
 // knn3_kernel<KB>: clouds of C <= 4 channels (the xyz kNN of DGCNN's first
 // block, PositionEmbedding and compute_hog_1x1), N <= K3_MAXN. No MFMA: a
@@ -1434,6 +1502,29 @@ const char* dgx_knn_kernel_name(int C, int k, int N) {
     const int b = k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4;
     static const int KBS[5] = {16, 20, 32, 40, 64};
     return names.s[a][b][knn_qg(ns, KBS[b], N) - 1];
+}
+
+int dgx_bn_lrelu_apply_knn_image_f32(const float* ysel, int B, int N, int Co, const float* scale,
+                                     const float* shift, float slope, float* out, int ldo, void* out_bf16, float* xx,
+                                     void* image, size_t image_bytes, void* stream) {
+    if (!ysel || !scale || !shift || !out || !xx || !image || B < 1 || N < 1 || ldo < Co) return DGX_EINVAL;
+    if ((Co != 64 && Co != 128) || N % 32 != 0) return DGX_EUNSUPPORTED;
+    if (image_bytes < dgx_knn_image_bytes(B, Co, N)) return DGX_EINVAL;
+    if (ldo % 4 || reinterpret_cast<uintptr_t>(out) % 16 || reinterpret_cast<uintptr_t>(ysel) % 16 ||
+        reinterpret_cast<uintptr_t>(scale) % 16 || reinterpret_cast<uintptr_t>(shift) % 16 ||
+        reinterpret_cast<uintptr_t>(out_bf16) % 8 || reinterpret_cast<uintptr_t>(image) % 16)
+        return DGX_EUNSUPPORTED;
+    float* img = static_cast<float*>(image);
+    float* xximg = img + (size_t)B * knn_image_floats(Co, N);
+    const int M = B * N;
+    hipStream_t st = dgx_stream(stream);
+    if (Co == 64)
+        hipLaunchKernelGGL(apply_image_kernel<64>, dim3((M + 15) / 16), dim3(256), 0, st, ysel, M, N, scale, shift,
+                           slope, out, ldo, static_cast<__bf16*>(out_bf16), xx, img, xximg);
+    else
+        hipLaunchKernelGGL(apply_image_kernel<128>, dim3((M + 7) / 8), dim3(256), 0, st, ysel, M, N, scale, shift,
+                           slope, out, ldo, static_cast<__bf16*>(out_bf16), xx, img, xximg);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,

@@ -31,7 +31,7 @@ from . import _native as nat
 from . import bn as bn_
 from . import gemm as G
 from . import precision as prec
-from .ops import knn_raw, reduction_order
+from .ops import knn_image_buffers, knn_raw, reduction_order
 
 _tls = threading.local()
 
@@ -55,6 +55,10 @@ FOLD_BN_BWD = os.environ.get("DGX_FOLD_BN_BWD", "1") == "1"
 # before the ticket costs more than the finalize launch it removes.
 # DGX_FOLD_BN_FWD=1 turns it on (A/B only).
 FOLD_BN_FWD = os.environ.get("DGX_FOLD_BN_FWD", "0") == "1"
+# blocks 1-3: the BN + LeakyReLU apply also writes the next block's kNN operand
+# image and |x|^2 (dgx_bn_lrelu_apply_knn_image_f32), so that kNN skips its
+# prepare pass (DGX_FUSE_KNN_IMAGE=0: separate prepare pass, A/B only)
+FUSE_KNN_IMAGE = os.environ.get("DGX_FUSE_KNN_IMAGE", "1") == "1"
 
 
 def debug_capture():
@@ -176,6 +180,7 @@ class _EdgeConvStack(torch.autograd.Function):
             jobs = [(params[3 * li], ly.cout, ly.cin, True, True) for li, ly in enumerate(layers) if li > 0]
             preps[1:] = G.prep_weights(jobs)
         dbg = debug_capture()
+        next_prepared = None   # the next block's kNN image, written by this block's apply
         for li, ly in enumerate(layers):
             w, gamma, beta = params[3 * li: 3 * li + 3]
             cin, co = ly.cin, ly.cout
@@ -191,7 +196,8 @@ class _EdgeConvStack(torch.autograd.Function):
                 # candidates then reach it)
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
                               strides=(N * total, 1, total), shape=(B, cin, N),
-                              seeds=idx if KNN_SEEDS else None)
+                              seeds=idx if KNN_SEEDS else None, prepared=next_prepared)
+            next_prepared = None
             wprep = None
             if cin <= G.SMALLK_MAX:
                 # raw coordinates (block 1, K = 3): exact fp32 in every mode
@@ -222,9 +228,16 @@ class _EdgeConvStack(torch.autograd.Function):
                         st = bn_.running_stats(bn, gamma, beta, stream)
                 if use_batch or need_grad:
                     out16 = xcat16[:, off:off + co] if bf16 else None
-                    nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, co, nat.f32(st.scale), nat.f32(st.shift),
-                                                       float(ly.slope), nat.f32(out), total, nat.ptr(out16, nat.BF16),
-                                                       stream), "bn apply")
+                    if FUSE_KNN_IMAGE and li + 1 < len(layers) and co in (64, 128) and N % 32 == 0:
+                        next_prepared = knn_image_buffers(B, co, N, dev)
+                        nat.check(L.dgx_bn_lrelu_apply_knn_image_f32(
+                            nat.f32(ysel), B, N, co, nat.f32(st.scale), nat.f32(st.shift), float(ly.slope),
+                            nat.f32(out), total, nat.ptr(out16, nat.BF16), nat.f32(next_prepared[0]),
+                            nat.f32(next_prepared[1]), next_prepared[1].numel() * 4, stream), "bn apply + knn image")
+                    else:
+                        nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, co, nat.f32(st.scale),
+                                                           nat.f32(st.shift), float(ly.slope), nat.f32(out), total,
+                                                           nat.ptr(out16, nat.BF16), stream), "bn apply")
                     have16 = bf16
                     saved.append((idx, PQ, ysel, arg, sumP, st, wprep))
                     if dbg is not None:

@@ -39,14 +39,29 @@ def _as_f32(x):
     return x if x.dtype == torch.float32 else x.float()
 
 
-def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False, seeds=None):
+def knn_image_buffers(B, C, N, dev):
+    """(xx, image) scratch of one kNN call (dgx_knn_prepare_f32's outputs); a
+    producer kernel may fill them (dgx_bn_lrelu_apply_knn_image_f32) and hand
+    them to knn_raw(prepared=...)."""
+    L = nat.lib()
+    img_bytes = L.dgx_knn_image_bytes(B, C, N)
+    xx = torch.empty((B * N,), dtype=torch.float32, device=dev)
+    img = torch.empty((max(img_bytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
+    return xx, img
+
+
+def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False, seeds=None,
+            prepared=None):
     """kNN on a (B,C,N) fp32 view. ``strides``/``shape`` let callers describe a
     strided slice of a larger buffer (the engine's point-major concat buffer).
     ``seeds``: optional int32 (B, N, ks >= k) candidate ids per query (e.g. the
     previous EdgeConv block's neighbours): the min of their distances is a
     lower bound of each row's k-th value (dgx_knn_seed_f32) that lets the
     selection skip the candidates below it. The result does not depend on the
-    seeds (a row whose seed were too high is recomputed exactly)."""
+    seeds (a row whose seed were too high is recomputed exactly).
+    ``prepared``: (xx, image) already holding |x|^2 in ``order`` and the operand
+    image of exactly this view (knn_image_buffers + a producer kernel): the
+    prepare pass is skipped."""
     nat.require_device(x)
     B, C, N = shape if shape is not None else x.shape
     sB, sC, sN = strides if strides is not None else x.stride()
@@ -66,14 +81,19 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     L = nat.lib()
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
     vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
-    xx = torch.empty((B * N,), dtype=torch.float32, device=x.device)
     img_bytes = L.dgx_knn_image_bytes(B, C, N)
-    img = torch.empty((max(img_bytes, 4) + 3) // 4, dtype=torch.float32, device=x.device)  # operand image scratch
     stream = nat.stream_of(x)
+    if prepared is not None:
+        xx, img = prepared
+        if xx.numel() != B * N or img.numel() * 4 < img_bytes:
+            raise RuntimeError("knn: prepared |x|^2 / image buffers do not match the cloud")
+    else:
+        xx, img = knn_image_buffers(B, C, N, x.device)
     with torch.cuda.device(x.device):
-        # |x|^2 and the MFMA operand image in one pass over x
-        nat.check(L.dgx_knn_prepare_f32(nat.f32(x), sB, sC, sN, B, C, N, order, nat.f32(xx), nat.f32(img),
-                                        img_bytes, stream), "knn prepare")
+        if prepared is None:
+            # |x|^2 and the MFMA operand image in one pass over x
+            nat.check(L.dgx_knn_prepare_f32(nat.f32(x), sB, sC, sN, B, C, N, order, nat.f32(xx), nat.f32(img),
+                                            img_bytes, stream), "knn prepare")
         timing = getattr(_tls, "timing", None)
         T = None
         spatial = seeds is None and SPATIAL_SEEDS and C <= 4 and 256 <= N <= 4096 and k <= 64

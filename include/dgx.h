@@ -69,6 +69,17 @@ size_t dgx_knn_image_bytes(int B, int C, int N);
  * rocprofv3 prints it (host-side query; lets profiles be matched to the
  * kernels that actually ran). "" for unsupported (C, k, N). */
 const char* dgx_knn_kernel_name(int C, int k, int N);
+/* dgx_bn_lrelu_apply_f32 for an EdgeConv block whose output feeds the next
+ * block's kNN (dgcnn.py:84-98, the feature-space knn of x_l): writes
+ * out = LeakyReLU(scale*ysel + shift) (+ its bf16 twin) AND the next kNN's
+ * prepared operands — |x|^2 in the reference's strided-layout order into xx
+ * (B*N) and the operand image (dgx_knn_image_bytes(B, Co, N)) — so that kNN
+ * runs dgx_knn_select_f32 directly (no dgx_knn_prepare_f32 pass).
+ * Co in {64, 128}, N % 32 == 0; else DGX_EUNSUPPORTED. */
+int dgx_bn_lrelu_apply_knn_image_f32(const float* ysel, int B, int N, int Co,
+                                     const float* scale, const float* shift, float slope,
+                                     float* out, int ldo, void* out_bf16, float* xx,
+                                     void* image, size_t image_bytes, void* stream);
 /* A/B tools only: knn3 != 0 lets 3-channel clouds (C <= 4, N <= 4096) take
  * the VALU selection kernel (knn3_kernel); 0 (default) keeps the MFMA
  * selection kernel for them. Process-wide; not for concurrent use. */

@@ -257,3 +257,43 @@ def test_knn3_variant_ties(golden, cuda, knn3_variant):
     idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
     pd = oracle.pairwise(_cpu_view(pts, "perm"))
     assert_knn_equivalent(idx, np.take_along_axis(pd, idx, 2), g["ties_perm_idx"], g["ties_perm_val"])
+
+
+@pytest.mark.parametrize("B,N,Co", [(4, 1024, 64), (2, 2048, 128), (3, 96, 64)])
+def test_apply_writes_next_knn_image(cuda, B, N, Co):
+    """dgx_bn_lrelu_apply_knn_image_f32 (EdgeConv apply + the next block's kNN
+    operands) equals dgx_bn_lrelu_apply_f32 followed by dgx_knn_prepare_f32 on
+    the written concat slice, bit for bit (|x|^2 in the reference's strided
+    order), and the kNN from the prepared buffers equals the plain kNN."""
+    from dgx import _native as nat
+    from dgx.ops import knn_image_buffers, knn_raw
+    L = nat.lib()
+    g = torch.Generator().manual_seed(N + Co)
+    M, total, off = B * N, Co + 32, 16
+    ysel = torch.randn(M, Co, generator=g).to(cuda)
+    scale, shift = torch.randn(Co, generator=g).to(cuda), torch.randn(Co, generator=g).to(cuda)
+    outs = []
+    for fused in (False, True):
+        xcat = torch.zeros(M, total, device=cuda)
+        x16 = torch.zeros(M, total, dtype=torch.bfloat16, device=cuda)
+        out, out16 = xcat[:, off:off + Co], x16[:, off:off + Co]
+        xx, img = knn_image_buffers(B, Co, N, cuda)
+        st = nat.stream_of(ysel)
+        if fused:
+            nat.check(L.dgx_bn_lrelu_apply_knn_image_f32(nat.f32(ysel), B, N, Co, nat.f32(scale), nat.f32(shift), 0.2,
+                                                         nat.f32(out), total, nat.ptr(out16), nat.f32(xx),
+                                                         nat.f32(img), img.numel() * 4, st), "fused")
+        else:
+            nat.check(L.dgx_bn_lrelu_apply_f32(nat.f32(ysel), M, Co, nat.f32(scale), nat.f32(shift), 0.2,
+                                               nat.f32(out), total, nat.ptr(out16), st), "apply")
+            nat.check(L.dgx_knn_prepare_f32(nat.f32(xcat[:, off:]), N * total, 1, total, B, Co, N, nat.ORDER_STRIDED,
+                                            nat.f32(xx), nat.f32(img), img.numel() * 4, st), "prepare")
+        outs.append((xcat, x16, xx, img))
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+    xcat, _, xx, img = outs[1]
+    kw = dict(order=nat.ORDER_STRIDED, out_dtype=torch.int32, strides=(N * total, 1, total), shape=(B, Co, N))
+    a = knn_raw(xcat[:, off:], 20, prepared=(xx, img), **kw)
+    b = knn_raw(xcat[:, off:], 20, **kw)
+    assert torch.equal(a, b)
