@@ -36,7 +36,8 @@ constexpr int GB_BM = 128;
 constexpr int GB_BK = 32;
 constexpr int GB_LDK = GB_BK + 8;  // bf16 per LDS row (80 B)
 
-enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4, EPI_DZ2 = 5, EPI_H1BWD = 6 };
+enum { EPI_STORE = 0, EPI_ACCUM = 1, EPI_STATS = 2, EPI_SLAB = 3, EPI_STATS16 = 4, EPI_DZ2 = 5, EPI_H1BWD = 6,
+       EPI_EDZ = 7 };
 
 // Extra operands of the PositionEmbedding edge-MLP epilogues (EPI_H1BWD):
 // g = dH1 * LReLU'(z1) with z1 = a1 (P_j + Q_i) + b1 for edge row e = i*k + s,
@@ -536,6 +537,18 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     constexpr int RR = BM / NR;
     static_assert(RR * LDT * 4 <= LDSB && WM % NR == 0, "epilogue tile must fit the stage buffers");
     constexpr int VO = (EPI == EPI_STATS16 || EPI == EPI_DZ2 || EPI == EPI_H1BWD) ? 8 : 4;  // outputs per 16-B store
+    // EPI_EDZ (EdgeConv backward, dgx_gemm_edge_dz_bf16): the product + addend is
+    // the gradient dY of the previous block's output; instead of storing it the
+    // epilogue applies that block's LeakyReLU' / BN-backward input: dz = dY *
+    // LReLU'(a ysel + b), stored as packed dz|slot words (the selected slot in the
+    // 6 low mantissa bits, dgx_edge_bwd_dz_packed_f32's format) with the per-tile
+    // column partials (sum dz, sum dz * yhat) — no dY round trip, no dz pass.
+    // ex.PQ = ysel (ld ex.ldpq), aux8 = the forward's slots (same ld).
+    float e1[4], e2[4];
+    if constexpr (EPI == EPI_EDZ) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { e1[u] = 0.f; e2[u] = 0.f; }
+    }
     constexpr int CPR = BN / VO;
     float* tile = reinterpret_cast<float*>(lds);
     const bool vec_out = (ldc % VO) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
@@ -640,6 +653,65 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
                 float acc_s = 0.f;
                 for (int r = grp; r < GB_THREADS; r += CPR) acc_s += red[r * 16 + which * 8 + u];
                 if (j0 + col < N) part[((int64_t)ti * 2 + which) * N + j0 + col] = acc_s;
+            }
+            continue;
+        }
+        if constexpr (EPI == EPI_EDZ) {
+            constexpr int IT = RR * CPR / GB_THREADS;
+            static_assert(RR * CPR % GB_THREADS == 0 && GB_THREADS % CPR == 0, "whole iterations, fixed columns");
+            const int jc = min(j0 + (tid % CPR) * VO, N - 4);
+            float yv[IT][4], av[IT][4];
+            uint32_t sw[IT];
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {   // loads of this round's rows issued before the tile is ready
+                const int e = tid + it * GB_THREADS;
+                const int64_t row = min((int64_t)(i0 + q * RR + e / CPR), (int64_t)M - 1);
+                *reinterpret_cast<float4*>(yv[it]) = *reinterpret_cast<const float4*>(ex.PQ + row * ex.ldpq + jc);
+                *reinterpret_cast<float4*>(av[it]) = *reinterpret_cast<const float4*>(addend + row * ldd + jc);
+                sw[it] = *reinterpret_cast<const uint32_t*>(aux8 + row * ex.ldpq + jc);
+            }
+            float ea[4], eb[4], em[4], ei[4];
+            *reinterpret_cast<float4*>(ea) = *reinterpret_cast<const float4*>(ex.scale + jc);
+            *reinterpret_cast<float4*>(eb) = *reinterpret_cast<const float4*>(ex.shift + jc);
+            *reinterpret_cast<float4*>(em) = *reinterpret_cast<const float4*>(ex.mean + jc);
+            *reinterpret_cast<float4*>(ei) = *reinterpret_cast<const float4*>(ex.invstd + jc);
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int e = tid + it * GB_THREADS;
+                const int rr = e / CPR, c = (e - rr * CPR) * VO;
+                const int64_t i = i0 + q * RR + rr;
+                const int j = j0 + c;
+                if (i >= M || j + 4 > N) continue;
+                const float* src = tile + rr * LDT + c;
+                uint32_t w[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float g = src[u] + av[it][u];   // dY, as EPI_ACCUM forms it
+                    const float z = fmaf(ea[u], yv[it][u], eb[u]);
+                    const float d = g * (z > 0.f ? 1.f : ex.slope);
+                    e1[u] += d;
+                    e2[u] = fmaf(d, (yv[it][u] - em[u]) * ei[u], e2[u]);
+                    w[u] = (__float_as_uint(d) & ~63u) | ((sw[it] >> (8 * u)) & 0xffu);
+                }
+                *reinterpret_cast<uint4*>(out + i * ldc + j) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            if (q == NR - 1) {   // column partials of the tile: the GB_THREADS / CPR threads of each column group
+                __syncthreads();
+                float* red = tile;  // [GB_THREADS][8]
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    red[tid * 8 + u] = e1[u];
+                    red[tid * 8 + 4 + u] = e2[u];
+                }
+                __syncthreads();
+                for (int o = tid; o < 2 * BN; o += GB_THREADS) {
+                    const int which = o / BN, col = o - which * BN;
+                    const int grp = col / VO, u = col - grp * VO;
+                    float acc_s = 0.f;
+                    for (int r = grp; r < GB_THREADS; r += CPR) acc_s += red[r * 8 + which * 4 + u];
+                    if (j0 + col < N) part[((int64_t)ti * 2 + which) * N + j0 + col] = acc_s;
+                }
             }
             continue;
         }
@@ -1283,6 +1355,57 @@ int dgx_gemm_h1bwd_bf16(const void* dZ2, const void* W2t, int M, int N, int K, c
                        dgx_stream(stream), static_cast<const bf16*>(dZ2), (int64_t)K, static_cast<const bf16*>(W2t),
                        (int64_t)K, M, N, K, K, K, static_cast<float*>(g), (int64_t)N, partials, nullptr, (int64_t)0,
                        nullptr, ex);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+// BM of the EPI_EDZ launch: 64-row tiles when 128-row ones would leave fewer
+// than 512 workgroups (launch_gemm_lds's skinny rule)
+inline int edz_bm(int M, int N) {
+    const int bn = N > 64 ? 128 : 64;
+    return (int64_t)((M + G2_BM - 1) / G2_BM) * ((N + bn - 1) / bn) < 512 ? 64 : G2_BM;
+}
+
+int dgx_gemm_edge_dz_rows(int M, int N) {
+    if (M < 1 || N < 1) return DGX_EINVAL;
+    return (M + edz_bm(M, N) - 1) / edz_bm(M, N);
+}
+
+int dgx_gemm_edge_dz_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, int M, int N, int K,
+                          const float* addend, int64_t ldd, const float* ysel, const uint8_t* arg, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, float slope, float* dz,
+                          float* partials, int nrows, void* stream) {
+    if (!A || !W || !addend || !ysel || !arg || !scale || !shift || !mean || !invstd || !dz || !partials)
+        return DGX_EINVAL;
+    if (M < 1 || N < 1 || K < 1 || nrows != dgx_gemm_edge_dz_rows(M, N)) return DGX_EINVAL;
+    if (N % 8 || N > 128 || K % G2_BK || ldd % 4 || !aligned_to(A, 16) || !aligned_to(W, 16) || lda % 8 ||
+        ldw % 8 || !aligned_to(addend, 16) || !aligned_to(ysel, 16) || !aligned_to(arg, 4) || !aligned_to(dz, 16) ||
+        !aligned_to(scale, 16) || !aligned_to(shift, 16) || !aligned_to(mean, 16) || !aligned_to(invstd, 16))
+        return DGX_EUNSUPPORTED;
+    EpiEdge ex{};
+    ex.PQ = ysel;
+    ex.ldpq = N;
+    ex.scale = scale;
+    ex.shift = shift;
+    ex.mean = mean;
+    ex.invstd = invstd;
+    ex.slope = slope;
+    const bf16* a = static_cast<const bf16*>(A);
+    const bf16* b = static_cast<const bf16*>(W);
+    hipStream_t st = dgx_stream(stream);
+    const int bm = edz_bm(M, N);
+    const int nI = (M + bm - 1) / bm;
+#define DGX_EDZ(BMV, BNV)                                                                                        \
+    hipLaunchKernelGGL((gemm_lds_kernel<false, BMV, BNV, EPI_EDZ>), dim3((unsigned)(nI * ((N + BNV - 1) / BNV))), \
+                       dim3(GB_THREADS), 0, st, a, lda, b, ldw, M, N, K, K, K, dz, (int64_t)N, partials, addend, ldd, \
+                       arg, ex)
+    if (N > 64) {
+        if (bm == 64) DGX_EDZ(64, 128);
+        else DGX_EDZ(G2_BM, 128);
+    } else {
+        if (bm == 64) DGX_EDZ(64, 64);
+        else DGX_EDZ(G2_BM, 64);
+    }
+#undef DGX_EDZ
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

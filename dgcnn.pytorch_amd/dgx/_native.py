@@ -81,6 +81,9 @@ _SIGS = {
     "dgx_to_bf16": [_vp, _i64, _i64, _i32, _vp, _vp],
     "dgx_gemm_stats_rows": [_i32],
     "dgx_gemm_splits": [_i32, _i32, _i32],
+    "dgx_gemm_edge_dz_rows": [_i32, _i32],
+    "dgx_gemm_edge_dz_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _f32,
+                              _vp, _vp, _i32, _vp],
     "dgx_gemm_bf16": [_vp, _i32, _i32, _i64, _vp, _i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp,
                       _vp],
     "dgx_gemm_f32": [_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp],

@@ -59,6 +59,10 @@ FOLD_BN_FWD = os.environ.get("DGX_FOLD_BN_FWD", "0") == "1"
 # image and |x|^2 (dgx_bn_lrelu_apply_knn_image_f32), so that kNN skips its
 # prepare pass (DGX_FUSE_KNN_IMAGE=0: separate prepare pass, A/B only)
 FUSE_KNN_IMAGE = os.environ.get("DGX_FUSE_KNN_IMAGE", "1") == "1"
+# bf16 backward: block l's input-gradient GEMM applies block l-1's LeakyReLU'
+# in its epilogue and writes that block's packed dz + BN partials
+# (dgx_gemm_edge_dz_bf16) instead of dY (DGX_FUSE_EDGE_DZ=0: dY + a dz pass)
+FUSE_EDGE_DZ = os.environ.get("DGX_FUSE_EDGE_DZ", "1") == "1"
 
 
 def debug_capture():
@@ -303,6 +307,7 @@ class _EdgeConvStack(torch.autograd.Function):
         for idx in (st[0] for st in ctx.layer_state):
             assert idx.dtype == torch.int32 and idx.is_contiguous()
         rev = _reverse_graphs([st[0] for st in ctx.layer_state], B, N, k, dev)
+        fused_dz = {}   # block -> (packed dz, partials, rows) made by the next block's dX GEMM
         for li in reversed(range(nl)):
             ly = layers[li]
             cin, co = ly.cin, ly.cout
@@ -316,16 +321,23 @@ class _EdgeConvStack(torch.autograd.Function):
                 dY, ldy = dnew[:, off:off + co], dnew.stride(0)
             else:
                 dY, ldy = dxcat[:, off:off + co], dxcat.stride(0)
-            nblk = max(1, min(1024, (M + 63) // 64))
-            dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dL/dz at the selected edge
-            partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
+            pre = fused_dz.pop(li, None)
+            if pre is not None:   # dz + partials already made by block li+1's dX GEMM epilogue
+                dz, partials, nblk = pre
+                dY = None
+            else:
+                nblk = max(1, min(1024, (M + 63) // 64))
+                dz = torch.empty((M, co), dtype=torch.float32, device=dev)  # dL/dz at the selected edge
+                partials = torch.empty((nblk, 2, co), dtype=torch.float32, device=dev)
             # dPQ only feeds the GEMMs: bf16 (what the GEMM would round it to) in bf16 mode
             dPQ = torch.empty((M, 2 * co), dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
             with torch.cuda.device(dev):
                 bn_args = (M, co, nat.f32(st.scale), nat.f32(st.shift), nat.f32(st.mean), nat.f32(st.invstd),
                            float(ly.slope), nat.f32(dz), nat.f32(partials), nblk, stream)
                 packed = bf16 and SCATTER_PACKED
-                if packed:
+                if pre is not None:
+                    pass
+                elif packed:
                     # dz words carry the selected slot in their 6 low mantissa bits (the
                     # dPQ they feed is rounded to bf16): one LDS word per in-edge-channel
                     nat.check(L.dgx_edge_bwd_dz_packed_f32(nat.f32(dY), ldy, nat.f32(ysel), nat.u8(arg), *bn_args),
@@ -355,7 +367,7 @@ class _EdgeConvStack(torch.autograd.Function):
                         nat.f32(PQ), PQ.stride(0), nat.i32(rowptr), nat.i32(edges), nat.f32(dz), nat.u8(arg),
                         nat.f32(sumP), *common), "edge bwd scatter")
             if dbg is not None:
-                dbg[li] = {"dY": dY.clone(), "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
+                dbg[li] = {"dY": dY.clone() if dY is not None else None, "dz": dz.clone(), "dgamma": dgamma.clone(), "dbeta": dbeta.clone(),
                            "c0": c0.clone(), "c1": c1.clone(), "dPQ": dPQ.float(), "partials": partials.clone(),
                            "ysel": ysel.clone(), "scale": st.scale.clone(), "shift": st.shift.clone(),
                            "arg": arg.clone(), "idx": idx.clone(), "PQ": PQ.clone(), "sumP": sumP.clone(),
@@ -374,7 +386,12 @@ class _EdgeConvStack(torch.autograd.Function):
                 if li > 0:
                     dst = dnew[:, prev:prev + cin]
                     add = dxcat[:, prev:prev + cin]
-                    if wprep is not None:
+                    prev_state = ctx.layer_state[li - 1]
+                    if wprep is not None and FUSE_EDGE_DZ and packed and prev_state is not None and cin % 8 == 0:
+                        _, _, ysel_p, arg_p, _, st_p, _ = prev_state
+                        fused_dz[li - 1] = G.lds_xwt_edge_dz(dPQ, wprep[1], add, ysel_p, arg_p, st_p,
+                                                             layers[li - 1].slope)
+                    elif wprep is not None:
                         G.lds_xwt(dPQ, wprep[1], out=dst, addend=add)
                     else:
                         dst.copy_(add)

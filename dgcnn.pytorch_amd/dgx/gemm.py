@@ -285,6 +285,27 @@ def lds_xwt(x16, w16, out=None, stats=False, accumulate=False, addend=None, out_
     return (out, part) if stats else out
 
 
+def lds_xwt_edge_dz(x16, w16, addend, ysel, arg, st, slope):
+    """dY = addend + x16 @ w16^T with the previous EdgeConv block's LeakyReLU'
+    applied in the epilogue (dgx_gemm_edge_dz_bf16): returns (packed dz|slot
+    words (M, N) fp32, column partials (rows, 2, N), rows) — what
+    dgx_edge_bwd_dz_packed_f32 would make from the stored dY."""
+    M, K = x16.shape
+    N = w16.shape[0]
+    L = nat.lib()
+    rows = L.dgx_gemm_edge_dz_rows(M, N)
+    dz = torch.empty((M, N), dtype=torch.float32, device=x16.device)
+    part = torch.empty((rows, 2, N), dtype=torch.float32, device=x16.device)
+    if addend.dtype != torch.float32 or addend.stride(1) != 1:
+        raise RuntimeError("dgx gemm: addend must be a row-major fp32 view")
+    with torch.cuda.device(x16.device), _Timed(2.0 * M * N * K):
+        nat.check(L.dgx_gemm_edge_dz_bf16(
+            nat.ptr(x16), _bf16_2d(x16), nat.ptr(w16), _bf16_2d(w16), M, N, K, nat.f32(addend), addend.stride(0),
+            nat.f32(ysel), nat.u8(arg), nat.f32(st.scale), nat.f32(st.shift), nat.f32(st.mean), nat.f32(st.invstd),
+            float(slope), nat.f32(dz), nat.f32(part), rows, nat.stream_of(x16)), "gemm edge dz")
+    return dz, part, rows
+
+
 def lds_atb(a16, b16, out, split_rows=None):
     """out = a16^T @ b16 for a16 (R, M), b16 (R, N) bf16 (reduction over R rows,
     split-K slabs summed deterministically); ``split_rows`` as in mm_atb."""

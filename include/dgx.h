@@ -406,6 +406,20 @@ int dgx_slab_reduce_f32(const float* slab, int S, int rows, int cols, int split,
  * a_k (tn = 0): A's k extent; 0 or K for a plain GEMM, K/2 for a split weight
  * B = [W_hi | W_lo] (N x K, W_lo = bf16(W - W_hi)): C = A W_hi^T + A W_lo^T,
  * i.e. the weight operand carries 16 significant bits (a_k % 64 == 0). */
+/* EdgeConv backward, bf16 mode: block l's input-gradient GEMM dY_{l-1} =
+ * addend + A W^T (A = dPQ_l (M x K) bf16, W = [W1;W2]^T (N x K) bf16, addend =
+ * the incoming gradient of the concat slice, ld ldd) whose epilogue applies
+ * block l-1's LeakyReLU' instead of storing dY: dz = dY * LReLU'(scale*ysel +
+ * shift) written as packed dz|slot words (dgx_edge_bwd_dz_packed_f32's format,
+ * arg = block l-1's selected slots) with per-tile column partials (sum dz,
+ * sum dz*yhat), nrows = dgx_gemm_edge_dz_rows(M, N) — no dY round trip and no
+ * separate dz pass. N <= 128, N % 8 == 0, K % 64 == 0. */
+int dgx_gemm_edge_dz_rows(int M, int N);
+int dgx_gemm_edge_dz_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, int M, int N, int K,
+                          const float* addend, int64_t ldd, const float* ysel, const uint8_t* arg,
+                          const float* scale, const float* shift, const float* mean,
+                          const float* invstd, float slope, float* dz, float* partials, int nrows,
+                          void* stream);
 int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int tn,
                       int M, int N, int K, int a_k, int epi, int splits, float* C,
                       int64_t ldc, float* partials, const float* addend,

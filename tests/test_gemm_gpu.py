@@ -286,3 +286,37 @@ def test_smallk_split_weight(cuda, M, Co, K):
     w2 = w.reshape(Co, 2 * K).double()
     exact = x.double() @ torch.cat([w2[:, :K], w2[:, K:]], 0).t()
     assert rel_err(out.cpu(), exact.cpu()) < 1e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 64, 128), (32768, 128, 512), (4000, 64, 256), (8192, 128, 256)])
+def test_gemm_edge_dz_epilogue(cuda, M, N, K):
+    """dgx_gemm_edge_dz_bf16 = the EdgeConv input-gradient GEMM (addend + A W^T)
+    followed by dgx_edge_bwd_dz_packed_f32 on its output: the packed dz|slot
+    words bit for bit, the BN-backward column partials (other summation order)
+    to 1e-5 of their sums."""
+    from dgx import _native as nat
+    from dgx import bn as bn_
+    from dgx import gemm as G
+    g = torch.Generator().manual_seed(M + N + K)
+    a16 = torch.randn(M, K, generator=g).to(cuda).bfloat16()
+    w16 = torch.randn(N, K, generator=g).to(cuda).bfloat16()
+    big = torch.randn(M, N + 24, generator=g).to(cuda)
+    add = big[:, 8:8 + N]
+    ysel = torch.randn(M, N, generator=g).to(cuda)
+    arg = torch.randint(0, 20, (M, N), generator=g, dtype=torch.uint8).to(cuda)
+    st = bn_.Stats(*(torch.randn(N, generator=g).to(cuda) for _ in range(4)), None, False)
+    dz, part, rows = G.lds_xwt_edge_dz(a16, w16, add, ysel, arg, st, 0.2)
+    dY = torch.empty(M, N, device=cuda)
+    G.lds_xwt(a16, w16, out=dY, addend=add)
+    nblk = max(1, min(1024, (M + 63) // 64))
+    dz_ref = torch.empty(M, N, device=cuda)
+    part_ref = torch.empty(nblk, 2, N, device=cuda)
+    L = nat.lib()
+    nat.check(L.dgx_edge_bwd_dz_packed_f32(nat.f32(dY), N, nat.f32(ysel), nat.u8(arg), M, N, nat.f32(st.scale),
+                                           nat.f32(st.shift), nat.f32(st.mean), nat.f32(st.invstd), 0.2,
+                                           nat.f32(dz_ref), nat.f32(part_ref), nblk, nat.stream_of(dY)), "dz")
+    torch.cuda.synchronize()
+    assert torch.equal(dz.view(torch.int32), dz_ref.view(torch.int32))
+    s, s_ref = part.double().sum(0), part_ref.double().sum(0)
+    scale = part_ref.double().abs().sum(0)
+    assert float(((s - s_ref).abs() / scale.clamp_min(1e-30)).max()) < 1e-5
