@@ -186,11 +186,17 @@ __device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (ro
 constexpr int KI_TILES = 1;  // tiles per image-builder block
 // One pass over x per layer: the operand image, the |x|^2 image and xx itself
 // (|x_i|^2 in the reference's rounding order, sqnorm_sum on the staged row).
+// Optional (Wref != nullptr, C <= 16): also the EdgeConv PQ rows of the block's
+// points, PQ[n] = x_n [W1; W2]^T for a reference conv weight Wref (Co, 2C) =
+// [W1 | W2], each output the fmaf chain over c of dgx_gemm_smallk_f32 (the
+// first block reads the cloud once for its kNN operands and its PQ GEMM).
 template <int NSTEP>
 __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
                                                         int64_t sN, int B, int C, int N, int order, int ntile,
                                                         int tgroups, float* __restrict__ xx,
-                                                        float* __restrict__ img, float* __restrict__ xximg) {
+                                                        float* __restrict__ img, float* __restrict__ xximg,
+                                                        const float* __restrict__ Wref = nullptr, int Co = 0,
+                                                        float* __restrict__ PQ = nullptr, int ldpq = 0) {
 #pragma clang fp contract(off)
     constexpr int CP = NSTEP * 4;
     constexpr int P = 16 * KI_TILES;
@@ -215,6 +221,24 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
         const int r = e - tl * 64 * NSTEP;
         const int l = r / NSTEP, st = r - l * NSTEP;
         dst[e] = rows[tl * 16 + knn_cand(l & 15)][4 * st + (l >> 4)];
+    }
+    if (Wref) {   // PQ rows: thread = (point, 4 consecutive outputs), 16-B stores along the row
+        const int nq = Co >> 1;   // 2Co / 4 output quads per point
+        for (int e = t; e < P * nq; e += 256) {
+            const int pl = e / nq, o = (e - pl * nq) * 4;
+            const int n = s0 * 16 + pl;
+            if (n >= N) continue;
+            float acc[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = o + u;
+                const float* __restrict__ wr = Wref + (r < Co ? r : r - Co) * 2 * C + (r < Co ? 0 : C);
+                float a = 0.f;
+                for (int c = 0; c < C; ++c) a = fmaf(rows[pl][c], wr[c], a);
+                acc[u] = a;
+            }
+            *reinterpret_cast<float4*>(PQ + ((int64_t)b * N + n) * ldpq + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
     }
     __syncthreads();
     if (t < P) {  // each thread squares its own row in place, then sums it in the reference order
@@ -1548,6 +1572,23 @@ size_t dgx_knn_workspace_bytes(int B, int C, int N) {
     if (B < 0 || C < 1 || N < 1) return 0;
     // |x|^2 (B*N floats, rounded up to 16 bytes) | operand image
     return ((((size_t)B * N + 3) & ~(size_t)3) * sizeof(float)) + dgx_knn_image_bytes(B, C, N);
+}
+
+int dgx_knn_prepare_pq_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order,
+                           float* xx, void* image, size_t image_bytes, const float* Wref, int Co, float* PQ,
+                           int ldpq, void* stream) {
+    if (!x || !xx || !Wref || !PQ || B < 1 || C < 1 || N < 1 || Co < 2) return DGX_EINVAL;
+    if (knn_nstep(C) != 1 || Co % 2 || ldpq % 4 || ldpq < 2 * Co || reinterpret_cast<uintptr_t>(PQ) % 16)
+        return DGX_EUNSUPPORTED;
+    if (!image || image_bytes < dgx_knn_image_bytes(B, C, N) || (reinterpret_cast<uintptr_t>(image) & 15) != 0)
+        return DGX_EINVAL;
+    float* img = static_cast<float*>(image);
+    float* xximg = img + (size_t)B * knn_image_floats(C, N);
+    const int ntile = knn_ntile(N);
+    const int tgroups = (ntile + KI_TILES - 1) / KI_TILES;
+    hipLaunchKernelGGL(knn_image_kernel<1>, dim3((unsigned)(B * tgroups)), dim3(256), 0, dgx_stream(stream), x, sB, sC,
+                       sN, B, C, N, order, ntile, tgroups, xx, img, xximg, Wref, Co, PQ, ldpq);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order,

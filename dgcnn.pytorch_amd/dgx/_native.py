@@ -32,6 +32,8 @@ _SIGS = {
     "dgx_knn_kernel_name": [_i32, _i32, _i32],
     "dgx_knn_set_variant": [_i32],
     "dgx_bn_lrelu_apply_knn_image_f32": [_vp, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _sz, _vp],
+    "dgx_knn_prepare_pq_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp, _i32, _vp, _i32,
+                               _vp],
     "dgx_knn_prepare_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp],
     "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
     "dgx_sqnorm_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp],

@@ -63,6 +63,12 @@ FUSE_KNN_IMAGE = os.environ.get("DGX_FUSE_KNN_IMAGE", "1") == "1"
 # in its epilogue and writes that block's packed dz + BN partials
 # (dgx_gemm_edge_dz_bf16) instead of dY (DGX_FUSE_EDGE_DZ=0: dY + a dz pass)
 FUSE_EDGE_DZ = os.environ.get("DGX_FUSE_EDGE_DZ", "1") == "1"
+# block 1: the kNN prepare pass over the xyz cloud also writing the PQ rows
+# (dgx_knn_prepare_pq_f32). Off: measured 1.351 -> 1.364 ms/step at cfg2 with
+# it on (the 16-point image blocks write the 128-wide PQ rows on the critical
+# path before the kNN; the separate small-K GEMM runs wider). DGX_FUSE_BLOCK1_PQ=1
+# turns it on (A/B only; bitwise-equal outputs, tests/test_knn_gpu.py).
+FUSE_BLOCK1_PQ = os.environ.get("DGX_FUSE_BLOCK1_PQ", "0") == "1"
 
 
 def debug_capture():
@@ -188,9 +194,21 @@ class _EdgeConvStack(torch.autograd.Function):
         for li, ly in enumerate(layers):
             w, gamma, beta = params[3 * li: 3 * li + 3]
             cin, co = ly.cin, ly.cout
+            PQ = None
             if li == 0:
                 X = x_pm
-                idx = knn_raw(x, k, order=reduction_order(x), out_dtype=torch.int32)
+                order0 = reduction_order(x)
+                prep0 = None
+                if FUSE_BLOCK1_PQ and cin <= G.SMALLK_MAX and C0 <= 4 and w.is_contiguous():
+                    # one pass over the cloud: kNN operand image, |x|^2 and the PQ rows
+                    prep0 = knn_image_buffers(B, C0, N, dev)
+                    PQ = torch.empty((M, 2 * ly.cout), dtype=torch.float32, device=dev)
+                    with torch.cuda.device(dev):
+                        nat.check(L.dgx_knn_prepare_pq_f32(
+                            nat.f32(x), *x.stride(), B, C0, N, order0, nat.f32(prep0[0]), nat.f32(prep0[1]),
+                            prep0[1].numel() * 4, nat.f32(w), ly.cout, nat.f32(PQ), 2 * ly.cout, stream),
+                            "knn prepare + PQ")
+                idx = knn_raw(x, k, order=order0, out_dtype=torch.int32, prepared=prep0)
             else:
                 X = xcat[:, off_in:off_in + cin]
                 # the reference's blocks 2-4 see contiguous (B,C,N) features (max over
@@ -203,7 +221,9 @@ class _EdgeConvStack(torch.autograd.Function):
                               seeds=idx if KNN_SEEDS else None, prepared=next_prepared)
             next_prepared = None
             wprep = None
-            if cin <= G.SMALLK_MAX:
+            if PQ is not None:
+                pass   # block 1's PQ came with its kNN operands
+            elif cin <= G.SMALLK_MAX:
                 # raw coordinates (block 1, K = 3): exact fp32 in every mode
                 PQ = G.mm_smallk_split(X, w, co)
             elif bf16:

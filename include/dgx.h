@@ -86,6 +86,13 @@ int dgx_bn_lrelu_apply_knn_image_f32(const float* ysel, int B, int N, int Co,
 void dgx_knn_set_variant(int knn3);
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                    int B, int C, int N, int order, float* xx, void* stream);
+/* dgx_knn_prepare_f32 for a coordinate cloud (C <= 4) that also writes the
+ * first EdgeConv block's PQ = X [W1; W2]^T (M x 2Co, row stride ldpq) from the
+ * reference conv weight Wref (Co, 2C) = [W1 | W2] (dgcnn.py:55), each output
+ * exactly dgx_gemm_smallk_split_f32's: the cloud is read once for both. */
+int dgx_knn_prepare_pq_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C,
+                           int N, int order, float* xx, void* image, size_t image_bytes,
+                           const float* Wref, int Co, float* PQ, int ldpq, void* stream);
 int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                         int B, int C, int N, int order, float* xx,
                         void* image, size_t image_bytes, void* stream);

@@ -297,3 +297,28 @@ def test_apply_writes_next_knn_image(cuda, B, N, Co):
     a = knn_raw(xcat[:, off:], 20, prepared=(xx, img), **kw)
     b = knn_raw(xcat[:, off:], 20, **kw)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,N,Co,layout", [(32, 1024, 64, "perm"), (3, 777, 24, "bcn"), (2, 2048, 64, "perm")])
+def test_prepare_with_block1_pq(cuda, B, N, Co, layout):
+    """dgx_knn_prepare_pq_f32: the kNN operands of a coordinate cloud equal
+    dgx_knn_prepare_f32's and its PQ rows equal dgx_gemm_smallk_split_f32's,
+    bit for bit."""
+    from dgx import _native as nat
+    from dgx import gemm as G
+    from dgx.ops import knn_image_buffers, reduction_order
+    L = nat.lib()
+    x = _view(synth.cube_clouds(B, N, N + Co), layout, cuda)
+    w = torch.randn(Co, 6, 1, 1, generator=torch.Generator().manual_seed(Co)).to(cuda)
+    order = reduction_order(x)
+    st = nat.stream_of(x)
+    xx1, img1 = knn_image_buffers(B, 3, N, cuda)
+    xx2, img2 = knn_image_buffers(B, 3, N, cuda)
+    pq = torch.empty(B * N, 2 * Co, device=cuda)
+    nat.check(L.dgx_knn_prepare_f32(nat.f32(x), *x.stride(), B, 3, N, order, nat.f32(xx1), nat.f32(img1),
+                                    img1.numel() * 4, st), "prepare")
+    nat.check(L.dgx_knn_prepare_pq_f32(nat.f32(x), *x.stride(), B, 3, N, order, nat.f32(xx2), nat.f32(img2),
+                                       img2.numel() * 4, nat.f32(w), Co, nat.f32(pq), 2 * Co, st), "prepare pq")
+    ref = G.mm_smallk_split(x.permute(0, 2, 1).reshape(B * N, 3), w, Co)
+    assert torch.equal(xx1, xx2) and torch.equal(img1, img2)
+    assert torch.equal(pq.view(torch.int32), ref.view(torch.int32))
