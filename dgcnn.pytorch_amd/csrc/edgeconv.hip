@@ -1075,7 +1075,12 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float kf = (float)k;
     const int32_t ibase = (int32_t)base;
     __syncthreads();
-    for (int r = t; r < np; r += EC_THREADS) {
+    // boustrophedon deal of the degree-sorted points: pass 2p takes ranks
+    // t, pass 2p+1 ranks from the far end, so a thread's in-degree total (and a
+    // wave's longest lane) is balanced instead of wave 0 holding every hub
+    for (int it = 0; it * EC_THREADS < np; ++it) {
+        const int r = it * EC_THREADS + ((it & 1) ? EC_THREADS - 1 - t : t);
+        if (r >= np) continue;
         const int n = n_beg + order[r];
         const int64_t j = base + n;
         const int32_t beg = rowptr[j], end = rowptr[j + 1];
