@@ -306,6 +306,11 @@ def lds_xwt_edge_dz(x16, w16, addend, ysel, arg, st, slope):
     return dz, part, rows
 
 
+# cap (MiB) on the split-K slab of the bf16 weight-gradient GEMMs (0: the
+# library's split rule, dgx_gemm_splits)
+SLAB_CAP_MB = int(__import__("os").environ.get("DGX_SLAB_CAP_MB", "0"))
+
+
 def lds_atb(a16, b16, out, split_rows=None):
     """out = a16^T @ b16 for a16 (R, M), b16 (R, N) bf16 (reduction over R rows,
     split-K slabs summed deterministically); ``split_rows`` as in mm_atb."""
@@ -315,6 +320,8 @@ def lds_atb(a16, b16, out, split_rows=None):
         raise RuntimeError("dgx gemm: output must be a row-major fp32 view")
     L = nat.lib()
     S = L.dgx_gemm_splits(M, N, R)
+    if SLAB_CAP_MB > 0 and M * N * 4 < (1 << 20):   # bound the slab traffic of small outputs (A/B knob)
+        S = max(1, min(S, (SLAB_CAP_MB << 20) // (M * N * 4)))
     chunk = -(-R // S)
     chunk = -(-chunk // 64) * 64
     used = -(-R // chunk)
