@@ -306,9 +306,11 @@ def lds_xwt_edge_dz(x16, w16, addend, ysel, arg, st, slope):
     return dz, part, rows
 
 
-# cap (MiB) on the split-K slab of the bf16 weight-gradient GEMMs (0: the
-# library's split rule, dgx_gemm_splits)
-SLAB_CAP_MB = int(__import__("os").environ.get("DGX_SLAB_CAP_MB", "0"))
+# cap (MiB) on the split-K slab of the small bf16 weight-gradient GEMMs (output
+# < 1 MiB: the EdgeConv blocks' dW; 0: dgx_gemm_splits's rule). 8: block 4's dW
+# takes 32 splits instead of 128 (33.5 -> 8.4 MB of slab); measured at cfg2
+# 1.3442 -> 1.3384 ms/step (2 / 4 MB: 1.401 / 1.359, too few workgroups)
+SLAB_CAP_MB = int(__import__("os").environ.get("DGX_SLAB_CAP_MB", "8"))
 
 
 def lds_atb(a16, b16, out, split_rows=None):
