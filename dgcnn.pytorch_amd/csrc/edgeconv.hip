@@ -181,54 +181,12 @@ __device__ __forceinline__ void stage_slice(float* __restrict__ dst, const float
     }
 }
 
-// BN batch-statistics finalize folded into the gather launch (no separate
-// dgx_bn_finalize launch): each workgroup publishes its partial row with
-// write-through (sc1) stores, drains them, and draws a ticket from its channel
-// slice's counter; the slice's last arriver (ticket B*nparts-1) acquires,
-// reduces the slice's partial rows in one fixed order (fp64, independent of
-// which workgroup arrives last) and writes scale / shift / mean / invstd and
-// the running statistics (cdna_hip_programming.md Guideline 16, counter form).
-// The counters (one int per slice) are zero before the launch and the last
-// arriver resets its own, so they stay zero between launches.
-struct BnFwdFin {
-    int* counter;            // nullptr: partials only (separate finalize)
-    double count;
-    const float* gamma;
-    const float* beta;
-    float* rmean;
-    float* rvar;
-    double momentum;
-    double eps;
-    float* scale;
-    float* shift;
-    float* mean;
-    float* invstd;
-    int64_t* nbt;
-};
-
-__device__ __forceinline__ void bn_finalize_channel(const BnFwdFin& f, int o, double s1, double s2) {
-    const double mean = s1 / f.count;
-    double var = s2 / f.count - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const double invstd = 1.0 / sqrt(var + f.eps);
-    const double a = (f.gamma ? (double)f.gamma[o] : 1.0) * invstd;
-    f.scale[o] = (float)a;
-    f.shift[o] = (float)((f.beta ? (double)f.beta[o] : 0.0) - mean * a);
-    if (f.mean) f.mean[o] = (float)mean;
-    if (f.invstd) f.invstd[o] = (float)invstd;
-    if (f.rmean) f.rmean[o] = (float)((1.0 - f.momentum) * (double)f.rmean[o] + f.momentum * mean);
-    if (f.rvar) {
-        const double unbiased = f.count > 1.0 ? var * f.count / (f.count - 1.0) : var;
-        f.rvar[o] = (float)((1.0 - f.momentum) * (double)f.rvar[o] + f.momentum * unbiased);
-    }
-}
-
 template <int CS, bool EVAL>
 __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, int B, int N, int k, int Co, int nparts,
     const float* __restrict__ sel_sign, const float* __restrict__ shift, float slope, float* __restrict__ ysel,
     uint8_t* __restrict__ arg, float* __restrict__ sumP, float* __restrict__ partials, float* __restrict__ out,
-    int ldo, BnFwdFin fin) {
+    int ldo) {
     constexpr int TPP = SliceSplit<CS>::TPP, V = SliceSplit<CS>::V;
     extern __shared__ float lds[];  // [N][CS] slice of P | idx rows of a pass; then the stat reduction
     int b, part, slice;
@@ -389,77 +347,8 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
             r1 += red[(2 * uc) * EC_THREADS + w];
             r2 += red[(2 * uc + 1) * EC_THREADS + w];
         }
-        // write-through (sc1) stores: the slice's last arriver may sit on another XCD
-        __hip_atomic_store(&partials[(int64_t)prow * 2 * Co + o0 + t], r1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&partials[(int64_t)prow * 2 * Co + Co + o0 + t], r2, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!fin.counter) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
-    __syncthreads();
-    int* last_flag = reinterpret_cast<int*>(lds);
-    if (t == 0) {
-        const int ticket = __hip_atomic_fetch_add(&fin.counter[slice], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = ticket == B * nparts - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&fin.counter[slice], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        last_flag[0] = last;
-    }
-    __syncthreads();
-    if (!last_flag[0]) return;
-    // last arriver: rows g, g + G, ... of channel o0 + t % CS per thread (fp64), lanes with
-    // the same channel combined by xor shuffles, then the waves in order
-    {
-        constexpr int G = EC_THREADS / CS;
-        const int c = t % CS, g = t / CS, o = o0 + c;
-        const int R = B * nparts;
-        double s1 = 0.0, s2 = 0.0;
-        if (o < Co) {
-            const float* __restrict__ pp = partials + o;
-            int r = g;
-            for (; r + 3 * G < R; r += 4 * G) {
-                float v1[4], v2[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    v1[u] = pp[(int64_t)(r + u * G) * 2 * Co];
-                    v2[u] = pp[(int64_t)(r + u * G) * 2 * Co + Co];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    s1 += (double)v1[u];
-                    s2 += (double)v2[u];
-                }
-            }
-            for (; r < R; r += G) {
-                s1 += (double)pp[(int64_t)r * 2 * Co];
-                s2 += (double)pp[(int64_t)r * 2 * Co + Co];
-            }
-        }
-#pragma unroll
-        for (int m = CS; m < 64; m <<= 1) {
-            s1 += __shfl_xor(s1, m);
-            s2 += __shfl_xor(s2, m);
-        }
-        double* wsum = reinterpret_cast<double*>(lds) + 2;   // [wave][2][CS] (after the flag)
-        const int lane = t & 63, wv = t >> 6;
-        if (lane < CS) {
-            wsum[(wv * 2) * CS + lane] = s1;
-            wsum[(wv * 2 + 1) * CS + lane] = s2;
-        }
-        __syncthreads();
-        if (t < CS && o0 + t < Co) {
-            double r1 = 0.0, r2 = 0.0;
-            for (int w = 0; w < EC_THREADS / 64; ++w) {
-                r1 += wsum[(w * 2) * CS + t];
-                r2 += wsum[(w * 2 + 1) * CS + t];
-            }
-            bn_finalize_channel(fin, o0 + t, r1, r2);
-            if (fin.nbt && slice == 0 && t == 0) *fin.nbt += 1;
-        }
+        partials[(int64_t)prow * 2 * Co + o0 + t] = r1;
+        partials[(int64_t)prow * 2 * Co + Co + o0 + t] = r2;
     }
 }
 
@@ -494,6 +383,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ 
     // count < 0: the element count follows the sums on the device (SyncBatchNorm:
     // all-reduced with them, never read back to the host)
     if (count < 0.0) count = (double)partials[(int64_t)nrows * 2 * Co];
+    // momentum < 0: nn.BatchNorm's cumulative average (momentum=None), factor
+    // 1 / (num_batches_tracked + 1) read here instead of on the host (the
+    // counter input is only read: the caller passes a separate nbt_new)
+    if (momentum < 0.0) momentum = nbt ? 1.0 / (double)(*nbt + 1) : 0.0;
     const double mean = r1[0] / count;
     double var = r2[0] / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -1199,11 +1092,11 @@ template <bool EVAL>
 int launch_gather(int cs, dim3 grid, size_t lds, hipStream_t st, const float* PQ, int ldpq, const int32_t* idx, int B,
                   int N,
                   int k, int Co, int nparts, const float* sel, const float* shift, float slope, float* ysel,
-                  uint8_t* arg, float* sumP, float* partials, float* out, int ldo, const BnFwdFin& fin = BnFwdFin{}) {
+                  uint8_t* arg, float* sumP, float* partials, float* out, int ldo) {
 #define DGX_GATHER_CASE(CSV)                                                                                      \
     case CSV:                                                                                                    \
         hipLaunchKernelGGL((edge_gather_lds_kernel<CSV, EVAL>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, idx, B, \
-                           N, k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo, fin);        \
+                           N, k, Co, nparts, sel, shift, slope, ysel, arg, sumP, partials, out, ldo);             \
         break;
     switch (cs) {
         DGX_GATHER_CASE(32)
@@ -1231,9 +1124,7 @@ inline GatherGeom gather_geom(int B, int N, int Co) {
     size_t stage = (size_t)N * g.cs * sizeof(float) + GF_ICAP * sizeof(int);
     const int v = g.cs >= 4 ? g.cs / 4 : 1;
     size_t red = (size_t)2 * v * EC_THREADS * sizeof(float);
-    const size_t fin = 16 + (size_t)(EC_THREADS / 64) * 2 * g.cs * sizeof(double);   // last-arriver scratch
     g.lds = stage > red ? stage : red;
-    if (g.lds < fin) g.lds = fin;
     return g;
 }
 
@@ -1259,29 +1150,6 @@ int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx, int B
                                 g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials, nullptr, 0);
 }
 
-int dgx_edge_fwd_gather_counters(int B, int N, int Co) {
-    if (B < 1 || N < 1 || Co < 1) return DGX_EINVAL;
-    return gather_geom(B, N, Co).slices;
-}
-
-int dgx_edge_fwd_gather_bn_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int Co,
-                               const float* gamma, const float* beta, float* ysel, uint8_t* arg, float* sumP,
-                               float* partials, int nrows, int* counters, double count, float* running_mean,
-                               float* running_var, double momentum, double eps, float* scale, float* shift,
-                               float* mean, float* invstd, int64_t* num_batches_tracked, void* stream) {
-    if (!PQ || !idx || !gamma || !ysel || !arg || !sumP || !partials || !counters || !scale || !shift)
-        return DGX_EINVAL;
-    if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co || count <= 0.0) return DGX_EINVAL;
-    const GatherGeom g = gather_geom(B, N, Co);
-    if (nrows != B * g.parts) return DGX_EINVAL;
-    if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
-    const BnFwdFin fin{counters, count, gamma, beta, running_mean, running_var, momentum, eps,
-                       scale, shift, mean, invstd, num_batches_tracked};
-    return launch_gather<false>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
-                                ldpq, idx, B, N, k, Co, g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials,
-                                nullptr, 0, fin);
-}
-
 int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N, int k, int Co,
                           const float* scale, const float* shift, float slope, float* out, int ldo, void* stream) {
     if (!PQ || !idx || !scale || !shift || !out) return DGX_EINVAL;
@@ -1302,6 +1170,8 @@ int dgx_bn_finalize_out_f32(const float* partials, int nrows, int Co, double cou
     if ((running_mean && !running_mean_new) || (running_var && !running_var_new) ||
         (num_batches_tracked && !num_batches_tracked_new))
         return DGX_EINVAL;
+    // cumulative average: every block reads the counter, so it may not be updated in place
+    if (momentum < 0.0 && num_batches_tracked && num_batches_tracked == num_batches_tracked_new) return DGX_EINVAL;
     hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
                        count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
                        num_batches_tracked, running_mean_new, running_var_new, num_batches_tracked_new);
@@ -1326,6 +1196,8 @@ int dgx_bn_finalize_out_f64(const double* sums, int nrows, int Co, double count,
     if ((running_mean && !running_mean_new) || (running_var && !running_var_new) ||
         (num_batches_tracked && !num_batches_tracked_new))
         return DGX_EINVAL;
+    // cumulative average: every block reads the counter, so it may not be updated in place
+    if (momentum < 0.0 && num_batches_tracked && num_batches_tracked == num_batches_tracked_new) return DGX_EINVAL;
     hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
                        num_batches_tracked, running_mean_new, running_var_new, num_batches_tracked_new);

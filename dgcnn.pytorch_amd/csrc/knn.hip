@@ -36,12 +36,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-// knn3_kernel (VALU 3-channel selection) off by default: measured against the
-// MFMA selection kernel (tools/knn3_ab.py, identical outputs) at 53.8 vs 53.4 us
-// (B 32 N 1024 k 20), 235 vs 185 us (N 2048 k 40), 145 vs 127 us (N 2048 k 20);
-// PMC at cfg2: 16.9 M VALU instructions per launch (old 24.7 M) but 57 % VALU
-// issue — pass 1's v_med3 lists and ~38 insertion rounds per wave dominate.
-bool g_knn3_enabled = false;                     // dgx_knn_set_variant (A/B tools only)
 constexpr int KQ_GROUPS = 2;                    // query groups of 16 per block
 constexpr int KQ_HALVES = 2;                    // candidate halves: waves per query group
 constexpr int KQ_WAVES = KQ_GROUPS * KQ_HALVES;
@@ -186,17 +180,11 @@ __device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (ro
 constexpr int KI_TILES = 1;  // tiles per image-builder block
 // One pass over x per layer: the operand image, the |x|^2 image and xx itself
 // (|x_i|^2 in the reference's rounding order, sqnorm_sum on the staged row).
-// Optional (Wref != nullptr, C <= 16): also the EdgeConv PQ rows of the block's
-// points, PQ[n] = x_n [W1; W2]^T for a reference conv weight Wref (Co, 2C) =
-// [W1 | W2], each output the fmaf chain over c of dgx_gemm_smallk_f32 (the
-// first block reads the cloud once for its kNN operands and its PQ GEMM).
 template <int NSTEP>
 __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
                                                         int64_t sN, int B, int C, int N, int order, int ntile,
                                                         int tgroups, float* __restrict__ xx,
-                                                        float* __restrict__ img, float* __restrict__ xximg,
-                                                        const float* __restrict__ Wref = nullptr, int Co = 0,
-                                                        float* __restrict__ PQ = nullptr, int ldpq = 0) {
+                                                        float* __restrict__ img, float* __restrict__ xximg) {
 #pragma clang fp contract(off)
     constexpr int CP = NSTEP * 4;
     constexpr int P = 16 * KI_TILES;
@@ -221,24 +209,6 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
         const int r = e - tl * 64 * NSTEP;
         const int l = r / NSTEP, st = r - l * NSTEP;
         dst[e] = rows[tl * 16 + knn_cand(l & 15)][4 * st + (l >> 4)];
-    }
-    if (Wref) {   // PQ rows: thread = (point, 4 consecutive outputs), 16-B stores along the row
-        const int nq = Co >> 1;   // 2Co / 4 output quads per point
-        for (int e = t; e < P * nq; e += 256) {
-            const int pl = e / nq, o = (e - pl * nq) * 4;
-            const int n = s0 * 16 + pl;
-            if (n >= N) continue;
-            float acc[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int r = o + u;
-                const float* __restrict__ wr = Wref + (r < Co ? r : r - Co) * 2 * C + (r < Co ? 0 : C);
-                float a = 0.f;
-                for (int c = 0; c < C; ++c) a = fmaf(rows[pl][c], wr[c], a);
-                acc[u] = a;
-            }
-            *reinterpret_cast<float4*>(PQ + ((int64_t)b * N + n) * ldpq + o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        }
     }
     __syncthreads();
     if (t < P) {  // each thread squares its own row in place, then sums it in the reference order
@@ -411,16 +381,6 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
     __syncthreads();  // the fix-up area is free for the next row
 }
 
-// Admission seeds of a selection launch: a per-row lower bound T of the k-th
-// value (dgx_knn_seed_f32), and/or candidate ids whose exact distances the
-// kernel computes itself (the previous EdgeConv block's graph) — min over ks
-// distinct candidates is a lower bound of the row's k-th value when ks >= k.
-struct KnnSeed {
-    const float* T;        // (B*N) or nullptr
-    const int32_t* sidx;   // (B, N, ks) local ids or nullptr
-    int ks;
-};
-
 // ------------------------------------------------------------ knn kernel ----
 // Block = KQ_GROUPS wave groups x 2 candidate halves, one wave each; a wave
 // serves QG groups of 16 queries (QG = 2: 32 queries per wave, 64 per block).
@@ -445,7 +405,7 @@ template <int NSTEP, int KB, int QG>
 __global__ __launch_bounds__(KQ_THREADS, QG == 1 ? (KB <= 40 ? 4 : 2) : (KB <= 40 ? 2 : 1))
 void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, const float* __restrict__ xx, int B,
                 int N, int k, int nqb, int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
-                float* __restrict__ vals, const KnnSeed sd
+                float* __restrict__ vals
 #ifdef DGX_KNN_STATS
                 , uint32_t* __restrict__ stats
 #endif
@@ -514,10 +474,10 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
 #pragma unroll
         for (int t = 0; t < NSTEP; ++t) S.bq[t] *= 2.0f;
         S.xxq = S.q < N ? xx[(int64_t)b * N + S.q] : 0.f;
-        // admission seed (dgx_knn_seed_f32): a lower bound of the row's k-th
-        // value in this kernel's exact arithmetic, so candidates below it can
-        // never enter the top-k; -inf without seeds
-        S.tseed = (sd.T != nullptr && S.q < N) ? sd.T[(int64_t)b * N + S.q] : -INFINITY;
+        // admission seed: a lower bound of the row's k-th value in this
+        // kernel's exact arithmetic (the 3-channel pre-pass below), so
+        // candidates below it can never enter the top-k; -inf without one
+        S.tseed = -INFINITY;
         S.thr = S.tseed;
 #pragma unroll
         for (int t = 0; t < KL; ++t) { S.lv[t] = -INFINITY; S.li[t] = 0x7fffffff; }
@@ -615,72 +575,6 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         const float T = fminf(tm, pub[(1 - h) * QPB + G0.qq]);
         if (G0.q < N) G0.tseed = fmaxf(G0.tseed, T);
         G0.thr = G0.tseed;
-    }
-    if constexpr (NSTEP % 4 == 0) {
-        if (sd.sidx != nullptr) {
-            // Graph seeds: the exact distances of ks given candidates (distinct
-            // ids, e.g. the previous block's neighbours) in this kernel's own
-            // arithmetic — the fmaf chain over c = 0..C-1 of x_j[c] * 2 x_q[c]
-            // that the MFMA chain computes (padded channels add exact zeros),
-            // then (dot - |x_j|^2) - |x_q|^2 — so T = their min is a lower bound
-            // of the row's k-th value (ks >= k). The query's 8 lanes (4 here x
-            // 2 halves) take seeds s = 4h + g, 4h + g + 8, ...
-            each([&](Grp& S, int) {
-                float tl = INFINITY;
-                const int qs = min(S.q, N - 1);
-                const int32_t* sj = sd.sidx + ((int64_t)b * N + qs) * sd.ks;
-                constexpr int SPL = 3;   // seeds per lane for ks <= 24
-                int jj[SPL];
-                float dot[SPL];
-#pragma unroll
-                for (int u = 0; u < SPL; ++u) {
-                    const int si = 4 * h + g + 8 * u;
-                    jj[u] = si < sd.ks ? min(max(sj[si], 0), N - 1) : -1;
-                    dot[u] = 0.f;
-                }
-                auto row = [&](int j, int kk) {   // lane-run kk (channels 4t + kk) of candidate j
-                    return ib + ((int64_t)(j >> 4) * 64 + 16 * kk + knn_row(j & 15)) * NSTEP;
-                };
-#pragma unroll 1
-                for (int t0 = 0; t0 < NSTEP; t0 += 4) {
-                    float xq4[4][4];
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const float4 v = *reinterpret_cast<const float4*>(row(qs, kk) + t0);
-                        xq4[kk][0] = 2.f * v.x; xq4[kk][1] = 2.f * v.y; xq4[kk][2] = 2.f * v.z; xq4[kk][3] = 2.f * v.w;
-                    }
-#pragma unroll
-                    for (int u = 0; u < SPL; ++u) {
-                        if (jj[u] < 0) continue;
-                        float xj4[4][4];
-#pragma unroll
-                        for (int kk = 0; kk < 4; ++kk) {
-                            const float4 v = *reinterpret_cast<const float4*>(row(jj[u], kk) + t0);
-                            xj4[kk][0] = v.x; xj4[kk][1] = v.y; xj4[kk][2] = v.z; xj4[kk][3] = v.w;
-                        }
-#pragma unroll
-                        for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-                            for (int kk = 0; kk < 4; ++kk) dot[u] = fmaf(xj4[kk][tt], xq4[kk][tt], dot[u]);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < SPL; ++u)
-                    if (jj[u] >= 0) tl = fminf(tl, (dot[u] - xx[(int64_t)b * N + jj[u]]) - S.xxq);
-                tl = fminf(tl, __shfl_xor(tl, 16));
-                tl = fminf(tl, __shfl_xor(tl, 32));
-                if (g == 0) pub[h * QPB + S.qq] = tl;
-            });
-            __syncthreads();
-            each([&](Grp& S, int) {
-                const float T = fminf(pub[h * QPB + S.qq], pub[(1 - h) * QPB + S.qq]);
-                if (S.q < N && T != INFINITY) S.tseed = fmaxf(S.tseed, T);
-                S.thr = S.tseed;
-            });
-            __syncthreads();
-            if (tid < KQ_HALVES * QPB) pub[tid] = -INFINITY;
-            __syncthreads();
-        }
     }
 #ifdef DGX_KNN_STATS
     uint32_t n_rounds = 0, n_flush = 0;
@@ -929,173 +823,6 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     }
 }
 
-// ------------------------------------------------------------ seed kernel ----
-// Admission seeds from a candidate subset (e.g. the previous EdgeConv block's
-// neighbours, SURVEY §3.2's dynamic graph): T[q] = min over q's ks seed
-// candidates j of v(q, j), each v in knn_kernel's exact arithmetic — the fmaf
-// chain over c = 0..C-1 of x_j[c] * 2 x_q[c] (what the MFMA chain computes,
-// the zero-padded channels add exact zeros), then (dot - |x_j|^2) - |x_q|^2.
-// ks >= k candidates reach T, so T <= the row's k-th value. G lanes per query,
-// one seed per lane, min over the G lanes.
-template <int G, bool VEC>
-__global__ __launch_bounds__(256) void knn_seed_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
-                                                       int64_t sN, const float* __restrict__ xx, int N, int C,
-                                                       int64_t rows, const int32_t* __restrict__ seeds, int ks,
-                                                       float* __restrict__ T) {
-#pragma clang fp contract(off)
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t r = t / G;
-    const int s = (int)(t - r * G);
-    float v = INFINITY;
-    if (r < rows && s < ks) {
-        const int b = (int)(r / N), q = (int)(r - (int64_t)b * N);
-        const int j = seeds[r * ks + s];
-        const float* __restrict__ xq = x + b * sB + (int64_t)q * sN;
-        const float* __restrict__ xj = x + b * sB + (int64_t)j * sN;
-        float d = 0.f;
-        if constexpr (VEC) {
-            for (int c = 0; c < C; c += 4) {
-                const float4 a = *reinterpret_cast<const float4*>(xj + c);
-                const float4 e = *reinterpret_cast<const float4*>(xq + c);
-                d = fmaf(a.x, 2.0f * e.x, d);
-                d = fmaf(a.y, 2.0f * e.y, d);
-                d = fmaf(a.z, 2.0f * e.z, d);
-                d = fmaf(a.w, 2.0f * e.w, d);
-            }
-        } else {
-            for (int c = 0; c < C; ++c) d = fmaf(xj[c * sC], 2.0f * xq[c * sC], d);
-        }
-        const float tq = d - xx[(int64_t)b * N + j];
-        v = tq - xx[r];
-    }
-#pragma unroll
-    for (int o = 1; o < G; o <<= 1) v = fminf(v, __shfl_xor(v, o));
-    if (s == 0 && r < rows) T[r] = v;
-}
-
-// ------------------------------------------------------- spatial seeds ----
-// Coordinate clouds (C <= 4: the xyz kNN of DGCNN's first block,
-// PositionEmbedding and compute_hog_1x1): streamed in index order, the
-// selection's lists keep admitting candidates for the whole stream (a random
-// cloud holds no spatial order; 53 insertion rounds per wave at cfg2, 83 at
-// k 40, measured) and the kernel sat at 2.3 % of the MFMA peak. A spatial
-// seed makes the bound tight from the first tile: order the cloud along a
-// Morton curve of an 8^3 cell grid (counting sort), take for each query the 64
-// points around it in that order, and seed the selection with their k-th best
-// value (exact arithmetic, knn_seed_kernel's argument: 64 >= k candidates
-// reach it, so it never exceeds the row's k-th value).
-constexpr int SP_MINN = 256;
-constexpr int SP_MAXN = 4096;
-constexpr int SP_THREADS = 1024;
-constexpr int SP_WIN = 64;
-constexpr int SP_CELLS = 512;   // 8 x 8 x 8
-
-inline bool knn_spatial_ok(int C, int N) { return C <= 4 && N >= SP_MINN && N <= SP_MAXN; }
-
-// 3-bit coordinate -> every third bit of 9
-__device__ __forceinline__ uint32_t spread3b(uint32_t v) {
-    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
-}
-
-// perm[b*N + p] = id of the p-th point along the cell curve (points of one
-// cell in arrival order: the order only shapes the seed windows, never a result)
-__global__ __launch_bounds__(SP_THREADS) void knn_cell_order_kernel(const float* __restrict__ x, int64_t sB,
-                                                                    int64_t sC, int64_t sN, int C, int N,
-                                                                    int32_t* __restrict__ perm) {
-    __shared__ int cnt[SP_CELLS];
-    __shared__ int scan[SP_THREADS];
-    __shared__ unsigned short cellof[SP_MAXN];
-    __shared__ float red[2][3][SP_THREADS / 64];
-    __shared__ float box[2][3];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float* __restrict__ xb = x + b * sB;
-    const int D = C < 3 ? C : 3;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int n = tid; n < N; n += SP_THREADS)
-        for (int d = 0; d < D; ++d) {
-            const float v = xb[d * sC + n * sN];
-            lo[d] = fminf(lo[d], v);
-            hi[d] = fmaxf(hi[d], v);
-        }
-    for (int d = 0; d < 3; ++d) {
-        for (int o = 1; o < 64; o <<= 1) {
-            lo[d] = fminf(lo[d], __shfl_xor(lo[d], o));
-            hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], o));
-        }
-        if (lane == 0) { red[0][d][wave] = lo[d]; red[1][d][wave] = hi[d]; }
-    }
-    for (int c = tid; c < SP_CELLS; c += SP_THREADS) cnt[c] = 0;
-    __syncthreads();
-    if (tid < 3) {
-        float l = INFINITY, h = -INFINITY;
-        for (int w = 0; w < SP_THREADS / 64; ++w) { l = fminf(l, red[0][tid][w]); h = fmaxf(h, red[1][tid][w]); }
-        box[0][tid] = l;
-        box[1][tid] = h;
-    }
-    __syncthreads();
-    for (int n = tid; n < N; n += SP_THREADS) {
-        uint32_t code = 0;
-        for (int d = 0; d < D; ++d) {
-            const float l = box[0][d], w = box[1][d] - l;
-            const float t = w > 0.f ? (xb[d * sC + n * sN] - l) * (8.f / w) : 0.f;
-            code |= spread3b((uint32_t)fminf(fmaxf(t, 0.f), 7.f)) << d;
-        }
-        cellof[n] = (unsigned short)code;
-        atomicAdd(&cnt[code], 1);
-    }
-    __syncthreads();
-    // exclusive scan of the cell counts (one cell per thread, Hillis-Steele over the block)
-    int v = tid < SP_CELLS ? cnt[tid] : 0;
-    scan[tid] = v;
-    __syncthreads();
-    for (int o = 1; o < SP_CELLS; o <<= 1) {
-        const int add = tid >= o ? scan[tid - o] : 0;
-        __syncthreads();
-        scan[tid] += add;
-        __syncthreads();
-    }
-    if (tid < SP_CELLS) cnt[tid] = scan[tid] - v;   // start of the cell
-    __syncthreads();
-    for (int n = tid; n < N; n += SP_THREADS) {
-        const int pos = atomicAdd(&cnt[cellof[n]], 1);
-        perm[(int64_t)b * N + pos] = n;
-    }
-}
-
-// T[b*N + q] = the k-th best value over the 64 points around q along the cell
-// curve, each value in knn_kernel's exact arithmetic (the fmaf chain over the
-// C <= 4 channels with the query doubled, then - |x_j|^2 - |x_q|^2). One wave
-// per query: lane = window candidate, a 64-lane bitonic sort, lane 64 - k.
-__global__ __launch_bounds__(256) void knn_window_seed_kernel(const float* __restrict__ x, int64_t sB, int64_t sC,
-                                                              int64_t sN, int C, const float* __restrict__ xx,
-                                                              int B, int N, int k, const int32_t* __restrict__ perm,
-                                                              float* __restrict__ T) {
-#pragma clang fp contract(off)
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= (int64_t)B * N) return;   // wave-uniform
-    const int b = (int)(r / N), p = (int)(r - (int64_t)b * N);
-    const int32_t* __restrict__ pb = perm + (int64_t)b * N;
-    const float* __restrict__ xb = x + b * sB;
-    const int q = pb[p];
-    const int w0 = min(max(p - SP_WIN / 2, 0), N - SP_WIN);
-    const int j = pb[w0 + lane];
-    float d = 0.f;
-    for (int c = 0; c < C; ++c) d = fmaf(xb[c * sC + (int64_t)j * sN], 2.0f * xb[c * sC + (int64_t)q * sN], d);
-    const float tq = d - xx[(int64_t)b * N + j];
-    float v = tq - xx[(int64_t)b * N + q];
-#pragma unroll
-    for (int size = 2; size <= 64; size <<= 1)
-#pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            const float o = __shfl_xor(v, stride);
-            const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0 || size == 64);
-            v = keep_min ? fminf(v, o) : fmaxf(v, o);
-        }
-    const float tk = __shfl(v, SP_WIN - k);   // ascending: the k-th largest
-    if (lane == 0) T[(int64_t)b * N + q] = tk;
-}
-
 #ifdef DGX_KNN_STATS
 uint32_t* g_knn_stats = nullptr;   // diagnostics build: device buffer set by dgx_knn_stats_buffer
 #endif
@@ -1172,260 +899,6 @@ __global__ __launch_bounds__(256) void apply_image_kernel(const float* __restric
     }
 }
 
-// ------------------------------------------------ 3-channel selection ----
-// knn3_kernel<KB>: clouds of C <= 4 channels (the xyz kNN of DGCNN's first
-// block, PositionEmbedding and compute_hog_1x1), N <= K3_MAXN. No MFMA: a
-// 3-term dot is three packed-fp32 VALU ops per two candidates, cheaper than
-// feeding a 16x16x4 MFMA and dealing its outputs over 8 lists per query.
-// Lane = query (64 queries per block); wave w of K3_W = 8 = candidate part w
-// (tiles s = w, w+8, ... of 16 candidates: ascending order inside a wave, so a
-// strict '>' keeps canonical tie order).
-//   stage   the cloud's candidates from the operand image into LDS as pairs
-//           {x0 x0' x1 x1'} {x2 x2' xx xx'} (one ds_read_b128 pair feeds packed
-//           math for two candidates); pad candidates get xx = +inf (v = -inf).
-//   pass 1  values only: each lane keeps the M1 = ceil(KB/8) best values of its
-//           part (one v_med3 per slot); T = min over the 8 parts of the M1-th
-//           value is a lower bound of the row's k-th value (the eight lists hold
-//           8*M1 >= k distinct candidates reaching T).
-//   pass 2  the same distances again; v >= T (then v > the list's tail) puts
-//           the candidate id in a per-lane LDS FIFO, drained in insertion rounds
-//           into a sorted register list of KB slots. A part's list keeps its
-//           whole top-KB, so no row can overflow (no fix-up pass).
-//   merge   the 8 part lists through LDS, wave 0: k steps of a canonical
-//           8-way merge per lane.
-// Distances are the MFMA chain's values: d = fmaf(a2, 2q2, fmaf(a1, 2q1,
-// a0 * 2q0)) (the padded 4th channel adds an exact 0), v = (d - xx_j) - xx_q.
-constexpr int K3_MAXN = 4096;
-// candidate parts = waves per block: 8 for k <= 20 (more waves in flight, a
-// shorter pass-1 list), 4 above (the merge holds W x KB list slots in LDS)
-template <int KB>
-constexpr int knn3_w() { return 4; }
-constexpr int K3_QCAP = 24;   // per-lane FIFO slots (drained when any lane passes QCAP - 16)
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-template <int KB>
-constexpr size_t knn3_lds_bytes(int N) {
-    constexpr int K3_W = knn3_w<KB>();
-    const size_t ntile = (size_t)(N + 15) / 16;
-    const size_t stream = ntile * 8 * 32 + K3_W * K3_QCAP * 64 * 4 + K3_W * 64 * 4;
-    const size_t merge = (size_t)K3_W * KB * 64 * 6;   // values | u16 ids
-    return stream > merge ? stream : merge;
-}
-
-__device__ __forceinline__ float knn3_prev_float(float t) {   // largest float below t (-inf stays)
-    if (t == -INFINITY) return t;
-    if (t == 0.f) return -__uint_as_float(1u);
-    const uint32_t u = __float_as_uint(t);
-    return t > 0.f ? __uint_as_float(u - 1u) : __uint_as_float(u + 1u);
-}
-
-template <int KB>
-__global__ __launch_bounds__(64 * knn3_w<KB>()) void knn3_kernel(const float* __restrict__ img,
-                                                         const float* __restrict__ xximg,
-                                                         const float* __restrict__ xx, int B, int N, int k, int nqb,
-                                                         int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
-                                                         float* __restrict__ vals) {
-#pragma clang fp contract(off)
-    constexpr int K3_W = knn3_w<KB>(), K3_THREADS = 64 * K3_W;
-    constexpr int M1 = (KB + K3_W - 1) / K3_W;
-    extern __shared__ float4 k3s[];
-    int b, qb;
-    if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ntile = (N + 15) >> 4;
-    float4* cp = k3s;                                                          // [ntile*8 pairs][2]
-    int* fj = reinterpret_cast<int*>(k3s + ntile * 16);                        // [W][QCAP][64]
-    float* tw = reinterpret_cast<float*>(fj + K3_W * K3_QCAP * 64);           // [W][64]
-    // stage: candidate j = 16 s + c sits at image row knn_row(c) of tile s
-    const float* __restrict__ ib = img + (int64_t)b * ntile * 64;
-    const float* __restrict__ xb = xximg + (int64_t)b * ntile * 16;
-    float* cpf = reinterpret_cast<float*>(cp);
-    for (int j0 = 0; j0 < ntile * 16; j0 += 4 * K3_THREADS) {   // 16 loads in flight per thread
-        float a[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + u * K3_THREADS + tid;
-            const int st = j >> 4, i = knn_row(j & 15);
-            const bool ok = j < N;
-            a[u][0] = ok ? ib[st * 64 + i] : 0.f;
-            a[u][1] = ok ? ib[st * 64 + 16 + i] : 0.f;
-            a[u][2] = ok ? ib[st * 64 + 32 + i] : 0.f;
-            a[u][3] = ok ? xb[st * 16 + i] : INFINITY;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + u * K3_THREADS + tid;
-            if (j < ntile * 16) {
-                const int p = j >> 1, h = j & 1;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) cpf[p * 8 + 2 * c + h] = a[u][c];
-            }
-        }
-    }
-    __syncthreads();
-    const int q = min(qb * 64 + lane, N - 1);
-    const bool live = qb * 64 + lane < N;
-    f32x2 q0, q1, q2, qq;
-    {
-        const float4 u = cp[(q >> 1) * 2], v = cp[(q >> 1) * 2 + 1];
-        const int h = q & 1;
-        const float x0 = h ? u.y : u.x, x1 = h ? u.w : u.z, x2 = h ? v.y : v.x;
-        q0 = 2.0f * x0;
-        q1 = 2.0f * x1;
-        q2 = 2.0f * x2;
-        qq = xx[(int64_t)b * N + q];
-    }
-    auto dist = [&](int p) -> f32x2 {
-        const float4 u = cp[2 * p], v = cp[2 * p + 1];
-        const f32x2 a0 = {u.x, u.y}, a1 = {u.z, u.w}, a2 = {v.x, v.y}, w = {v.z, v.w};
-        const f32x2 d = __builtin_elementwise_fma(a2, q2, __builtin_elementwise_fma(a1, q1, a0 * q0));
-        return (d - w) - qq;
-    };
-    // pass 1: the M1 best values of this quarter
-    float L[M1];
-#pragma unroll
-    for (int m = 0; m < M1; ++m) L[m] = -INFINITY;
-    auto med_insert = [&](float nv) {
-#pragma unroll
-        for (int m = M1 - 1; m > 0; --m) L[m] = __builtin_amdgcn_fmed3f(L[m - 1], L[m], nv);
-        L[0] = fmaxf(L[0], nv);
-    };
-    for (int st = wave; st < ntile; st += K3_W) {
-#pragma unroll
-        for (int pp = 0; pp < 8; ++pp) {
-            const f32x2 v = dist(st * 8 + pp);
-            med_insert(v.x);
-            med_insert(v.y);
-        }
-    }
-    tw[wave * 64 + lane] = L[M1 - 1];
-    __syncthreads();
-    float T = tw[lane];
-#pragma unroll
-    for (int w = 1; w < K3_W; ++w) T = fminf(T, tw[w * 64 + lane]);
-    // pass 2: admissions v >= T into the FIFO, insertion rounds into the list
-    float lv[KB];
-    int li[KB];
-#pragma unroll
-    for (int m = 0; m < KB; ++m) {
-        lv[m] = -INFINITY;
-        li[m] = 0x7fffffff;
-    }
-    float thr = knn3_prev_float(T);
-    int cnt = 0;
-    int* __restrict__ myf = fj + wave * K3_QCAP * 64 + lane;
-    auto drain = [&]() {
-        for (int r = 0; __any(r < cnt); ++r) {
-            float nv = -INFINITY;
-            int nj = 0x7fffffff;
-            if (r < cnt) {
-                nj = myf[r * 64];
-                const float4 u = cp[2 * (nj >> 1)], v = cp[2 * (nj >> 1) + 1];
-                const int h = nj & 1;
-                const float a0 = h ? u.y : u.x, a1 = h ? u.w : u.z, a2 = h ? v.y : v.x, w = h ? v.w : v.z;
-                const float d = fmaf(a2, q2.x, fmaf(a1, q1.x, a0 * q0.x));
-                nv = (d - w) - qq.x;
-            }
-            list_insert_ordered<KB>(lv, li, nv, nj);
-        }
-        cnt = 0;
-        thr = fmaxf(thr, lv[KB - 1]);
-    };
-    for (int st = wave; st < ntile; st += K3_W) {
-        // the tile's candidate reads all issued before the first FIFO store (the
-        // compiler may not move LDS reads across those stores)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {   // half tiles: 4 pairs of operands in registers
-        float4 U[4], V[4];
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-            U[pp] = cp[2 * (st * 8 + 4 * hh + pp)];
-            V[pp] = cp[2 * (st * 8 + 4 * hh + pp) + 1];
-        }
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-            const int p = st * 8 + 4 * hh + pp;
-            const f32x2 a0 = {U[pp].x, U[pp].y}, a1 = {U[pp].z, U[pp].w}, a2 = {V[pp].x, V[pp].y};
-            const f32x2 w = {V[pp].z, V[pp].w};
-            const f32x2 d = __builtin_elementwise_fma(a2, q2, __builtin_elementwise_fma(a1, q1, a0 * q0));
-            const f32x2 v = (d - w) - qq;
-            if (v.x > thr) { myf[cnt * 64] = 2 * p; ++cnt; }
-            if (v.y > thr) { myf[cnt * 64] = 2 * p + 1; ++cnt; }
-        }
-        }
-        if (__any(cnt > K3_QCAP - 16)) drain();
-    }
-    drain();
-    // merge the 4 quarter lists (canonical order) in wave 0
-    __syncthreads();   // every wave is done with the candidates and its FIFO
-    float* lvv = reinterpret_cast<float*>(k3s);                          // [W][KB][64] values
-    uint16_t* lvi = reinterpret_cast<uint16_t*>(lvv + K3_W * KB * 64);   // [W][KB][64] ids (N <= 4096)
-#pragma unroll
-    for (int m = 0; m < KB; ++m) {
-        lvv[(wave * KB + m) * 64 + lane] = lv[m];
-        lvi[(wave * KB + m) * 64 + lane] = (uint16_t)min(li[m], 0xffff);
-    }
-    __syncthreads();
-    if (wave != 0) return;
-    int pos[K3_W];
-    float2 hd[K3_W];
-#pragma unroll
-    for (int w = 0; w < K3_W; ++w) {
-        pos[w] = 0;
-        hd[w] = make_float2(lvv[(w * KB) * 64 + lane], __int_as_float((int)lvi[(w * KB) * 64 + lane]));
-    }
-    const int64_t row = ((int64_t)b * N + qb * 64 + lane) * k;
-    for (int r = 0; r < k; ++r) {
-        int bw = 0;
-        float bv = hd[0].x;
-        int bj = __float_as_int(hd[0].y);
-#pragma unroll
-        for (int w = 1; w < K3_W; ++w) {
-            const float v = hd[w].x;
-            const int j = __float_as_int(hd[w].y);
-            if (canon_better(v, j, bv, bj)) { bv = v; bj = j; bw = w; }
-        }
-        if (live) {
-            if (idx64) idx64[row + r] = bj;
-            if (idx32) idx32[row + r] = bj;
-            if (vals) vals[row + r] = bv;
-        }
-#pragma unroll
-        for (int w = 0; w < K3_W; ++w) {
-            if (w == bw) {
-                ++pos[w];
-                hd[w] = pos[w] < KB ? make_float2(lvv[(w * KB + pos[w]) * 64 + lane],
-                                                  __int_as_float((int)lvi[(w * KB + pos[w]) * 64 + lane]))
-                                    : make_float2(-INFINITY, __int_as_float(0xffff));
-            }
-        }
-    }
-}
-
-template <int KB>
-int launch_knn3(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img,
-                const float* xximg, hipStream_t st) {
-    const int nqb = (N + 63) / 64;
-    const size_t lds = knn3_lds_bytes<KB>(N);
-    hipLaunchKernelGGL((knn3_kernel<KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(64 * knn3_w<KB>()), lds, st, img, xximg, xx,
-                       B, N, k, nqb, idx64, idx32, vals);
-    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
-}
-
-int dispatch_knn3(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
-                  const float* img, const float* xximg, hipStream_t st) {
-    if (k <= 16) return launch_knn3<16>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
-    if (k <= 20) return launch_knn3<20>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
-    if (k <= 32) return launch_knn3<32>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
-    if (k <= 40) return launch_knn3<40>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
-    return launch_knn3<64>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
-}
-
-// whether dgx_knn_select_f32 takes knn3_kernel for (C, N, k)
-inline bool knn3_ok(int C, int N, int k) { return g_knn3_enabled && C <= 4 && N <= K3_MAXN && k <= 64 && k <= N; }
-
 template <int NSTEP>
 int launch_prepare(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order, float* xx,
                    float* img, float* xximg, hipStream_t st) {
@@ -1451,10 +924,10 @@ inline int knn_qg(int nstep, int kb, int N) {
 
 template <int NSTEP, int KB, int QG>
 int launch_knn_qg(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
-                  const float* img, const float* xximg, KnnSeed seed, hipStream_t st) {
+                  const float* img, const float* xximg, hipStream_t st) {
     const int nqb = (N + KQ_QPB * QG - 1) / (KQ_QPB * QG);
     hipLaunchKernelGGL((knn_kernel<NSTEP, KB, QG>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st, img,
-                       xximg, xx, B, N, k, nqb, idx64, idx32, vals, seed
+                       xximg, xx, B, N, k, nqb, idx64, idx32, vals
 #ifdef DGX_KNN_STATS
                        , g_knn_stats
 #endif
@@ -1465,22 +938,21 @@ int launch_knn_qg(const float* xx, int B, int N, int k, int64_t* idx64, int32_t*
 template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
-               KnnSeed seed, hipStream_t st) {
+               hipStream_t st) {
     // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
     // the lists of two groups fit in registers); one where the selection does
     if constexpr (KB <= 40 && NSTEP >= 16) {
         if (knn_qg(NSTEP, KB, N) == 2) return launch_knn_qg<NSTEP, KB, 2>(xx, B, N, k, idx64, idx32, vals, img, xximg,
-                                                                          seed, st);
+                                                                          st);
     }
-    return launch_knn_qg<NSTEP, KB, 1>(xx, B, N, k, idx64, idx32, vals, img, xximg, seed, st);
+    return launch_knn_qg<NSTEP, KB, 1>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
 }
 
 template <int NSTEP>
 int dispatch_k(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, KnnSeed seed,
-               hipStream_t st) {
+               int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg, hipStream_t st) {
 #define DGX_KNN_K(KBV) \
-    return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st)
+    return launch_knn<NSTEP, KBV>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st)
     if (k <= 16) DGX_KNN_K(16);
     if (k <= 20) DGX_KNN_K(20);
     if (k <= 32) DGX_KNN_K(32);
@@ -1499,8 +971,6 @@ extern "C" {
 void dgx_knn_stats_buffer(void* dev) { g_knn_stats = static_cast<uint32_t*>(dev); }
 #endif
 
-void dgx_knn_set_variant(int knn3) { g_knn3_enabled = knn3 != 0; }
-
 const char* dgx_knn_kernel_name(int C, int k, int N) {
     // the selection kernel dgx_knn_select_f32 launches for (C, k, N), as profilers print it
     struct Names {
@@ -1516,11 +986,6 @@ const char* dgx_knn_kernel_name(int C, int k, int N) {
     };
     static const Names names;  // thread-safe one-time initialisation
     if (C < 1 || C > 128 || k < 1 || k > 64 || N < 1) return "";
-    if (knn3_ok(C, N, k)) {
-        static const char* k3[5] = {"knn3_kernel<16>", "knn3_kernel<20>", "knn3_kernel<32>", "knn3_kernel<40>",
-                                    "knn3_kernel<64>"};
-        return k3[k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4];
-    }
     const int ns = knn_nstep(C);
     const int a = ns == 1 ? 0 : ns == 3 ? 1 : ns == 8 ? 2 : ns == 16 ? 3 : 4;
     const int b = k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4;
@@ -1574,23 +1039,6 @@ size_t dgx_knn_workspace_bytes(int B, int C, int N) {
     return ((((size_t)B * N + 3) & ~(size_t)3) * sizeof(float)) + dgx_knn_image_bytes(B, C, N);
 }
 
-int dgx_knn_prepare_pq_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order,
-                           float* xx, void* image, size_t image_bytes, const float* Wref, int Co, float* PQ,
-                           int ldpq, void* stream) {
-    if (!x || !xx || !Wref || !PQ || B < 1 || C < 1 || N < 1 || Co < 2) return DGX_EINVAL;
-    if (knn_nstep(C) != 1 || Co % 2 || ldpq % 4 || ldpq < 2 * Co || reinterpret_cast<uintptr_t>(PQ) % 16)
-        return DGX_EUNSUPPORTED;
-    if (!image || image_bytes < dgx_knn_image_bytes(B, C, N) || (reinterpret_cast<uintptr_t>(image) & 15) != 0)
-        return DGX_EINVAL;
-    float* img = static_cast<float*>(image);
-    float* xximg = img + (size_t)B * knn_image_floats(C, N);
-    const int ntile = knn_ntile(N);
-    const int tgroups = (ntile + KI_TILES - 1) / KI_TILES;
-    hipLaunchKernelGGL(knn_image_kernel<1>, dim3((unsigned)(B * tgroups)), dim3(256), 0, dgx_stream(stream), x, sB, sC,
-                       sN, B, C, N, order, ntile, tgroups, xx, img, xximg, Wref, Co, PQ, ldpq);
-    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
-}
-
 int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int order,
                         float* xx, void* image, size_t image_bytes, void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1) return DGX_EINVAL;
@@ -1614,8 +1062,7 @@ int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int 
 
 namespace {
 int knn_select(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N, int k,
-               int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes, KnnSeed seed,
-               void* stream) {
+               int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes, void* stream) {
     if (!x || !xx || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
     if (!idx64 && !idx32) return DGX_EINVAL;
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
@@ -1625,73 +1072,22 @@ int knn_select(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
     const float* img = static_cast<const float*>(image);
     const float* xximg = img + (size_t)B * knn_image_floats(C, N);
     hipStream_t st = dgx_stream(stream);
-    if (!seed.T && !seed.sidx && knn3_ok(C, N, k)) return dispatch_knn3(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
     switch (knn_nstep(C)) {
-        case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
-        case 3: return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
-        case 8: return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
-        case 16: return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
-        default: return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, seed, st);
+        case 1: return dispatch_k<1>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 3: return dispatch_k<3>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 8: return dispatch_k<8>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        case 16: return dispatch_k<16>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
+        default: return dispatch_k<32>(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, img, xximg, st);
     }
 }
 }  // namespace
 
 extern "C" {
 
-int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
-                              int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image,
-                              size_t image_bytes, const float* seed, void* stream) {
-    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes,
-                      KnnSeed{seed, nullptr, 0}, stream);
-}
-
-int dgx_knn_select_graph_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B,
-                                    int C, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
-                                    const void* image, size_t image_bytes, const int32_t* seeds, int ks,
-                                    void* stream) {
-    if (!seeds || ks < k || ks > 24) return DGX_EINVAL;
-    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes,
-                      KnnSeed{nullptr, seeds, ks}, stream);
-}
-
 int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                        int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image, size_t image_bytes,
                        void* stream) {
-    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes,
-                      KnnSeed{nullptr, nullptr, 0}, stream);
-}
-
-int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                     const int32_t* seeds, int ks, float* T, void* stream) {
-    if (!x || !xx || !seeds || !T || B < 0 || C < 1 || N < 1 || ks < 1 || ks > 64) return DGX_EINVAL;
-    if (C > 128) return DGX_EUNSUPPORTED;
-    if (B == 0) return DGX_OK;
-    const int64_t rows = (int64_t)B * N;
-    const bool vec = sC == 1 && C % 4 == 0 && sN % 4 == 0 && sB % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    hipStream_t st = dgx_stream(stream);
-    if (ks <= 32) {
-        const unsigned grid = (unsigned)((rows * 32 + 255) / 256);
-        if (vec) hipLaunchKernelGGL((knn_seed_kernel<32, true>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
-        else hipLaunchKernelGGL((knn_seed_kernel<32, false>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
-    } else {
-        const unsigned grid = (unsigned)((rows * 64 + 255) / 256);
-        if (vec) hipLaunchKernelGGL((knn_seed_kernel<64, true>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
-        else hipLaunchKernelGGL((knn_seed_kernel<64, false>), dim3(grid), dim3(256), 0, st, x, sB, sC, sN, xx, N, C, rows, seeds, ks, T);
-    }
-    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
-}
-
-int dgx_knn_spatial_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
-                             int N, int k, int32_t* perm, float* T, void* stream) {
-    if (!x || !xx || !perm || !T || B < 0 || C < 1 || N < 1 || k < 1 || k > N) return DGX_EINVAL;
-    if (!knn_spatial_ok(C, N) || k > SP_WIN) return DGX_EUNSUPPORTED;
-    if (B == 0) return DGX_OK;
-    hipStream_t st = dgx_stream(stream);
-    hipLaunchKernelGGL(knn_cell_order_kernel, dim3((unsigned)B), dim3(SP_THREADS), 0, st, x, sB, sC, sN, C, N, perm);
-    DGX_CHECK_LAUNCH();
-    const unsigned grid = (unsigned)(((int64_t)B * N + 3) / 4);
-    hipLaunchKernelGGL(knn_window_seed_kernel, dim3(grid), dim3(256), 0, st, x, sB, sC, sN, C, xx, B, N, k, perm, T);
-    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+    return knn_select(x, sB, sC, sN, xx, B, C, N, k, idx64, idx32, vals, image, image_bytes, stream);
 }
 
 int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int k, int order,

@@ -30,27 +30,15 @@ _SIGS = {
     "dgx_knn_workspace_bytes": [_i32, _i32, _i32],
     "dgx_knn_image_bytes": [_i32, _i32, _i32],
     "dgx_knn_kernel_name": [_i32, _i32, _i32],
-    "dgx_knn_set_variant": [_i32],
     "dgx_bn_lrelu_apply_knn_image_f32": [_vp, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _sz, _vp],
-    "dgx_knn_prepare_pq_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp, _i32, _vp, _i32,
-                               _vp],
     "dgx_knn_prepare_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp],
     "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
     "dgx_sqnorm_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp],
     "dgx_knn_select_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp],
-    "dgx_knn_select_seeded_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp,
-                                  _vp],
-    "dgx_knn_seed_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp],
-    "dgx_knn_select_graph_seeded_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz,
-                                        _vp, _i32, _vp],
-    "dgx_knn_spatial_seed_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_edge_partials_rows": [_i32, _i32, _i32],
     "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
-    "dgx_edge_fwd_gather_counters": [_i32, _i32, _i32],
-    "dgx_edge_fwd_gather_bn_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
-                                   _f64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_bn_finalize_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_bn_finalize_out_f32": [_vp, _i32, _i32, _f64, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -132,7 +120,6 @@ _RESTYPES = {
     "dgx_version": ctypes.c_char_p,
     "dgx_strerror": ctypes.c_char_p,
     "dgx_knn_kernel_name": ctypes.c_char_p,
-    "dgx_knn_set_variant": None,
     "dgx_knn_workspace_bytes": _sz,
     "dgx_knn_image_bytes": _sz,
 }

@@ -92,10 +92,11 @@ def batch_stats(partials, rows, count, bn, gamma, beta, stream):
     _, update = mode(bn)
     rm_new, rv_new, nbt_new = _update_targets(bn)
     if update and getattr(bn, "stats_out", None) is not None and bn.momentum is None:
-        # cumulative average: the counter is bumped on the host side of the op
+        # cumulative average (momentum=None): the finalize reads the counter and
+        # uses 1 / (count + 1) on the device (factor -1), writing count + 1 to the
+        # op's own output — no host read, so the op stays graph-capturable
         if bn.num_batches_tracked is not None:
-            nbt_new.copy_(bn.num_batches_tracked).add_(1)
-            factor, nbt = 1.0 / float(nbt_new.item()), None
+            factor, nbt = -1.0, bn.num_batches_tracked
         else:
             factor, nbt = 0.0, None
     else:
@@ -117,47 +118,6 @@ def batch_stats(partials, rows, count, bn, gamma, beta, stream):
                                             nat.f32(mean), nat.f32(invstd), nat.ptr(nbt, nat.I64), *outs, stream),
                   "bn finalize")
     return Stats(scale, shift, mean, invstd, group if sync else None, False)
-
-
-_COUNTER_SETS = 64      # independent counter sets per device, taken round-robin
-_COUNTER_WORDS = 1024   # ints per set (>= the channel slices of one launch)
-_counters = {}
-
-
-def launch_counters(dev, n):
-    """Zeroed int32 counters for one in-launch finalize (the last-arriver
-    kernels leave them zero again). One buffer per device, allocated on first
-    use outside stream capture; calls take its sets round-robin, so launches in
-    flight on different streams of the device use different counters unless 64
-    are outstanding at once. Returns None while capturing before the buffer
-    exists (the caller then takes the separate-finalize path)."""
-    if n > _COUNTER_WORDS:
-        return None
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    ent = _counters.get(key)
-    if ent is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        ent = _counters[key] = [torch.zeros((_COUNTER_SETS, _COUNTER_WORDS), dtype=torch.int32, device=dev), 0]
-    buf, i = ent
-    ent[1] = (i + 1) % _COUNTER_SETS
-    return buf[i]
-
-
-def fused_finalize_args(bn, gamma, beta, co, count, dev):
-    """(mode arguments of an in-launch finalize, Stats) for a BN layer whose
-    batch statistics are local (no SyncBatchNorm), or None."""
-    sync, _ = dist_.sync_group(bn)
-    if sync or getattr(bn, "stats_out", None) is not None:   # in-place updates only
-        return None
-    scale, shift, mean, invstd = _vec(co, dev), _vec(co, dev), _vec(co, dev), _vec(co, dev)
-    _, update = mode(bn)
-    factor, nbt = _factor(bn) if update else (0.0, None)
-    rm = nat.f32(bn.running_mean) if update else None
-    rv = nat.f32(bn.running_var) if update else None
-    args = (float(count), rm, rv, factor, float(bn.eps), nat.f32(scale), nat.f32(shift), nat.f32(mean),
-            nat.f32(invstd), nat.ptr(nbt, nat.I64))
-    return args, Stats(scale, shift, mean, invstd, None, False)
 
 
 def running_stats(bn, gamma, beta, stream):

@@ -35,26 +35,12 @@ from .ops import knn_image_buffers, knn_raw, reduction_order
 
 _tls = threading.local()
 
-# blocks 2-4: seed each kNN's admission bound with the previous block's graph
-# (the selection kernel computes the seeds' distances itself,
-# dgx_knn_select_graph_seeded_f32). Off: measured at cfg2 the seeded selection
-# launches take 111 / 210 us (C = 64 / 128) against 90 / 139 us unseeded —
-# the per-lane gather of 3 seed rows costs more than the insertion rounds it
-# saves (a separate seed pass, dgx_knn_seed_f32: 87 -> 70 us selection plus
-# 58 us per block for the pass). DGX_KNN_SEEDS=1 turns it on (A/B only).
-KNN_SEEDS = os.environ.get("DGX_KNN_SEEDS", "0") == "1"
 # bf16 mode: the backward scatter reads packed dz|slot words (DGX_SCATTER_PACKED=0:
 # separate dz and slot arrays, A/B only; cfg2 step 1.4178 -> 1.4131 ms)
 SCATTER_PACKED = os.environ.get("DGX_SCATTER_PACKED", "1") == "1"
 # BN backward finalize folded into the scatter's prologue (DGX_FOLD_BN_BWD=0: a
 # separate finalize launch, A/B only; cfg2 step 1.4131 -> 1.4065 ms)
 FOLD_BN_BWD = os.environ.get("DGX_FOLD_BN_BWD", "1") == "1"
-# forward BN finalize inside the gather launch (last arriver per channel slice,
-# dgx_edge_fwd_gather_bn_f32). Off: measured at cfg2 (tools/ab_step.py --graph)
-# 1.4065 -> 1.4118 ms/step with it on — every workgroup's drain of its stores
-# before the ticket costs more than the finalize launch it removes.
-# DGX_FOLD_BN_FWD=1 turns it on (A/B only).
-FOLD_BN_FWD = os.environ.get("DGX_FOLD_BN_FWD", "0") == "1"
 # blocks 1-3: the BN + LeakyReLU apply also writes the next block's kNN operand
 # image and |x|^2 (dgx_bn_lrelu_apply_knn_image_f32), so that kNN skips its
 # prepare pass (DGX_FUSE_KNN_IMAGE=0: separate prepare pass, A/B only)
@@ -63,12 +49,6 @@ FUSE_KNN_IMAGE = os.environ.get("DGX_FUSE_KNN_IMAGE", "1") == "1"
 # in its epilogue and writes that block's packed dz + BN partials
 # (dgx_gemm_edge_dz_bf16) instead of dY (DGX_FUSE_EDGE_DZ=0: dY + a dz pass)
 FUSE_EDGE_DZ = os.environ.get("DGX_FUSE_EDGE_DZ", "1") == "1"
-# block 1: the kNN prepare pass over the xyz cloud also writing the PQ rows
-# (dgx_knn_prepare_pq_f32). Off: measured 1.351 -> 1.364 ms/step at cfg2 with
-# it on (the 16-point image blocks write the 128-wide PQ rows on the critical
-# path before the kNN; the separate small-K GEMM runs wider). DGX_FUSE_BLOCK1_PQ=1
-# turns it on (A/B only; bitwise-equal outputs, tests/test_knn_gpu.py).
-FUSE_BLOCK1_PQ = os.environ.get("DGX_FUSE_BLOCK1_PQ", "0") == "1"
 
 
 def debug_capture():
@@ -133,34 +113,6 @@ def edge_select(PQ, idx, B, N, k, co, gamma, stream):
     return ysel, arg, sumP, partials, prow
 
 
-def edge_select_stats(PQ, idx, B, N, k, co, bn, gamma, beta, count, stream):
-    """edge_select + the BN batch-statistics finalize in one launch
-    (dgx_edge_fwd_gather_bn_f32). Returns (ysel, arg, sumP, Stats) or None when
-    the layer needs the separate path (SyncBatchNorm, no counters under capture)."""
-    L = nat.lib()
-    dev = PQ.device
-    if not FOLD_BN_FWD:
-        return None
-    fa = bn_.fused_finalize_args(bn, gamma, beta, co, count, dev)
-    if fa is None:
-        return None
-    ctr = bn_.launch_counters(dev, L.dgx_edge_fwd_gather_counters(B, N, co))
-    if ctr is None:
-        return None
-    args, st = fa
-    M = B * N
-    ysel = torch.empty((M, co), dtype=torch.float32, device=dev)
-    arg = torch.empty((M, co), dtype=torch.uint8, device=dev)
-    sumP = torch.empty((M, co), dtype=torch.float32, device=dev)
-    prow = L.dgx_edge_partials_rows(B, N, co)
-    partials = torch.empty((prow, 2, co), dtype=torch.float32, device=dev)
-    nat.check(L.dgx_edge_fwd_gather_bn_f32(nat.f32(PQ), PQ.stride(0), nat.i32(idx), B, N, k, co, nat.f32(gamma),
-                                           nat.f32(beta), nat.f32(ysel), nat.u8(arg), nat.f32(sumP),
-                                           nat.f32(partials), prow, nat.ptr(ctr, nat.I32), *args, stream),
-              "edge gather + bn finalize")
-    return ysel, arg, sumP, st
-
-
 class _EdgeConvStack(torch.autograd.Function):
     @staticmethod
     @prec.no_autocast
@@ -194,36 +146,18 @@ class _EdgeConvStack(torch.autograd.Function):
         for li, ly in enumerate(layers):
             w, gamma, beta = params[3 * li: 3 * li + 3]
             cin, co = ly.cin, ly.cout
-            PQ = None
             if li == 0:
                 X = x_pm
-                order0 = reduction_order(x)
-                prep0 = None
-                if FUSE_BLOCK1_PQ and cin <= G.SMALLK_MAX and C0 <= 4 and w.is_contiguous():
-                    # one pass over the cloud: kNN operand image, |x|^2 and the PQ rows
-                    prep0 = knn_image_buffers(B, C0, N, dev)
-                    PQ = torch.empty((M, 2 * ly.cout), dtype=torch.float32, device=dev)
-                    with torch.cuda.device(dev):
-                        nat.check(L.dgx_knn_prepare_pq_f32(
-                            nat.f32(x), *x.stride(), B, C0, N, order0, nat.f32(prep0[0]), nat.f32(prep0[1]),
-                            prep0[1].numel() * 4, nat.f32(w), ly.cout, nat.f32(PQ), 2 * ly.cout, stream),
-                            "knn prepare + PQ")
-                idx = knn_raw(x, k, order=order0, out_dtype=torch.int32, prepared=prep0)
+                idx = knn_raw(x, k, order=reduction_order(x), out_dtype=torch.int32)
             else:
                 X = xcat[:, off_in:off_in + cin]
                 # the reference's blocks 2-4 see contiguous (B,C,N) features (max over
                 # dim -1 of a contiguous tensor), hence the strided rounding order
-                # optionally the previous block's neighbours seed the admission bound:
-                # feature-space neighbourhoods of consecutive blocks overlap (~1.3 k
-                # candidates then reach it)
                 idx = knn_raw(xcat[:, off_in:], k, order=nat.ORDER_STRIDED, out_dtype=torch.int32,
-                              strides=(N * total, 1, total), shape=(B, cin, N),
-                              seeds=idx if KNN_SEEDS else None, prepared=next_prepared)
+                              strides=(N * total, 1, total), shape=(B, cin, N), prepared=next_prepared)
             next_prepared = None
             wprep = None
-            if PQ is not None:
-                pass   # block 1's PQ came with its kNN operands
-            elif cin <= G.SMALLK_MAX:
+            if cin <= G.SMALLK_MAX:
                 # raw coordinates (block 1, K = 3): exact fp32 in every mode
                 PQ = G.mm_smallk_split(X, w, co)
             elif bf16:
@@ -241,10 +175,7 @@ class _EdgeConvStack(torch.autograd.Function):
             bn = ly.bn
             use_batch, _ = bn_.mode(bn)
             with torch.cuda.device(dev):
-                fused = edge_select_stats(PQ, idx, B, N, k, co, bn, gamma, beta, count, stream) if use_batch else None
-                if fused is not None:
-                    ysel, arg, sumP, st = fused
-                if fused is None and (use_batch or need_grad):
+                if use_batch or need_grad:
                     ysel, arg, sumP, partials, prow = edge_select(PQ, idx, B, N, k, co, gamma, stream)
                     if use_batch:
                         st = bn_.batch_stats(partials, prow, count, bn, gamma, beta, stream)
@@ -407,7 +338,7 @@ class _EdgeConvStack(torch.autograd.Function):
                     dst = dnew[:, prev:prev + cin]
                     add = dxcat[:, prev:prev + cin]
                     prev_state = ctx.layer_state[li - 1]
-                    if wprep is not None and FUSE_EDGE_DZ and packed and prev_state is not None and cin % 8 == 0:
+                    if wprep is not None and FUSE_EDGE_DZ and packed and prev_state is not None and G.edge_dz_ok(dPQ, cin):
                         _, _, ysel_p, arg_p, _, st_p, _ = prev_state
                         fused_dz[li - 1] = G.lds_xwt_edge_dz(dPQ, wprep[1], add, ysel_p, arg_p, st_p,
                                                              layers[li - 1].slope)

@@ -125,6 +125,8 @@ def mm32(a, b, out=None, accumulate=False, addend=None):
     N = b.shape[1]
     if b.shape[0] != K:
         raise RuntimeError(f"dgx mm32: inner dims {K} and {b.shape[0]} differ")
+    if accumulate and out is None:
+        raise RuntimeError("dgx mm32: accumulate=True needs an output to accumulate into")
     ta, aic, lda = _op32(a, 1)
     tb, bic, ldb = _op32(b, 0)
     if out is None:
@@ -156,6 +158,8 @@ def mm16(a, b, out=None, accumulate=False):
     """out (M,N) (+)= a (M,K) @ b (K,N) on the bf16 MFMA GEMM (dgx_gemm_bf16:
     fp32 or bf16 operands rounded to bf16 while staged, fp32 accumulation);
     transposed views read in place; long reductions split-K (deterministic)."""
+    if accumulate and out is None:
+        raise RuntimeError("dgx mm16: accumulate=True needs an output to accumulate into")
     M, K = a.shape
     N = b.shape[1]
     if a.stride(1) != 1 and a.stride(0) != 1:
@@ -307,9 +311,10 @@ def lds_xwt_edge_dz(x16, w16, addend, ysel, arg, st, slope):
 
 
 # cap (MiB) on the split-K slab of the small bf16 weight-gradient GEMMs (output
-# < 1 MiB: the EdgeConv blocks' dW; 0: dgx_gemm_splits's rule). 8: block 4's dW
-# takes 32 splits instead of 128 (33.5 -> 8.4 MB of slab); measured at cfg2
-# 1.3442 -> 1.3384 ms/step (2 / 4 MB: 1.401 / 1.359, too few workgroups)
+# < 1 MiB: the EdgeConv blocks' dW). Default 8: block 4's dW takes 32 splits
+# instead of 128 (33.5 -> 8.4 MB of slab); measured at cfg2 1.3442 -> 1.3384
+# ms/step (2 / 4 MB: 1.401 / 1.359, too few workgroups). DGX_SLAB_CAP_MB=0
+# restores dgx_gemm_splits's own rule.
 SLAB_CAP_MB = int(__import__("os").environ.get("DGX_SLAB_CAP_MB", "8"))
 
 
@@ -322,7 +327,7 @@ def lds_atb(a16, b16, out, split_rows=None):
         raise RuntimeError("dgx gemm: output must be a row-major fp32 view")
     L = nat.lib()
     S = L.dgx_gemm_splits(M, N, R)
-    if SLAB_CAP_MB > 0 and M * N * 4 < (1 << 20):   # bound the slab traffic of small outputs (A/B knob)
+    if SLAB_CAP_MB > 0 and M * N * 4 < (1 << 20):   # bound the slab traffic of small outputs
         S = max(1, min(S, (SLAB_CAP_MB << 20) // (M * N * 4)))
     chunk = -(-R // S)
     chunk = -(-chunk // 64) * 64
@@ -411,3 +416,13 @@ def prep_weights(jobs, buf=None):
 def lds_ok_nt(x, K):
     """Whether the DMA path takes this k-contiguous operand (else the register-staged kernel)."""
     return x.dtype == torch.bfloat16 and K % 64 == 0 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0
+
+
+def edge_dz_ok(dpq16, cin):
+    """Whether dgx_gemm_edge_dz_bf16 takes this block's input-gradient GEMM
+    (dX columns = cin, K = dPQ width): the kernel's own limits (cin a multiple
+    of 8 and <= 128, K a multiple of its 64-deep K step, 16-byte rows);
+    otherwise the caller keeps the dY + dz-pass path."""
+    K = dpq16.shape[1]
+    return (dpq16.dtype == torch.bfloat16 and cin % 8 == 0 and cin <= 128 and K % 64 == 0
+            and dpq16.stride(0) % 8 == 0 and dpq16.data_ptr() % 16 == 0)

@@ -152,7 +152,8 @@ def graph_feature(x: Tensor, k: int, mode: int) -> tuple[Tensor, Tensor]:
     cat(x_j, x_i) (B,2C,N,k), 1 = x_j - x_i (B,C,N,k), 2 = x_j (B,N,k,C)."""
     xf = x.float()
     idx = ops.knn_raw(xf.detach(), k, out_dtype=_I32)
-    return ops._GraphFeature.forward(_Rec(), xf, idx, mode), idx.clone() if idx._base is not None else idx
+    shared = idx._base is not None or getattr(ops._tls, "cache", None) is not None   # a cache entry: never alias it
+    return ops._GraphFeature.forward(_Rec(), xf, idx, mode), idx.clone() if shared else idx
 
 
 @graph_feature.register_fake

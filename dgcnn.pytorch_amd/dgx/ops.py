@@ -13,15 +13,6 @@ from . import _native as nat
 
 _tls = threading.local()
 
-# coordinate clouds (C <= 4, 256 <= N <= 4096): seed the selection with the
-# k-th value of each point's 64 neighbours along a Morton curve of the cloud
-# (dgx_knn_spatial_seed_f32). Off: measured (profiles/r03i_knn_seed_stats.log)
-# the seeds cut the insertion rounds per wave 53 -> 15.5 (k 20) and 83 -> 55
-# (k 40) and the selection 56 -> 44 / 208 -> 185 us, but the two seed launches
-# cost 11 + 23 us per call (latency-bound gathers): no net gain yet.
-SPATIAL_SEEDS = False
-
-
 def reduction_order(x):
     """Rounding order of the reference's ``sum(x**2, dim=1)`` (dgcnn.py:8) for a
     (B,C,N) tensor with these strides: torch reduces a channel-innermost layout
@@ -50,15 +41,9 @@ def knn_image_buffers(B, C, N, dev):
     return xx, img
 
 
-def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False, seeds=None,
-            prepared=None):
+def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False, prepared=None):
     """kNN on a (B,C,N) fp32 view. ``strides``/``shape`` let callers describe a
     strided slice of a larger buffer (the engine's point-major concat buffer).
-    ``seeds``: optional int32 (B, N, ks >= k) candidate ids per query (e.g. the
-    previous EdgeConv block's neighbours): the min of their distances is a
-    lower bound of each row's k-th value (dgx_knn_seed_f32) that lets the
-    selection skip the candidates below it. The result does not depend on the
-    seeds (a row whose seed were too high is recomputed exactly).
     ``prepared``: (xx, image) already holding |x|^2 in ``order`` and the operand
     image of exactly this view (knn_image_buffers + a producer kernel): the
     prepare pass is skipped."""
@@ -73,10 +58,11 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
         raise NotImplementedError(f"dgx knn kernels are built for C <= 128 and k <= 64 (C={C}, k={k})")
     cache = getattr(_tls, "cache", None)
     key = None
-    if cache is not None and seeds is None and not return_values:
+    if cache is not None and not return_values:
         key = (x.device, x.data_ptr(), (B, C, N), (sB, sC, sN), x._version, k, order)
         hit = cache.get(key)
         if hit is not None:
+            hit = hit[0]
             return hit if hit.dtype == out_dtype else hit.to(out_dtype)
     L = nat.lib()
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
@@ -95,61 +81,21 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
             nat.check(L.dgx_knn_prepare_f32(nat.f32(x), sB, sC, sN, B, C, N, order, nat.f32(xx), nat.f32(img),
                                             img_bytes, stream), "knn prepare")
         timing = getattr(_tls, "timing", None)
-        T = None
-        spatial = seeds is None and SPATIAL_SEEDS and C <= 4 and 256 <= N <= 4096 and k <= 64
-        if spatial:
-            T = torch.empty((B * N,), dtype=torch.float32, device=x.device)
-            perm = torch.empty((B * N,), dtype=torch.int32, device=x.device)
-            if timing is not None:
-                es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                es0.record()
-            nat.check(L.dgx_knn_spatial_seed_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k, nat.i32(perm),
-                                                 nat.f32(T), stream), "knn spatial seed")
-            if timing is not None:
-                es1.record()
-                seed_log = getattr(_tls, "seed_timing", None)
-                if seed_log is not None:
-                    seed_log.append((es0, es1))
-        graph_seeded = seeds is not None and C > 12 and seeds.shape[-1] <= 24
-        if seeds is not None and not graph_seeded:
-            if seeds.dtype != torch.int32 or not seeds.is_contiguous() or seeds.shape[:2] != (B, N) \
-                    or not k <= seeds.shape[2] <= 64:
-                raise RuntimeError("knn seeds: int32 contiguous (B, N, ks) with k <= ks <= 64")
-            T = torch.empty((B * N,), dtype=torch.float32, device=x.device)
-            if timing is not None:
-                es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                es0.record()
-            nat.check(L.dgx_knn_seed_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, nat.i32(seeds),
-                                         seeds.shape[2], nat.f32(T), stream), "knn seed")
-            if timing is not None:
-                es1.record()
-                seed_log = getattr(_tls, "seed_timing", None)
-                if seed_log is not None:
-                    seed_log.append((es0, es1))
         if timing is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        if graph_seeded:
-            # the selection kernel computes the seeds' distances itself (one launch)
-            if seeds.dtype != torch.int32 or not seeds.is_contiguous() or seeds.shape[:2] != (B, N) \
-                    or not k <= seeds.shape[2]:
-                raise RuntimeError("knn seeds: int32 contiguous (B, N, ks) with k <= ks")
-            rc = L.dgx_knn_select_graph_seeded_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
-                                                   nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
-                                                   nat.i32(idx) if out_dtype == torch.int32 else None,
-                                                   nat.f32(vals), nat.f32(img), img_bytes, nat.i32(seeds),
-                                                   seeds.shape[2], stream)
-        else:
-            rc = L.dgx_knn_select_seeded_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
-                                             nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
-                                             nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
-                                             nat.f32(img), img_bytes, nat.f32(T), stream)
+        rc = L.dgx_knn_select_f32(nat.f32(x), sB, sC, sN, nat.f32(xx), B, C, N, k,
+                                  nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
+                                  nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals),
+                                  nat.f32(img), img_bytes, stream)
         if timing is not None:
             ev1.record()
             timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
     nat.check(rc, "knn")
     if key is not None:
-        cache[key] = idx
+        # the entry holds x too: its storage (whose address is part of the key)
+        # cannot be freed and reused by another tensor while the scope lives
+        cache[key] = (idx, x)
     return (idx, vals) if return_values else idx
 
 
@@ -161,8 +107,8 @@ def knn_cache():
     times (reference model_partseg.py:177 -> dgcnn.py:84, :179 -> :26 and
     :183 -> layers.py:45); the result is a deterministic function
     of those keys, so the shared result is the one each call would compute.
-    The caller's references keep the input alive for the whole scope, so a
-    storage pointer cannot be reused inside it. Thread-local (DataParallel
+    Each entry keeps its input tensor alive for the whole scope, so a storage
+    address cannot be reused by another tensor inside it. Thread-local (DataParallel
     replicas run in threads)."""
     prev = getattr(_tls, "cache", None)
     _tls.cache = {} if prev is None else prev
@@ -172,13 +118,11 @@ def knn_cache():
         _tls.cache = prev
 
 
-def set_knn_timing(lst, seed_lst=None):
+def set_knn_timing(lst):
     """Optional per-thread instrumentation (tools): when a list, every kNN
     selection launch of this thread appends (start_event, end_event,
-    gram_flops, shape) recorded on the launch stream; ``seed_lst`` collects
-    (start_event, end_event) of the admission-seed launches."""
+    gram_flops, shape) recorded on the launch stream."""
     _tls.timing = lst
-    _tls.seed_timing = seed_lst
 
 
 def knn(x, k):

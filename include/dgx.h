@@ -80,19 +80,8 @@ int dgx_bn_lrelu_apply_knn_image_f32(const float* ysel, int B, int N, int Co,
                                      const float* scale, const float* shift, float slope,
                                      float* out, int ldo, void* out_bf16, float* xx,
                                      void* image, size_t image_bytes, void* stream);
-/* A/B tools only: knn3 != 0 lets 3-channel clouds (C <= 4, N <= 4096) take
- * the VALU selection kernel (knn3_kernel); 0 (default) keeps the MFMA
- * selection kernel for them. Process-wide; not for concurrent use. */
-void dgx_knn_set_variant(int knn3);
 int dgx_sqnorm_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                    int B, int C, int N, int order, float* xx, void* stream);
-/* dgx_knn_prepare_f32 for a coordinate cloud (C <= 4) that also writes the
- * first EdgeConv block's PQ = X [W1; W2]^T (M x 2Co, row stride ldpq) from the
- * reference conv weight Wref (Co, 2C) = [W1 | W2] (dgcnn.py:55), each output
- * exactly dgx_gemm_smallk_split_f32's: the cloud is read once for both. */
-int dgx_knn_prepare_pq_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C,
-                           int N, int order, float* xx, void* image, size_t image_bytes,
-                           const float* Wref, int Co, float* PQ, int ldpq, void* stream);
 int dgx_knn_prepare_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                         int B, int C, int N, int order, float* xx,
                         void* image, size_t image_bytes, void* stream);
@@ -100,42 +89,6 @@ int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                        const float* xx, int B, int C, int N, int k,
                        int64_t* idx64, int32_t* idx32, float* vals,
                        const void* image, size_t image_bytes, void* stream);
-/* dgx_knn_select_f32 with admission seeds: seed (B*N fp32, or NULL) holds a
- * lower bound of each row's k-th value in the selection's exact arithmetic
- * (dgx_knn_seed_f32); candidates below it are skipped without list work. A
- * row whose admitted candidates fall short of k is recomputed exactly, so the
- * output equals dgx_knn_select_f32's for any seed. */
-int dgx_knn_select_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
-                              int N, int k, int64_t* idx64, int32_t* idx32, float* vals, const void* image,
-                              size_t image_bytes, const float* seed, void* stream);
-/* Admission seeds from a candidate subset (reference dgcnn.py:88-98: blocks
- * 2-4 search a feature space whose neighbourhoods overlap the previous
- * block's): T[b*N+q] = min over the ks local ids seeds[(b*N+q)*ks + s] of the
- * negated squared distance (dgcnn.py:7-9) as the selection kernel computes it
- * (fmaf chain over the channels with the query doubled, xx from
- * dgx_knn_prepare_f32). ks >= k makes T a lower bound of the k-th value. */
-int dgx_knn_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
-                     const int32_t* seeds, int ks, float* T, void* stream);
-/* dgx_knn_select_f32 seeded by a candidate subset in ONE launch (reference
- * dgcnn.py:88-98, blocks 2-4: the previous block's neighbours): the selection
- * kernel computes the exact distances of the ks (k <= ks <= 24) local ids
- * seeds[(b*N+q)*ks + s] itself (the arithmetic of dgx_knn_seed_f32) and
- * admits only candidates at or above their min. The output equals
- * dgx_knn_select_f32's for any seeds (a row short of k admitted candidates is
- * recomputed exactly); seeds are ignored for C <= 12. */
-int dgx_knn_select_graph_seeded_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B,
-                                    int C, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
-                                    const void* image, size_t image_bytes, const int32_t* seeds, int ks,
-                                    void* stream);
-/* Spatial admission seeds for coordinate clouds (C <= 4, 256 <= N <= 4096,
- * k <= 64; reference dgcnn.py:6-12 on the xyz input of DGCNN block 1,
- * layers.py:45 and model_partseg.py:26): the cloud is ordered along a Morton
- * curve of an 8^3 cell grid (perm: B*N int32 scratch) and T[b*N+q] = the k-th
- * best value among the 64 points around q in that order, in the selection's
- * exact arithmetic (a lower bound of q's k-th value). DGX_EUNSUPPORTED
- * outside that range (select unseeded then). */
-int dgx_knn_spatial_seed_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C,
-                             int N, int k, int32_t* perm, float* T, void* stream);
 
 /* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
  * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in
@@ -172,20 +125,6 @@ int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx,
                             int B, int N, int k, int Co, const float* gamma,
                             float* ysel, uint8_t* arg, float* sumP,
                             float* partials, int nrows, void* stream);
-/* dgx_edge_fwd_gather_f32 + dgx_bn_finalize_f32 in ONE launch: the last
- * workgroup of each channel slice reduces the slice's partial rows (fp64, fixed
- * order) and writes scale / shift / mean / invstd and the running statistics.
- * counters: dgx_edge_fwd_gather_counters(B, N, Co) ints, ZERO before the first
- * call; each launch leaves them zero again. Concurrent launches (other streams)
- * need their own counters. */
-int dgx_edge_fwd_gather_counters(int B, int N, int Co);
-int dgx_edge_fwd_gather_bn_f32(const float* PQ, int ldpq, const int32_t* idx, int B, int N,
-                               int k, int Co, const float* gamma, const float* beta,
-                               float* ysel, uint8_t* arg, float* sumP, float* partials,
-                               int nrows, int* counters, double count,
-                               float* running_mean, float* running_var, double momentum,
-                               double eps, float* scale, float* shift, float* mean,
-                               float* invstd, int64_t* num_batches_tracked, void* stream);
 int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
                         const float* gamma, const float* beta,
                         float* running_mean, float* running_var,
@@ -195,7 +134,10 @@ int dgx_bn_finalize_f32(const float* partials, int nrows, int Co, double count,
 /* dgx_bn_finalize_f32 writing the updated running statistics (and the
  * incremented batch counter) to separate *_new outputs instead of in place —
  * the form a functional op (torch.library) needs: no private copy of the
- * buffers is made first. dgx_bn_finalize_f32 = this with *_new = the inputs. */
+ * buffers is made first. dgx_bn_finalize_f32 = this with *_new = the inputs.
+ * momentum < 0 selects nn.BatchNorm's cumulative average (momentum=None,
+ * torch/nn/modules/batchnorm.py): factor 1 / (*num_batches_tracked + 1) read on
+ * the device; the counter must then not alias num_batches_tracked_new. */
 int dgx_bn_finalize_out_f32(const float* partials, int nrows, int Co, double count,
                             const float* gamma, const float* beta,
                             const float* running_mean, const float* running_var,

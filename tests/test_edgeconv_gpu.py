@@ -66,7 +66,8 @@ def test_edgeconv_block_golden(golden, cuda):
     assert int(blk[1].num_batches_tracked) == 1
 
 
-@pytest.mark.parametrize("C,Co,N,k", [(3, 64, 300, 20), (64, 128, 256, 16), (128, 256, 130, 10), (64, 64, 1024, 20)])
+@pytest.mark.parametrize("C,Co,N,k", [(3, 64, 300, 20), (64, 128, 256, 16), (128, 256, 130, 10), (64, 64, 1024, 20),
+                                      (9, 64, 4096, 20)])   # cfg5 block 1: S3DIS 9-channel input, N 4096
 def test_edgeconv_block_routed(cuda, C, Co, N, k):
     """Strict 1e-3 parity of outputs AND all gradients against the fp64 oracle
     that follows the engine's routing decisions (ragged N, negative gammas)."""
@@ -137,21 +138,33 @@ def test_dgcnn_train_golden(golden, cuda):
 ROUTED_GRAD_TOL = 1e-4
 
 
-@pytest.mark.parametrize("emb,N,k,B", [(64, 128, 10, 2), (1024, 1024, 20, 4),
-                                       (256, 2048, 40, 2),     # cfg3 geometry (N 2048, k 40)
-                                       (128, 4096, 20, 1)])    # cfg5 geometry (N 4096, k 20)
-def test_dgcnn_train_routed(golden, cuda, emb, N, k, B):
+def _clouds(B, N, in_dims, seed):
+    """(B, N, in_dims) synthetic input: unit-cube xyz clouds, or the S3DIS
+    9-channel block layout (prepare_data/indoor3d_util.py:251-260) for cfg5."""
+    from dgx import synth
+    if in_dims == 9:
+        return synth.s3dis_blocks(B, N, seed=seed)
+    return synth.cube_clouds(B, N, seed)
+
+
+@pytest.mark.parametrize("emb,N,k,B,in_dims", [(64, 128, 10, 2, 3), (1024, 1024, 20, 4, 3),
+                                               (256, 2048, 40, 2, 3),     # cfg3 geometry (N 2048, k 40)
+                                               (128, 4096, 20, 1, 3),     # cfg5 cloud size, xyz input
+                                               (1024, 4096, 20, 2, 9)])   # cfg5: DGCNN(in_dims=9), S3DIS blocks
+def test_dgcnn_train_routed(golden, cuda, emb, N, k, B, in_dims):
     """Strict parity of DGCNN train-mode output and EVERY parameter gradient vs
     the fp64 oracle following the engine's routing decisions, at the cfg2 /
-    cfg3 / cfg5 cloud sizes (the kernels' LDS slicing changes with N); one
-    fixed bar for every gradient (ROUTED_GRAD_TOL)."""
+    cfg3 / cfg5 cloud sizes (the kernels' LDS slicing changes with N) and the
+    cfg5 model itself (9-channel S3DIS input, reference models/dgcnn.py:84-98
+    with conv1 = Conv2d(18, 64)); one fixed bar for every gradient
+    (ROUTED_GRAD_TOL)."""
     from models.dgcnn import DGCNN
     from dgx import synth
-    torch.manual_seed(emb + N)
-    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k))
+    torch.manual_seed(emb + N + (in_dims if in_dims != 3 else 0))
+    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k, in_dims=in_dims))
     init = {n: t.detach().clone() for n, t in m.state_dict().items()}
     m = m.to(cuda).train()
-    pts = synth.cube_clouds(B, N, 60 + N)
+    pts = _clouds(B, N, in_dims, 60 + N)
     x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1)
     with Capture() as cap:
         y = m(x)
@@ -289,19 +302,22 @@ def test_dgcnn_full_size_train_step(cuda):
     np.testing.assert_array_equal(idx1, want)
 
 
-def test_dgcnn_bf16_headline_cfg2_routed(cuda):
+@pytest.mark.parametrize("B,N,k,emb,in_dims", [(32, 1024, 20, 1024, 3),    # cfg2: the bench headline
+                                               (2, 4096, 20, 1024, 9)])    # cfg5 model, S3DIS blocks
+def test_dgcnn_bf16_headline_cfg2_routed(cuda, B, N, k, emb, in_dims):
     """The headline configuration (BASELINE configs[1]: DGCNN(emb 1024), B 32,
-    N 1024, k 20, bf16 GEMMs) at full size: train-mode output and every
-    parameter gradient within SURVEY §8(c)'s bf16 bar (2e-2) of the fp64 oracle
-    routed by the engine's own decisions."""
+    N 1024, k 20, bf16 GEMMs) at full size, and the cfg5 model bench.py
+    --config cfg5 times (DGCNN(in_dims=9) on S3DIS blocks, N 4096, k 20; two
+    clouds of the per-GPU 24): train-mode output and every parameter gradient
+    within SURVEY §8(c)'s bf16 bar (2e-2) of the fp64 oracle routed by the
+    engine's own decisions."""
     from dgx import precision, synth
     from models.dgcnn import DGCNN
     torch.manual_seed(0)
-    B, N, k, emb = 32, 1024, 20, 1024
-    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k))
+    m = DGCNN(types.SimpleNamespace(emb_dim=emb, k=k, in_dims=in_dims))
     init = {n: t.detach().clone() for n, t in m.state_dict().items()}
     m = m.to(cuda).train()
-    pts = synth.cube_clouds(B, N, 0)
+    pts = _clouds(B, N, in_dims, 0 if in_dims == 3 else 2)
     x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1)
     gout = torch.from_numpy(synth.uniform(1234, (B, emb, N)) - 0.5).float()
     precision.set("bf16")

@@ -162,50 +162,13 @@ def test_knn_prepare_norms_match_sqnorm(cuda, B, C, N, layout):
     np.testing.assert_array_equal(xx1.cpu().numpy().view(np.uint32), ref.astype(np.float32).view(np.uint32))
 
 
-@pytest.mark.parametrize("C,N,k,layout", [(64, 1024, 20, "pm"), (128, 2048, 40, "pm"), (64, 777, 20, "bcn"),
-                                          (3, 500, 16, "perm"), (9, 1000, 20, "bcn")])
-def test_knn_seeded_equals_unseeded(cuda, C, N, k, layout):
-    """Admission seeds (dgx_knn_seed_f32 + dgx_knn_select_seeded_f32) never change
-    the result: seeded by the exact kNN itself (the bound equals the k-th
-    value: only the top-k and its ties are admitted), by random distinct ids (a
-    loose bound), by another layer's graph (what EdgeConv blocks 2-4 pass), and
-    by an INVALID seed list (k copies of the query itself: the bound exceeds
-    the k-th value, every row falls short of k admitted candidates and is
-    recomputed exactly by the fix-up) — all bit-identical to the unseeded kNN
-    and to the oracle."""
-    import oracle
-    from dgx import synth
-    from dgx.ops import knn_raw
-    B = 2
-    if C == 3:
-        f = torch.from_numpy(synth.cube_clouds(B, N, 5)).permute(0, 2, 1)
-    else:
-        f = torch.from_numpy(synth.relu_normal(6 + C, (B, C, N)))
-    if layout == "pm":   # point-major memory, as the engine's concat buffer
-        f = f.permute(0, 2, 1).contiguous().permute(0, 2, 1)
-    elif layout == "perm":
-        f = f.permute(0, 2, 1).contiguous().permute(0, 2, 1)
-    x = f.to(cuda)
-    base = knn_raw(x, k, out_dtype=torch.int32)
-    np.testing.assert_array_equal(base.cpu().numpy(), oracle.knn(f, k))
-    g = torch.Generator().manual_seed(C + N)
-    rnd = torch.argsort(torch.rand(B, N, N, generator=g), dim=-1)[..., :k + 3].to(torch.int32)
-    other = knn_raw((x * x).contiguous(), k, out_dtype=torch.int32)        # a different graph of the same points
-    selfs = torch.arange(N, dtype=torch.int32).view(1, N, 1).expand(B, N, k).contiguous()
-    for name, seeds in (("exact", base), ("random", rnd), ("other graph", other), ("invalid", selfs)):
-        got = knn_raw(x, k, out_dtype=torch.int32, seeds=seeds.to(cuda).contiguous())
-        assert torch.equal(got, base), name
-
-
 @pytest.mark.parametrize("B,N,k,layout", [(3, 1024, 20, "perm"), (2, 2048, 40, "bcn"), (1, 4096, 64, "perm"),
                                           (2, 256, 16, "bcn"), (2, 777, 33, "perm")])
-def test_knn_spatial_seeds_change_nothing(cuda, monkeypatch, B, N, k, layout):
-    """Coordinate clouds take spatial admission seeds (dgx_knn_spatial_seed_f32):
-    the result is bit-identical to the unseeded selection and to the oracle,
-    including clouds of duplicated points (exact ties at the seed) and a
-    degenerate flat cloud."""
-    import oracle
-    from dgx import ops, synth
+def test_knn_coordinate_clouds_duplicates_and_flat(cuda, B, N, k, layout):
+    """Coordinate clouds (reference dgcnn.py:6-12 on xyz input) with duplicated
+    points (exact distance ties, some at the k-th value) and a degenerate flat
+    cloud (one coordinate constant): selected values bit-exact, indices in
+    canonical order, against the oracle."""
     from dgx.ops import knn_raw
     pts = synth.cube_clouds(B, N, N + k)
     pts[:, N // 2:N // 2 + N // 8] = pts[:, :N // 8]            # duplicated points: ties
@@ -215,48 +178,9 @@ def test_knn_spatial_seeds_change_nothing(cuda, monkeypatch, B, N, k, layout):
     if layout == "bcn":
         f = f.contiguous()
     x = f.to(cuda)
-    monkeypatch.setattr(ops, "SPATIAL_SEEDS", True)
-    seeded = knn_raw(x, k)
-    monkeypatch.setattr(ops, "SPATIAL_SEEDS", False)
-    plain = knn_raw(x, k)
-    assert torch.equal(seeded, plain)
     idx, vals = oracle.knn(f, k, return_values=True)
     got_idx, got_vals = knn_raw(x, k, return_values=True)
-    from conftest import assert_knn_equivalent
-    assert_knn_equivalent(seeded.cpu().numpy(), got_vals.cpu().numpy(), idx, vals)
-
-
-@pytest.fixture
-def knn3_variant():
-    from dgx import _native as nat
-    nat.lib().dgx_knn_set_variant(1)
-    yield
-    nat.lib().dgx_knn_set_variant(0)
-
-
-@pytest.mark.parametrize("B,N,k,layout", [(2, 77, 1, "perm"), (1, 64, 64, "bcn"), (3, 1024, 20, "perm"),
-                                          (2, 2048, 40, "bcn"), (1, 4096, 20, "perm"), (2, 333, 33, "bcn")])
-def test_knn3_variant_vs_oracle(cuda, knn3_variant, B, N, k, layout):
-    """The VALU 3-channel selection kernel (dgx_knn_set_variant(1), off by
-    default: measured no faster) returns the reference's neighbours too."""
-    from models.dgcnn import knn
-    pts = synth.cube_clouds(B, N, 3 * N + k)
-    idx = knn(_view(pts, layout, cuda), k).cpu().numpy()
-    ref_idx, ref_vals = oracle.knn(_cpu_view(pts, layout), k, return_values=True)
-    if N <= 1024:
-        pd = oracle.pairwise(_cpu_view(pts, layout))
-        assert_knn_equivalent(idx, np.take_along_axis(pd, idx, 2), ref_idx, ref_vals)
-    else:
-        np.testing.assert_array_equal(idx, ref_idx)
-
-
-def test_knn3_variant_ties(golden, cuda, knn3_variant):
-    from models.dgcnn import knn
-    g = golden("knn_cases.npz")
-    pts = g["ties_perm_x"]
-    idx = knn(_view(pts, "perm", cuda), 20).cpu().numpy()
-    pd = oracle.pairwise(_cpu_view(pts, "perm"))
-    assert_knn_equivalent(idx, np.take_along_axis(pd, idx, 2), g["ties_perm_idx"], g["ties_perm_val"])
+    assert_knn_equivalent(got_idx.cpu().numpy(), got_vals.cpu().numpy(), idx, vals)
 
 
 @pytest.mark.parametrize("B,N,Co", [(4, 1024, 64), (2, 2048, 128), (3, 96, 64)])
@@ -297,28 +221,3 @@ def test_apply_writes_next_knn_image(cuda, B, N, Co):
     a = knn_raw(xcat[:, off:], 20, prepared=(xx, img), **kw)
     b = knn_raw(xcat[:, off:], 20, **kw)
     assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("B,N,Co,layout", [(32, 1024, 64, "perm"), (3, 777, 24, "bcn"), (2, 2048, 64, "perm")])
-def test_prepare_with_block1_pq(cuda, B, N, Co, layout):
-    """dgx_knn_prepare_pq_f32: the kNN operands of a coordinate cloud equal
-    dgx_knn_prepare_f32's and its PQ rows equal dgx_gemm_smallk_split_f32's,
-    bit for bit."""
-    from dgx import _native as nat
-    from dgx import gemm as G
-    from dgx.ops import knn_image_buffers, reduction_order
-    L = nat.lib()
-    x = _view(synth.cube_clouds(B, N, N + Co), layout, cuda)
-    w = torch.randn(Co, 6, 1, 1, generator=torch.Generator().manual_seed(Co)).to(cuda)
-    order = reduction_order(x)
-    st = nat.stream_of(x)
-    xx1, img1 = knn_image_buffers(B, 3, N, cuda)
-    xx2, img2 = knn_image_buffers(B, 3, N, cuda)
-    pq = torch.empty(B * N, 2 * Co, device=cuda)
-    nat.check(L.dgx_knn_prepare_f32(nat.f32(x), *x.stride(), B, 3, N, order, nat.f32(xx1), nat.f32(img1),
-                                    img1.numel() * 4, st), "prepare")
-    nat.check(L.dgx_knn_prepare_pq_f32(nat.f32(x), *x.stride(), B, 3, N, order, nat.f32(xx2), nat.f32(img2),
-                                       img2.numel() * 4, nat.f32(w), Co, nat.f32(pq), 2 * Co, st), "prepare pq")
-    ref = G.mm_smallk_split(x.permute(0, 2, 1).reshape(B * N, 3), w, Co)
-    assert torch.equal(xx1, xx2) and torch.equal(img1, img2)
-    assert torch.equal(pq.view(torch.int32), ref.view(torch.int32))

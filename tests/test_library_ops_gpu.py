@@ -130,3 +130,26 @@ def test_torch_export_dgcnn_eval(cuda):
     assert any("dgx.edgeconv_chain" in t for t in targets) and any("dgx.pointconv" in t for t in targets), targets
     with torch.no_grad():
         assert rel_err(ep.module()(x.contiguous()).cpu(), m(x.contiguous()).cpu()) == 0.0
+
+
+def test_bn_cumulative_average_op_path(cuda, monkeypatch):
+    """BatchNorm with momentum=None (nn.BatchNorm's cumulative moving average):
+    the op layer's finalize reads num_batches_tracked on the device (no host
+    read, so the step stays capturable) and three train steps leave the same
+    running statistics and counters as the autograd-Function path, which
+    updates the module buffers in place like nn.BatchNorm."""
+    from dgx import library
+    base = _model(seed=6)
+    for m in base.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = None
+    x = _cloud(cuda, seed=11)
+    gout = torch.randn((4, 128, 512), device=cuda)
+    ma, mb = copy.deepcopy(base).to(cuda).train(), copy.deepcopy(base).to(cuda).train()
+    for _ in range(3):
+        monkeypatch.setattr(library, "ENABLED", True)
+        a = _step(ma, x, gout)
+        monkeypatch.setattr(library, "ENABLED", False)
+        b = _step(mb, x, gout)
+        _assert_same(a, b)
+    assert int(ma.conv1[1].num_batches_tracked) == 3

@@ -10,9 +10,6 @@ from dgx import synth  # noqa: E402
 from dgx.ops import knn_raw  # noqa: E402
 
 dev = torch.device("cuda:0")
-if "DGX_SPATIAL_SEEDS" in os.environ:
-    from dgx import ops
-    ops.SPATIAL_SEEDS = os.environ["DGX_SPATIAL_SEEDS"] == "1"
 which = sys.argv[1] if len(sys.argv) > 1 else "C3"
 B, N, k = (32, 2048, 40) if which == "C3k40" else (32, 1024, 20)
 x = torch.from_numpy(synth.cube_clouds(B, N, 0)).to(dev).permute(0, 2, 1)
