@@ -29,6 +29,7 @@ import torch
 
 from . import _native as nat
 from . import bn as bn_
+from . import cpu
 from . import gemm as G
 from . import precision as prec
 from .ops import knn_image_buffers, knn_raw, reduction_order
@@ -379,7 +380,10 @@ def edgeconv_stack_pair(x, k, convs, training=None, preps=None):
     ``preps``: optional per-block bf16 weight copies (gemm.prep_weights) made
     by the caller in one launch with other layers' (None for block 1).
     ``training`` is accepted for call compatibility only: every BatchNorm
-    decides batch vs running statistics by its own flags, as nn.BatchNorm does."""
+    decides batch vs running statistics by its own flags, as nn.BatchNorm does.
+    A host tensor takes the CPU path (dgx.cpu)."""
+    if cpu.is_cpu(x):
+        return cpu.edgeconv_stack_pair(x, k, convs, training)
     nat.require_device(x)
     if x.dtype != torch.float32:
         x = x.float()

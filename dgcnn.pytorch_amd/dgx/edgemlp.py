@@ -24,6 +24,7 @@ and its BN statistics come from the EdgeConv gather kernel.
 import torch
 
 from . import _native as nat
+from . import cpu
 from . import bn as bn_
 from . import gemm as G
 from . import precision as prec
@@ -294,7 +295,10 @@ def edge_mlp2(x, k, conv1, conv2, training=None, knn_src=None):
     ``training`` is accepted for call compatibility only (dgx.bn: each BN
     module's own flags decide batch vs running statistics). ``knn_src``:
     optional (B, C', N) tensor the neighbours are searched on instead of x
-    (upstream's dim9 semseg graph: kNN on the normalised xyz channels)."""
+    (upstream's dim9 semseg graph: kNN on the normalised xyz channels).
+    A host tensor takes the CPU path (dgx.cpu)."""
+    if cpu.is_cpu(x):
+        return cpu.edge_mlp2(x, k, conv1, conv2, training, knn_src)
     nat.require_device(x)
     if x.dtype != torch.float32:
         x = x.float()

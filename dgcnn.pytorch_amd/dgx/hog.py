@@ -1,10 +1,11 @@
 """compute_hog_1x1's work after the kNN call, on the device (SURVEY §8 row f1;
 reference models/model_partseg.py:28-92): one C-ABI call (dgx_hog_1x1_f32,
 csrc/hog.hip) replaces the D2H copy, np.linalg.svd over B*N neighbourhoods,
-the H2D copy and the histogram votes. No host round trip, no CPU fallback."""
+the H2D copy and the histogram votes. No host round trip; host tensors take the CPU path."""
 import torch
 
 from . import _native as N
+from . import cpu
 
 # k range of the device path: csrc/svd3.h restates LAPACK dgesdd's tall-matrix
 # path (QR first), which dgesdd takes for k >= 5 rows (its mnthr = 3*11/6), and
@@ -14,7 +15,10 @@ HOG_K_MIN, HOG_K_MAX = 5, 64
 
 def hog_1x1(x, idx):
     """x (B, 3, N) fp32 on the device, idx (B, N, k) int64 local kNN ids ->
-    (B, N, 18) histograms, as the reference computes them from the same idx."""
+    (B, N, 18) histograms, as the reference computes them from the same idx.
+    Host tensors take the reference's own host path (dgx.cpu.hog_1x1)."""
+    if cpu.is_cpu(x) and cpu.is_cpu(idx):
+        return cpu.hog_1x1(x, idx)
     N.require_device(x, idx)
     B, C, P = x.shape
     if C != 3:

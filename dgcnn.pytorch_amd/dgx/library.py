@@ -34,6 +34,7 @@ import torch
 from torch import Tensor
 
 from . import bn as bn_
+from . import cpu
 from . import edgeconv as E
 from . import gemm as G
 from . import ops
@@ -126,6 +127,11 @@ def knn(x: Tensor, k: int) -> Tensor:
     return ops.knn(x, k).clone() if getattr(ops._tls, "cache", None) is not None else ops.knn(x, k)
 
 
+@knn.register_kernel("cpu")
+def _(x, k):
+    return cpu.knn(x, k)
+
+
 @knn.register_fake
 def _(x, k):
     B, _, N = x.shape
@@ -156,6 +162,14 @@ def graph_feature(x: Tensor, k: int, mode: int) -> tuple[Tensor, Tensor]:
     return ops._GraphFeature.forward(_Rec(), xf, idx, mode), idx.clone() if shared else idx
 
 
+@graph_feature.register_kernel("cpu")
+def _(x, k, mode):
+    xf = x.float().detach()
+    idx = cpu.knn(xf, k)
+    out = cpu.graph_feature(xf, k, knn_only=mode == ops.nat.GF_KNN_ONLY, disp_only=mode == ops.nat.GF_DISP, idx=idx)
+    return out, idx.to(_I32)
+
+
 @graph_feature.register_fake
 def _(x, k, mode):
     B, _, N = x.shape
@@ -170,6 +184,27 @@ def graph_feature_backward(grad: Tensor, idx: Tensor, C: int, mode: int) -> Tens
     B, N, _ = idx.shape
     rec.shape = (B, C, N)
     return ops._GraphFeature.backward(rec, grad)[0]
+
+
+@graph_feature_backward.register_kernel("cpu")
+def _(grad, idx, C, mode):
+    """dx of the edge tensor (reference dgcnn.py:31-44 autograd): neighbour
+    channels scatter-add to x_j, centre channels sum over k into x_i."""
+    B, N, k = idx.shape
+    flat = (idx.long() + torch.arange(B).view(-1, 1, 1) * N).view(-1)
+    if mode == ops.nat.GF_KNN_ONLY:                       # (B, N, k, C) = x_j
+        gn, gc = grad.reshape(B * N * k, C), None
+    elif mode == ops.nat.GF_DISP:                         # (B, C, N, k) = x_j - x_i
+        g = grad.permute(0, 2, 3, 1).reshape(B * N * k, C)
+        gn, gc = g, -g
+    else:                                                 # (B, 2C, N, k) = cat(x_j, x_i)
+        g = grad.permute(0, 2, 3, 1).reshape(B * N * k, 2 * C)
+        gn, gc = g[:, :C], g[:, C:]
+    rows = torch.zeros((B * N, C), dtype=torch.float32)
+    rows.index_add_(0, flat, gn.float())
+    if gc is not None:
+        rows += gc.float().reshape(B * N, k, C).sum(dim=1)
+    return rows.view(B, N, C).permute(0, 2, 1).contiguous()
 
 
 @graph_feature_backward.register_fake

@@ -10,6 +10,7 @@ import threading
 import torch
 
 from . import _native as nat
+from . import cpu
 
 _tls = threading.local()
 
@@ -67,8 +68,27 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     L = nat.lib()
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
     vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
-    img_bytes = L.dgx_knn_image_bytes(B, C, N)
     stream = nat.stream_of(x)
+    if prepared is None and L.dgx_knn_grid_ok(C, N, k):
+        # coordinate clouds: one launch over a cell grid built in LDS (no
+        # prepare pass, no operand image; |x|^2 of <= 3 channels rounds the same
+        # in either torch order)
+        timing = getattr(_tls, "timing", None)
+        with torch.cuda.device(x.device):
+            if timing is not None:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            rc = L.dgx_knn_grid_f32(nat.f32(x), sB, sC, sN, B, C, N, k,
+                                    nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
+                                    nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals), stream)
+            if timing is not None:
+                ev1.record()
+                timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
+        nat.check(rc, "knn (grid)")
+        if key is not None:
+            cache[key] = (idx, x)
+        return (idx, vals) if return_values else idx
+    img_bytes = L.dgx_knn_image_bytes(B, C, N)
     if prepared is not None:
         xx, img = prepared
         if xx.numel() != B * N or img.numel() * 4 < img_bytes:
@@ -128,6 +148,8 @@ def set_knn_timing(lst):
 def knn(x, k):
     """Drop-in for reference ``knn(x, k)`` (models/dgcnn.py:6-12): int64 (B,N,k)
     local indices, nearest first; ties in canonical (index ascending) order."""
+    if cpu.is_cpu(x):   # host tensors: the CPU path (dgx.cpu), same canonical result
+        return cpu.knn(x, k)
     x = _as_f32(x.detach())
     return knn_raw(x, k)
 
@@ -173,6 +195,8 @@ def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
     Default: (B,2C,N,k) fp32 contiguous, channels [0,C) = x_j, [C,2C) = x_i
     (dgcnn.py:42). knn_only: (B,N,k,C) neighbour rows (dgcnn.py:37-38).
     disp_only: (B,C,N,k) x_j - x_i (dgcnn.py:39-40). Differentiable w.r.t. x."""
+    if cpu.is_cpu(x):
+        return cpu.graph_feature(x, k, knn_only, disp_only, idx)
     nat.require_device(x)
     x = _as_f32(x)
     if idx is None:

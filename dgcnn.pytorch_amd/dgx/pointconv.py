@@ -14,6 +14,7 @@ average).
 import torch
 
 from . import _native as nat
+from . import cpu
 from . import bn as bn_
 from . import gemm as G
 from . import precision as prec
@@ -134,7 +135,9 @@ def pointconv_bn_lrelu(X, B, N, seq, training=None, X16=None, wprep=None):
     (precision "bf16"), the GEMM operand. ``wprep``: optional bf16 (W, W^T) of
     the conv weight already made for this step (gemm.prep_weights).
     ``training`` is accepted for call compatibility only (dgx.bn: each BN
-    module's own flags decide)."""
+    module's own flags decide). A host tensor takes the CPU path (dgx.cpu)."""
+    if cpu.is_cpu(X):
+        return cpu.pointconv_bn_lrelu(X, B, N, seq, training)
     nat.require_device(X)
     conv, bn, act = seq[0], seq[1], seq[2]
     if conv.bias is not None or bn.weight is None:

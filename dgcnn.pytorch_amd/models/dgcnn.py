@@ -85,6 +85,11 @@ class DGCNN(nn.Module):
         return [self.conv1, self.conv2, self.conv3, self.conv4]
 
     def forward(self, x):
+        if x.device.type == "cpu":
+            # host tensors (reference dgcnn.py:19-20 runs on either device): the
+            # CPU path of every block (dgx.cpu), same modules and state
+            feats, _ = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training)
+            return pointconv_bn_lrelu(feats, x.shape[0], x.shape[2], self.conv5, self.training)
         if _library.enabled_for(self):
             # the same kernels behind torch.ops.dgx custom ops (torch.compile / export see one node each)
             return _library.dgcnn_forward(self, x)

@@ -43,13 +43,6 @@ def test_net_state_dict_matches_reference(golden):
             assert tuple(sd[k].shape) == g["init." + k].shape, k
 
 
-def test_product_rejects_cpu_tensors():
-    """The engine has no CPU fallback: a CPU cloud fails loudly at the kNN."""
-    from models.model_partseg import compute_hog_1x1
-    with pytest.raises(RuntimeError):
-        compute_hog_1x1(torch.zeros(1, 3, 32), 4, use_cpu=True)
-
-
 def _hog_agreement(got, ref):
     """(fraction of points bit-identical, fraction within HOG_TOL per point)."""
     exact = (got == ref).all(axis=-1)
