@@ -1,0 +1,520 @@
+// libdgx_torch.so — the PyTorch-ROCm C++ extension of the engine: DGCNN's
+// train-mode forward (4 EdgeConv blocks + conv5, reference models/dgcnn.py:
+// 84-103) and its backward as ONE custom op, dgx_host::dgcnn_train, whose
+// autograd node is C++ (torch::autograd::Function). Every launch goes to
+// libdgx.so's C ABI (include/dgx.h) straight from C++: the eager step issues
+// its ~60 kernels without a Python frame, a ctypes conversion or a Python
+// autograd node per launch (the Python dispatch of dgx.edgeconv /
+// dgx.pointconv costs ~1 ms of host time per cfg2 step).
+//
+// The kernel sequence, operand views, launch arguments and reduction orders
+// are exactly those of the Python path for precision "bf16" in training mode
+// (dgx.edgeconv._EdgeConvStack, dgx.pointconv._PointConvBNLReLU,
+// dgx.gemm.lds_*, dgx.bn.batch_stats / backward_consts, dgx.ops.knn_raw), so
+// results are bit-identical (tests/test_host_ext_gpu.py). dgx.host decides
+// when this op applies (bf16, plain BatchNorm2d in training mode with running
+// statistics and a momentum, gradients wanted); every other case keeps the
+// Python dispatch of the same kernels.
+#include <ATen/ATen.h>
+#include <torch/library.h>
+#include <torch/csrc/autograd/custom_function.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/dgx.h"
+
+namespace {
+
+using at::Tensor;
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+constexpr int kBlocks = 4;          // EdgeConv blocks of DGCNN (dgcnn.py:54-73)
+constexpr int kEpiStore = 0, kEpiStats16 = 4, kEpiSlab = 3;
+constexpr int64_t kSlabCapMB = 8;   // dgx.gemm.SLAB_CAP_MB default
+
+void check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "dgx: ", what, " failed (", rc, ": ", dgx_strerror(rc), ")");
+}
+
+template <typename T = float>
+T* P(const Tensor& t) { return t.defined() ? static_cast<T*>(t.data_ptr()) : nullptr; }
+
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct Ctx {
+  at::TensorOptions f32, bf16, i32, u8;
+  void* stream;
+  Tensor empty(at::IntArrayRef shape, const at::TensorOptions& o) const { return at::empty(shape, o); }
+};
+
+// per-channel BatchNorm state of one layer (dgx.bn.Stats)
+struct Stats {
+  Tensor scale, shift, mean, invstd;
+};
+
+// dgx.bn._compact: a tall (rows, 2, co) partial array pre-reduced to ~128 rows
+std::pair<Tensor, int> compact(const Ctx& c, const Tensor& partials, int rows, int co) {
+  if (rows <= 1024) return {partials, rows};
+  const int R = 128, S = rows / R, left = rows - S * R;
+  Tensor out = c.empty({R + left, 2, co}, c.f32);
+  check(dgx_slab_reduce_f32(P(partials), S, R, 2 * co, R, P(out), 2 * co, c.stream), "bn partial reduce");
+  if (left) out.narrow(0, R, left).copy_(partials.view({-1, 2, co}).narrow(0, (int64_t)S * R, left));
+  return {out, R + left};
+}
+
+// dgx.bn.batch_stats for a BatchNorm in training mode that tracks running
+// statistics with a momentum: the finalize updates the module buffers in place
+// and bumps the batch counter on the device
+Stats batch_stats(const Ctx& c, Tensor partials, int rows, double count, const Tensor& gamma, const Tensor& beta,
+                  const Tensor& rm, const Tensor& rv, const Tensor& nbt, double momentum, double eps) {
+  const int co = (int)gamma.size(0);
+  Stats st{c.empty({co}, c.f32), c.empty({co}, c.f32), c.empty({co}, c.f32), c.empty({co}, c.f32)};
+  auto pr = compact(c, partials, rows, co);
+  check(dgx_bn_finalize_out_f32(P(pr.first), pr.second, co, count, P(gamma), P(beta), P(rm), P(rv), momentum, eps,
+                                P(st.scale), P(st.shift), P(st.mean), P(st.invstd), P<int64_t>(nbt), P(rm), P(rv),
+                                P<int64_t>(nbt), c.stream),
+        "bn finalize");
+  return st;
+}
+
+// dgx.ops.knn_image_buffers
+std::pair<Tensor, Tensor> knn_image_buffers(const Ctx& c, int B, int C, int N) {
+  const size_t img_bytes = dgx_knn_image_bytes(B, C, N);
+  Tensor xx = c.empty({(int64_t)B * N}, c.f32);
+  Tensor img = c.empty({(int64_t)((std::max<size_t>(img_bytes, 4) + 3) / 4)}, c.f32);
+  return {xx, img};
+}
+
+// dgx.ops.knn_raw (int32 ids; prepared: the producer already wrote |x|^2 + image)
+Tensor knn(const Ctx& c, const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int k, int order,
+           const std::pair<Tensor, Tensor>* prepared) {
+  Tensor idx = c.empty({B, N, k}, c.i32);
+  const size_t img_bytes = dgx_knn_image_bytes(B, C, N);
+  std::pair<Tensor, Tensor> bufs;
+  if (prepared) {
+    bufs = *prepared;
+    TORCH_CHECK(bufs.first.numel() == (int64_t)B * N && (size_t)bufs.second.numel() * 4 >= img_bytes,
+                "knn: prepared |x|^2 / image buffers do not match the cloud");
+  } else {
+    bufs = knn_image_buffers(c, B, C, N);
+    check(dgx_knn_prepare_f32(x, sB, sC, sN, B, C, N, order, P(bufs.first), P(bufs.second), img_bytes, c.stream),
+          "knn prepare");
+  }
+  check(dgx_knn_select_f32(x, sB, sC, sN, P(bufs.first), B, C, N, k, nullptr, P<int32_t>(idx), nullptr,
+                           P(bufs.second), img_bytes, c.stream),
+        "knn");
+  return idx;
+}
+
+int64_t ld_of(const Tensor& t) {   // dgx.gemm._bf16_2d / _operand row stride
+  return t.size(0) > 1 ? t.stride(0) : std::max<int64_t>(8, t.size(1));
+}
+
+// dgx.gemm.lds_xwt: out (M,N) = x16 (M,K) w16 (N,Kw)^T, plain store or bf16 store + column statistics
+Tensor lds_xwt(const Ctx& c, const Tensor& x16, const Tensor& w16, Tensor* part_out) {
+  const int M = (int)x16.size(0), K = (int)x16.size(1), N = (int)w16.size(0), Kw = (int)w16.size(1);
+  TORCH_CHECK(Kw == K || Kw == 2 * K, "dgx gemm: weight k extent does not match the operand's");
+  const bool stats = part_out != nullptr;
+  Tensor out = c.empty({M, N}, stats ? c.bf16 : c.f32);
+  Tensor part;
+  if (stats) part = c.empty({dgx_gemm_stats_rows(M), 2, N}, c.f32);
+  check(dgx_gemm_lds_bf16(x16.data_ptr(), ld_of(x16), w16.data_ptr(), ld_of(w16), 0, M, N, Kw, K,
+                          stats ? kEpiStats16 : kEpiStore, 1, P(out), out.stride(0), stats ? P(part) : nullptr,
+                          nullptr, 0, c.stream),
+        "gemm lds nt");
+  if (stats) *part_out = part;
+  return out;
+}
+
+// dgx.gemm.lds_atb: out = a16^T b16 (split-K slabs, fixed-order sum); split_rows un-stacks [W1;W2]
+void lds_atb(const Ctx& c, const Tensor& a16, const Tensor& b16, Tensor& out, int split_rows) {
+  const int R = (int)a16.size(0), M = (int)a16.size(1), N = (int)b16.size(1);
+  int S = dgx_gemm_splits(M, N, R);
+  const int64_t bytes = (int64_t)M * N * 4;
+  if (kSlabCapMB > 0 && bytes < (1 << 20)) S = (int)std::max<int64_t>(1, std::min<int64_t>(S, (kSlabCapMB << 20) / bytes));
+  int64_t chunk = cdiv(R, S);
+  chunk = cdiv(chunk, 64) * 64;
+  const int used = (int)cdiv(R, chunk);
+  Tensor slab = c.empty({used, M, N}, c.f32);
+  check(dgx_gemm_lds_bf16(a16.data_ptr(), ld_of(a16), b16.data_ptr(), ld_of(b16), 1, M, N, R, R, kEpiSlab, S,
+                          P(slab), N, nullptr, nullptr, 0, c.stream),
+        "gemm lds tn");
+  check(dgx_slab_reduce_f32(P(slab), used, M, N, split_rows > 0 ? split_rows : M, P(out), out.stride(0), c.stream),
+        "slab reduce");
+}
+
+// dgx.gemm.mm_atb with a bf16 (R, M) and an fp32 (R, N) operand (block 1's
+// weight gradient: dPQ^T x, K = 3 raw coordinates)
+void mm_atb(const Ctx& c, const Tensor& a, const Tensor& b, Tensor& out, int split_rows) {
+  const int R = (int)a.size(0), M = (int)a.size(1), N = (int)b.size(1);
+  const int S = dgx_gemm_splits(M, N, R);
+  Tensor slab = c.empty({S, M, N}, c.f32);
+  auto ld = [](const Tensor& t) { return t.size(0) > 1 ? t.stride(0) : std::max<int64_t>(1, t.size(1)); };
+  check(dgx_gemm_bf16(a.data_ptr(), a.scalar_type() == at::kBFloat16, 1, ld(a), b.data_ptr(),
+                      b.scalar_type() == at::kBFloat16, 1, ld(b), M, N, R, kEpiSlab, S, P(slab), N, nullptr, c.stream),
+        "gemm bf16");
+  int64_t chunk = cdiv(R, S);
+  chunk = cdiv(chunk, 32) * 32;
+  const int used = (int)cdiv(R, chunk);
+  check(dgx_slab_reduce_f32(P(slab), used, M, N, split_rows > 0 ? split_rows : M, P(out), out.stride(0), c.stream),
+        "slab reduce");
+}
+
+// per-step bf16 operand copies of conv2..conv5 (dgx.gemm.prep_layout / prep_weights):
+// [nt, tn] views of one buffer, nt of an EdgeConv weight in the split [hi | lo] form
+struct Prep {
+  Tensor buf;
+  std::array<Tensor, 4> nt, tn;
+};
+
+Prep prep_weights(const Ctx& c, const std::array<Tensor, 4>& w) {
+  int rows[4], cols[4], st[4];
+  int64_t off_nt[4], off_tn[4], total = 0;
+  std::array<std::array<int64_t, 2>, 4> shp_nt, shp_tn;
+  for (int j = 0; j < 4; ++j) {
+    const bool edge = j < 3;
+    rows[j] = (int)w[j].size(0);
+    cols[j] = (int)(edge ? w[j].size(1) / 2 : w[j].size(1));
+    st[j] = edge ? 3 : 0;                      // stacked | split for blocks 2-4, plain for conv5
+    const int64_t R = edge ? 2 * rows[j] : rows[j];
+    const int64_t n_tn = R * cols[j], n_nt = (edge ? 2 : 1) * R * cols[j];
+    off_nt[j] = total;
+    off_tn[j] = total + cdiv(n_nt, 8) * 8;
+    shp_nt[j] = {R, edge ? 2 * cols[j] : cols[j]};
+    shp_tn[j] = {cols[j], R};
+    total += cdiv(n_nt, 8) * 8 + cdiv(n_tn, 8) * 8;
+  }
+  Prep p;
+  p.buf = c.empty({total}, c.bf16);
+  const void* W[4];
+  void* NT[4];
+  void* TN[4];
+  for (int j = 0; j < 4; ++j) {
+    p.nt[j] = p.buf.narrow(0, off_nt[j], shp_nt[j][0] * shp_nt[j][1]).view({shp_nt[j][0], shp_nt[j][1]});
+    p.tn[j] = p.buf.narrow(0, off_tn[j], shp_tn[j][0] * shp_tn[j][1]).view({shp_tn[j][0], shp_tn[j][1]});
+    TORCH_CHECK(w[j].scalar_type() == at::kFloat && w[j].is_contiguous(), "dgx weight prep: fp32 weights expected");
+    W[j] = w[j].data_ptr();
+    NT[j] = p.nt[j].data_ptr();
+    TN[j] = p.tn[j].data_ptr();
+  }
+  check(dgx_weight_prep_multi_bf16(4, reinterpret_cast<const float* const*>(W), rows, cols, st, NT, TN, c.stream),
+        "weight prep");
+  return p;
+}
+
+// hyper-parameters per layer (5 = four EdgeConv blocks + conv5)
+struct Hyper {
+  std::array<double, 5> momentum, eps, slope;
+};
+
+class DgcnnTrain : public torch::autograd::Function<DgcnnTrain> {
+ public:
+  // params: (w, gamma, beta) x 5; bufs: (running_mean, running_var, num_batches_tracked) x 5;
+  // idx0: optional int32 (B,N,k) kNN ids of x (a shared kNN-cache entry) or undefined
+  static variable_list forward(AutogradContext* ctx, Tensor x, at::TensorList params, at::TensorList bufs,
+                               std::optional<Tensor> idx0_opt, int64_t k, std::vector<double> hyper) {
+    const Tensor idx0 = idx0_opt.has_value() ? *idx0_opt : Tensor();
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+    Ctx c;
+    c.f32 = x.options().dtype(at::kFloat);
+    c.bf16 = x.options().dtype(at::kBFloat16);
+    c.i32 = x.options().dtype(at::kInt);
+    c.u8 = x.options().dtype(at::kByte);
+    c.stream = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(x.device().index()).stream();
+    Hyper h;
+    for (int l = 0; l < 5; ++l) {
+      h.momentum[l] = hyper[3 * l];
+      h.eps[l] = hyper[3 * l + 1];
+      h.slope[l] = hyper[3 * l + 2];
+    }
+    const int B = (int)x.size(0), C0 = (int)x.size(1), N = (int)x.size(2), K = (int)k;
+    const int64_t M = (int64_t)B * N;
+    std::array<int, kBlocks> co, cin;
+    int total = 0;
+    for (int l = 0; l < kBlocks; ++l) {
+      co[l] = (int)params[3 * l].size(0);
+      cin[l] = (int)params[3 * l].size(1) / 2;
+      total += co[l];
+    }
+    const Tensor& w5 = params[12];
+    const int emb = (int)w5.size(0);
+    TORCH_CHECK(w5.size(1) == total, "dgx dgcnn_train: conv5 takes the concat of the blocks");
+
+    // one launch for every bf16 operand copy of the step (blocks 2-4, conv5)
+    Prep prep = prep_weights(c, {params[3].contiguous(), params[6].contiguous(), params[9].contiguous(),
+                                 w5.reshape({emb, total}).contiguous()});
+    Tensor xcat = c.empty({M, total}, c.f32);
+    Tensor xcat16 = c.empty({M, total}, c.bf16);
+    // point-major rows of x (a view for the channel-innermost layout the scripts feed)
+    Tensor x_pm = x.permute({0, 2, 1}).reshape({M, C0}).contiguous();
+    const double count = (double)M * K;
+    std::vector<Tensor> saved;   // per block: idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd
+    std::pair<Tensor, Tensor> next_prepared;
+    bool have_prepared = false;
+    int off_in = 0, off = 0;   // column offsets of block l's input and output in the concat buffer
+    for (int l = 0; l < kBlocks; ++l) {
+      const Tensor &w = params[3 * l], &gamma = params[3 * l + 1], &beta = params[3 * l + 2];
+      Tensor idx, PQ;
+      if (l == 0) {
+        if (idx0.defined()) {
+          idx = idx0;
+        } else {
+          // the reference's sum(x**2, dim=1) rounding order for x's strides (dgx.ops.reduction_order)
+          const int order = (C0 > 1 && N > 1 && x.stride(1) < x.stride(2)) ? 1 : 0;
+          idx = knn(c, P(x), x.stride(0), x.stride(1), x.stride(2), B, C0, N, K, order, nullptr);
+        }
+        TORCH_CHECK(cin[0] <= 16, "dgx dgcnn_train: block 1 takes raw coordinates (C <= 16)");
+        Tensor wr = w.reshape({co[0], 2 * cin[0]}).contiguous();
+        PQ = c.empty({M, 2 * co[0]}, c.f32);
+        check(dgx_gemm_smallk_split_f32(P(x_pm), M > 1 ? x_pm.stride(0) : C0, P(wr), (int)M, co[0], cin[0], P(PQ),
+                                        2 * co[0], c.stream),
+              "gemm small-k");
+      } else {
+        // blocks 2-4 see contiguous (B,C,N) features: the strided rounding order
+        idx = knn(c, P(xcat) + off_in, (int64_t)N * total, 1, total, B, cin[l], N, K, 0,
+                  have_prepared ? &next_prepared : nullptr);
+        Tensor X16 = xcat16.narrow(1, off_in, cin[l]);
+        PQ = lds_xwt(c, X16, prep.nt[l - 1], nullptr);
+      }
+      have_prepared = false;
+      Tensor ysel = c.empty({M, co[l]}, c.f32);
+      Tensor arg = c.empty({M, co[l]}, c.u8);
+      Tensor sumP = c.empty({M, co[l]}, c.f32);
+      const int prow = dgx_edge_partials_rows(B, N, co[l]);
+      Tensor partials = c.empty({prow, 2, co[l]}, c.f32);
+      check(dgx_edge_fwd_gather_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(idx), B, N, K, co[l], P(gamma), P(ysel),
+                                    P<uint8_t>(arg), P(sumP), P(partials), prow, c.stream),
+            "edge gather");
+      Stats st = batch_stats(c, partials, prow, count, gamma, beta, bufs[3 * l], bufs[3 * l + 1], bufs[3 * l + 2],
+                             h.momentum[l], h.eps[l]);
+      float* out = P(xcat) + off;
+      void* out16 = static_cast<at::BFloat16*>(xcat16.data_ptr()) + off;
+      if (l + 1 < kBlocks && (co[l] == 64 || co[l] == 128) && N % 32 == 0) {
+        // the apply also writes the next block's kNN |x|^2 and operand image
+        next_prepared = knn_image_buffers(c, B, co[l], N);
+        have_prepared = true;
+        check(dgx_bn_lrelu_apply_knn_image_f32(P(ysel), B, N, co[l], P(st.scale), P(st.shift), (float)h.slope[l], out,
+                                               total, out16, P(next_prepared.first), P(next_prepared.second),
+                                               (size_t)next_prepared.second.numel() * 4, c.stream),
+              "bn apply + knn image");
+      } else {
+        check(dgx_bn_lrelu_apply_f32(P(ysel), (int)M, co[l], P(st.scale), P(st.shift), (float)h.slope[l], out, total,
+                                     out16, c.stream),
+              "bn apply");
+      }
+      saved.insert(saved.end(), {idx, PQ, ysel, arg, sumP, st.scale, st.shift, st.mean, st.invstd});
+      off_in = off;
+      off += co[l];
+    }
+    // conv5 -> BN -> LeakyReLU (dgcnn.py:100-102): bf16 Z with the statistics from the fp32 sums
+    Tensor part5;
+    Tensor Z = lds_xwt(c, xcat16, prep.nt[3], &part5);
+    Stats st5 = batch_stats(c, part5, (int)part5.size(0), (double)M, params[13], params[14], bufs[12], bufs[13],
+                            bufs[14], h.momentum[4], h.eps[4]);
+    Tensor out = c.empty({B, emb, N}, c.f32);
+    check(dgx_pointconv_apply_bf16(Z.data_ptr(), B, N, emb, P(st5.scale), P(st5.shift), (float)h.slope[4], P(out),
+                                   c.stream),
+          "pointconv apply bf16");
+    saved.insert(saved.end(), {Z, st5.scale, st5.shift, st5.mean, st5.invstd, x_pm, xcat16, prep.buf});
+
+    std::vector<Tensor> to_save(params.begin(), params.end());
+    ctx->save_for_backward(to_save);
+    ctx->saved_data["state"] = at::IValue(c10::List<Tensor>(saved));
+    ctx->saved_data["k"] = k;
+    ctx->saved_data["hyper"] = at::IValue(hyper);
+    ctx->saved_data["shape"] = at::IValue(std::vector<int64_t>{B, C0, N});
+    return {out};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto params = ctx->get_saved_variables();
+    auto state_list = ctx->saved_data["state"].toTensorList();
+    std::vector<Tensor> S(state_list.begin(), state_list.end());
+    const int K = (int)ctx->saved_data["k"].toInt();
+    auto hyper = ctx->saved_data["hyper"].toDoubleVector();
+    auto shape = ctx->saved_data["shape"].toIntVector();
+    const int B = (int)shape[0], C0 = (int)shape[1], N = (int)shape[2];
+    const int64_t M = (int64_t)B * N;
+    const size_t n_in = 1 + 15 + 15 + 1 + 1 + 1;   // x, params, bufs, idx0, k, hyper
+    variable_list out_grads(n_in);
+    Tensor dout = grads[0];
+    if (!dout.defined()) return out_grads;
+
+    const Tensor& Z = S[36];
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z.device());
+    Ctx c;
+    c.f32 = Z.options().dtype(at::kFloat);
+    c.bf16 = Z.options().dtype(at::kBFloat16);
+    c.i32 = Z.options().dtype(at::kInt);
+    c.u8 = Z.options().dtype(at::kByte);
+    c.stream = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(Z.device().index()).stream();
+    Stats st5{S[37], S[38], S[39], S[40]};
+    const Tensor &x_pm = S[41], &xcat16 = S[42], &pbuf = S[43];
+    std::array<int, kBlocks> co, cin;
+    int total = 0;
+    for (int l = 0; l < kBlocks; ++l) {
+      co[l] = (int)params[3 * l].size(0);
+      cin[l] = (int)params[3 * l].size(1) / 2;
+      total += co[l];
+    }
+    const int emb = (int)params[12].size(0);
+    // the prep buffer's views (same layout as the forward's prep_weights)
+    std::array<Tensor, 4> nt, tn;
+    {
+      int64_t off = 0;
+      for (int j = 0; j < 4; ++j) {
+        const bool edge = j < 3;
+        const int64_t rows = edge ? co[j + 1] : emb, cols = edge ? cin[j + 1] : total;
+        const int64_t R = edge ? 2 * rows : rows, n_nt = (edge ? 2 : 1) * R * cols, n_tn = R * cols;
+        nt[j] = pbuf.narrow(0, off, n_nt).view({R, edge ? 2 * cols : cols});
+        tn[j] = pbuf.narrow(0, off + cdiv(n_nt, 8) * 8, n_tn).view({cols, R});
+        off += cdiv(n_nt, 8) * 8 + cdiv(n_tn, 8) * 8;
+      }
+    }
+
+    // ---- conv5 + BN + LeakyReLU backward (dgx.pointconv, bf16 Z) ----
+    dout = dout.to(at::kFloat).contiguous();
+    const int rows5 = dgx_pointconv_bf16_rows(B, N);
+    Tensor part5 = c.empty({rows5, 2, emb}, c.f32);
+    Tensor dZ = c.empty({M, emb}, c.bf16);
+    check(dgx_pointconv_bwd_bf16(P(dout), Z.data_ptr(), B, N, emb, P(st5.scale), P(st5.shift), P(st5.mean),
+                                 P(st5.invstd), (float)hyper[14], nullptr, nullptr, P(part5), nullptr, 0, c.stream),
+          "pointconv bwd stats");
+    Tensor dg5 = c.empty({emb}, c.f32), db5 = c.empty({emb}, c.f32), c05 = c.empty({emb}, c.f32),
+           c15 = c.empty({emb}, c.f32);
+    {
+      auto pr = compact(c, part5, rows5, emb);
+      check(dgx_bn_bwd_finalize_f32(P(pr.first), pr.second, emb, (double)M, P(st5.scale), P(st5.mean), P(st5.invstd),
+                                    P(dg5), P(db5), P(c05), P(c15), 0, c.stream),
+            "bn bwd finalize");
+    }
+    check(dgx_pointconv_bwd_bf16(P(dout), Z.data_ptr(), B, N, emb, P(st5.scale), P(st5.shift), nullptr, nullptr,
+                                 (float)hyper[14], P(c05), P(c15), nullptr, dZ.data_ptr(), 1, c.stream),
+          "pointconv bwd dZ");
+    Tensor dW5 = c.empty({emb, total}, c.f32);
+    lds_atb(c, dZ, xcat16, dW5, 0);
+    Tensor dxcat = lds_xwt(c, dZ, tn[3], nullptr);   // (M, total) fp32
+
+    // ---- EdgeConv chain backward (dgx.edgeconv._EdgeConvStack.backward, bf16) ----
+    std::vector<Tensor> rowptr(kBlocks), edges(kBlocks);
+    {
+      const int32_t* ids[kBlocks];
+      int32_t* rp[kBlocks];
+      int32_t* ed[kBlocks];
+      for (int l = 0; l < kBlocks; ++l) {
+        const Tensor& idx = S[9 * l];
+        TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous(), "dgx: kNN ids must be contiguous int32");
+        rowptr[l] = c.empty({M + 1}, c.i32);
+        edges[l] = c.empty({M * K}, c.i32);
+        ids[l] = P<int32_t>(idx);
+        rp[l] = P<int32_t>(rowptr[l]);
+        ed[l] = P<int32_t>(edges[l]);
+      }
+      check(dgx_graph_reverse_multi(kBlocks, ids, B, N, K, rp, ed, c.stream), "reverse graphs");
+    }
+    const double count = (double)M * K;
+    Tensor pre_dz, pre_part;
+    int pre_rows = 0;
+    bool have_pre = false;
+    Tensor dx_in;
+    int off = total;
+    for (int l = kBlocks - 1; l >= 0; --l) {
+      off -= co[l];
+      const int prev = l > 0 ? off - co[l - 1] : 0;
+      const Tensor &idxl = S[9 * l], &PQ = S[9 * l + 1], &ysel = S[9 * l + 2], &arg = S[9 * l + 3],
+                   &sumP = S[9 * l + 4];
+      Stats st{S[9 * l + 5], S[9 * l + 6], S[9 * l + 7], S[9 * l + 8]};
+      (void)idxl;
+      Tensor dz, partials;
+      int nblk;
+      if (have_pre) {   // dz + partials already made by block l+1's dX GEMM epilogue
+        dz = pre_dz;
+        partials = pre_part;
+        nblk = pre_rows;
+        have_pre = false;
+      } else {          // the last block reads its incoming gradient slice of dxcat
+        nblk = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (M + 63) / 64));
+        dz = c.empty({M, co[l]}, c.f32);
+        partials = c.empty({nblk, 2, co[l]}, c.f32);
+        check(dgx_edge_bwd_dz_packed_f32(P(dxcat) + off, (int)dxcat.stride(0), P(ysel), P<uint8_t>(arg), (int)M,
+                                         co[l], P(st.scale), P(st.shift), P(st.mean), P(st.invstd),
+                                         (float)hyper[3 * l + 2], P(dz), P(partials), nblk, c.stream),
+              "edge bwd dz");
+      }
+      Tensor dPQ = c.empty({M, 2 * co[l]}, c.bf16);
+      Tensor dgamma = c.empty({co[l]}, c.f32), dbeta = c.empty({co[l]}, c.f32), c0 = c.empty({co[l]}, c.f32),
+             c1 = c.empty({co[l]}, c.f32);
+      check(dgx_edge_bwd_scatter_fin_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(rowptr[l]), P<int32_t>(edges[l]), P(dz),
+                                         nullptr, P(sumP), B, N, K, co[l], P(partials), nblk, count, P(st.scale),
+                                         P(st.mean), P(st.invstd), 0, P(dgamma), P(dbeta), P(c0), P(c1),
+                                         dPQ.data_ptr(), 1, 1, c.stream),
+            "edge bwd scatter");
+      out_grads[1 + 3 * l + 1] = dgamma;
+      out_grads[1 + 3 * l + 2] = dbeta;
+      // dW = dPQ^T X, un-stacked to the reference layout [W1 | W2]
+      Tensor gw = c.empty({co[l], 2 * cin[l]}, c.f32);
+      if (l > 0) {
+        lds_atb(c, dPQ, xcat16.narrow(1, prev, cin[l]), gw, co[l]);
+        // block l-1's dY = dxcat slice + dPQ [W1;W2], its LeakyReLU' + packed dz + BN partials in the epilogue
+        const Tensor &ysel_p = S[9 * (l - 1) + 2], &arg_p = S[9 * (l - 1) + 3];
+        Stats sp{S[9 * (l - 1) + 5], S[9 * (l - 1) + 6], S[9 * (l - 1) + 7], S[9 * (l - 1) + 8]};
+        const Tensor& w16 = tn[l - 1];   // (cin, 2co)
+        const int rows = dgx_gemm_edge_dz_rows((int)M, cin[l]);
+        pre_dz = c.empty({M, cin[l]}, c.f32);
+        pre_part = c.empty({rows, 2, cin[l]}, c.f32);
+        check(dgx_gemm_edge_dz_bf16(dPQ.data_ptr(), ld_of(dPQ), w16.data_ptr(), ld_of(w16), (int)M, cin[l],
+                                    2 * co[l], P(dxcat) + prev, dxcat.stride(0), P(ysel_p), P<uint8_t>(arg_p),
+                                    P(sp.scale), P(sp.shift), P(sp.mean), P(sp.invstd), (float)hyper[3 * (l - 1) + 2],
+                                    P(pre_dz), P(pre_part), rows, c.stream),
+              "gemm edge dz");
+        pre_rows = rows;
+        have_pre = true;
+      } else {
+        mm_atb(c, dPQ, x_pm, gw, co[0]);
+        if (ctx->needs_input_grad(0)) {
+          // dx = dPQ [W1; W2] (M, C0) -> (B, C0, N)
+          Tensor w = params[0].reshape({co[0], 2 * cin[0]});
+          Tensor wcat = at::cat({w.narrow(1, 0, cin[0]), w.narrow(1, cin[0], cin[0])}, 0).contiguous();
+          Tensor dx = c.empty({M, C0}, c.f32);
+          check(dgx_gemm_bf16(dPQ.data_ptr(), 1, 0, ld_of(dPQ), P(wcat), 0, 1,
+                              wcat.size(0) > 1 ? wcat.stride(0) : std::max<int64_t>(1, wcat.size(1)), (int)M, C0,
+                              2 * co[0], kEpiStore, 1, P(dx), dx.stride(0), nullptr, c.stream),
+                "gemm bf16");
+          dx_in = dx.view({B, N, C0}).permute({0, 2, 1});
+        }
+      }
+      out_grads[1 + 3 * l] = gw.view(params[3 * l].sizes());
+    }
+    out_grads[0] = dx_in;
+    out_grads[1 + 12] = dW5.view(params[12].sizes());
+    out_grads[1 + 13] = dg5;
+    out_grads[1 + 14] = db5;
+    return out_grads;
+  }
+};
+
+Tensor dgcnn_train(const Tensor& x, at::TensorList params, at::TensorList bufs, const std::optional<Tensor>& idx0,
+                   int64_t k, std::vector<double> hyper) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 3, "dgx dgcnn_train: fp32 (B,C,N) device cloud");
+  TORCH_CHECK(params.size() == 15 && bufs.size() == 15 && hyper.size() == 15, "dgx dgcnn_train: 5 conv/BN layers");
+  TORCH_CHECK(k >= 1 && k <= std::min<int64_t>(64, x.size(2)), "dgx dgcnn_train: k out of range");
+  for (const auto& p : params) TORCH_CHECK(p.scalar_type() == at::kFloat && p.is_cuda(), "dgx: fp32 device parameters");
+  if (idx0.has_value() && idx0->defined())
+    TORCH_CHECK(idx0->scalar_type() == at::kInt && idx0->is_contiguous() && idx0->size(0) == x.size(0) &&
+                    idx0->size(1) == x.size(2) && idx0->size(2) == k,
+                "dgx dgcnn_train: idx0 must be contiguous int32 (B, N, k)");
+  return DgcnnTrain::apply(x, params, bufs, idx0, k, std::move(hyper))[0];
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dgx_host, m) {
+  m.def("dgcnn_train(Tensor x, Tensor[] params, Tensor[] bufs, Tensor? idx0, int k, float[] hyper) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(dgx_host, CompositeImplicitAutograd, m) { m.impl("dgcnn_train", dgcnn_train); }

@@ -986,7 +986,6 @@ const char* dgx_knn_kernel_name(int C, int k, int N) {
     };
     static const Names names;  // thread-safe one-time initialisation
     if (C < 1 || C > 128 || k < 1 || k > 64 || N < 1) return "";
-    if (dgx_knn_grid_ok(C, N, k)) return dgx_knn_grid_kernel_name(C, k);
     const int ns = knn_nstep(C);
     const int a = ns == 1 ? 0 : ns == 3 ? 1 : ns == 8 ? 2 : ns == 16 ? 3 : 4;
     const int b = k <= 16 ? 0 : k <= 20 ? 1 : k <= 32 ? 2 : k <= 40 ? 3 : 4;
@@ -1098,7 +1097,6 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C
     if (C > 128 || k > 64 || N > FIX_MAXN) return DGX_EUNSUPPORTED;
     if (workspace_bytes < dgx_knn_workspace_bytes(B, C, N) || !workspace) return DGX_EINVAL;
     if (B == 0) return DGX_OK;
-    if (dgx_knn_grid_ok(C, N, k)) return dgx_knn_grid_f32(x, sB, sC, sN, B, C, N, k, idx64, idx32, nullptr, stream);
     float* xx = static_cast<float*>(workspace);
     float* image = xx + (((size_t)B * N + 3) & ~(size_t)3);  // 16-byte aligned after xx
     const size_t ib = dgx_knn_image_bytes(B, C, N);

@@ -30,9 +30,6 @@ _SIGS = {
     "dgx_knn_workspace_bytes": [_i32, _i32, _i32],
     "dgx_knn_image_bytes": [_i32, _i32, _i32],
     "dgx_knn_kernel_name": [_i32, _i32, _i32],
-    "dgx_knn_grid_ok": [_i32, _i32, _i32],
-    "dgx_knn_grid_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
-    "dgx_knn_grid_kernel_name": [_i32, _i32],
     "dgx_bn_lrelu_apply_knn_image_f32": [_vp, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _sz, _vp],
     "dgx_knn_prepare_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp],
     "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
@@ -123,7 +120,6 @@ _RESTYPES = {
     "dgx_version": ctypes.c_char_p,
     "dgx_strerror": ctypes.c_char_p,
     "dgx_knn_kernel_name": ctypes.c_char_p,
-    "dgx_knn_grid_kernel_name": ctypes.c_char_p,
     "dgx_knn_workspace_bytes": _sz,
     "dgx_knn_image_bytes": _sz,
 }

@@ -300,6 +300,9 @@ def edge_mlp2(x, k, conv1, conv2, training=None, knn_src=None):
     if cpu.is_cpu(x):
         return cpu.edge_mlp2(x, k, conv1, conv2, training, knn_src)
     nat.require_device(x)
+    if torch.compiler.is_compiling():   # traced as one dgx::edge_mlp2 op (dgx.library)
+        from . import library
+        return library.edge_mlp2_call(x, k, conv1, conv2, knn_src)
     if x.dtype != torch.float32:
         x = x.float()
     (cv1, bn1, act1), (cv2, bn2, act2) = (conv1[0], conv1[1], conv1[2]), (conv2[0], conv2[1], conv2[2])

@@ -17,6 +17,9 @@ def hog_1x1(x, idx):
     """x (B, 3, N) fp32 on the device, idx (B, N, k) int64 local kNN ids ->
     (B, N, 18) histograms, as the reference computes them from the same idx.
     Host tensors take the reference's own host path (dgx.cpu.hog_1x1)."""
+    if torch.compiler.is_compiling():   # traced as one dgx::hog_1x1 op (dgx.library)
+        from . import library  # noqa: F401
+        return torch.ops.dgx.hog_1x1(x, idx)
     if cpu.is_cpu(x) and cpu.is_cpu(idx):
         return cpu.hog_1x1(x, idx)
     N.require_device(x, idx)

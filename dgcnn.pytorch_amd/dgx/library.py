@@ -570,3 +570,192 @@ def dgcnn_forward(model, x):
                                                      bf16, prep5)
     _store_bn(list(zip(bns, rms, rvs, nbs)) + [(bn5, rm5, rv5, nb5)])
     return out
+
+
+# ------------------------------------------------- PositionEmbedding edge MLP ----
+# dgx::edge_mlp2: PositionEmbedding's edge stage (reference models/layers.py:
+# 45-52: get_graph_feature -> conv1 -> conv2 -> max over k) as dgx.edgemlp runs
+# it. The forward returns the output and the updated BatchNorm statistics only;
+# the backward op re-runs the forward kernels (no statistics update: the BNs
+# are replayed with their batch / running choice and tracking off) to rebuild
+# the saved state, then runs the engine's backward — the same kernels on the
+# same inputs, so the gradients equal the eager Function path's bit for bit.
+# Eager callers keep the Function path (no recompute); torch.compile / export
+# trace this op (dgx.edgemlp.edge_mlp2 routes here while compiling).
+def _emlp_specs(training, track, rms, rvs, nbts, momentum, eps, outs):
+    return [_BNSpec(t, tr, rm, rv, nb, mo, e, out=o)
+            for t, tr, rm, rv, nb, mo, e, o in zip(training, track, rms, rvs, nbts, momentum, eps, outs)]
+
+
+@torch.library.custom_op("dgx::edge_mlp2", mutates_args=(), device_types="cuda")
+def edge_mlp2(x: Tensor, k: int, w1: Tensor, g1: Tensor, b1: Tensor, rm1: Tensor, rv1: Tensor, nbt1: Tensor,
+              w2: Tensor, g2: Tensor, b2: Tensor, rm2: Tensor, rv2: Tensor, nbt2: Tensor, training: list[bool],
+              track: list[bool], momentum: list[float], eps: list[float], slopes: list[float], bf16: bool,
+              knn_src: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    from . import edgemlp as EM
+    outs = _stat_outputs(training, track, [rm1, rm2], [rv1, rv2], [nbt1, nbt2])
+    s1, s2 = _emlp_specs(training, track, [rm1, rm2], [rv1, rv2], [nbt1, nbt2], momentum, eps, outs)
+    with prec.mode("bf16" if bf16 else "fp32"):
+        out = EM._EdgeMLP2.forward(_Rec(), x, k, s1, s2, slopes[0], slopes[1], False, knn_src, w1, g1, b1, w2, g2,
+                                   b2)
+    (a1, a2, a3), (c1, c2, c3) = outs
+    return out, a1, a2, a3, c1, c2, c3
+
+
+@edge_mlp2.register_fake
+def _(x, k, w1, g1, b1, rm1, rv1, nbt1, w2, g2, b2, rm2, rv2, nbt2, training, track, momentum, eps, slopes, bf16,
+      knn_src):
+    B, _, N = x.shape
+    return (x.new_empty((B, w2.shape[0], N), dtype=_F32), torch.empty_like(rm1), torch.empty_like(rv1),
+            torch.empty_like(nbt1), torch.empty_like(rm2), torch.empty_like(rv2), torch.empty_like(nbt2))
+
+
+@torch.library.custom_op("dgx::edge_mlp2_backward", mutates_args=(), device_types="cuda")
+def edge_mlp2_backward(dout: Tensor, x: Tensor, k: int, w1: Tensor, g1: Tensor, b1: Tensor, rm1: Tensor, rv1: Tensor,
+                       w2: Tensor, g2: Tensor, b2: Tensor, rm2: Tensor, rv2: Tensor, use_batch: list[bool],
+                       eps: list[float], slopes: list[float], bf16: bool, knn_src: Optional[Tensor],
+                       x_needs_grad: bool) -> tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    from . import edgemlp as EM
+    e = _empty(x.device)
+    en = _empty(x.device, torch.int64)
+    specs = [_BNSpec(u, False, rm if not u else e, rv if not u else e, en, 0.1, ep)
+             for u, rm, rv, ep in zip(use_batch, (rm1, rm2), (rv1, rv2), eps)]
+    rec = _Rec()
+    rec.needs_input_grad = (x_needs_grad,) + (True,) * 63
+    with prec.mode("bf16" if bf16 else "fp32"):
+        EM._EdgeMLP2.forward(rec, x, k, specs[0], specs[1], slopes[0], slopes[1], True, knn_src, w1, g1, b1, w2, g2,
+                             b2)
+        res = EM._EdgeMLP2.backward(rec, dout)
+    dx = res[0].contiguous() if res[0] is not None else _empty(x.device)
+    gw1, dg1, db1, gw2, dg2, db2 = res[8:14]
+    return dx, gw1.contiguous(), dg1, db1, gw2.contiguous(), dg2, db2
+
+
+@edge_mlp2_backward.register_fake
+def _(dout, x, k, w1, g1, b1, rm1, rv1, w2, g2, b2, rm2, rv2, use_batch, eps, slopes, bf16, knn_src, x_needs_grad):
+    dx = x.new_empty(x.shape, dtype=_F32) if x_needs_grad else x.new_empty((0,), dtype=_F32)
+    return (dx, torch.empty_like(w1, dtype=_F32), torch.empty_like(g1, dtype=_F32), torch.empty_like(b1, dtype=_F32),
+            torch.empty_like(w2, dtype=_F32), torch.empty_like(g2, dtype=_F32), torch.empty_like(b2, dtype=_F32))
+
+
+def _emlp_setup(ctx, inputs, output):
+    (x, k, w1, g1, b1, rm1, rv1, nbt1, w2, g2, b2, rm2, rv2, nbt2, training, track, momentum, eps, slopes, bf16,
+     knn_src) = inputs
+    ctx.set_materialize_grads(False)
+    ctx.k, ctx.eps, ctx.slopes, ctx.bf16 = k, list(eps), list(slopes), bf16
+    ctx.use_batch = [_use_batch(training[0], rm1), _use_batch(training[1], rm2)]
+    ctx.has_src = knn_src is not None
+    # the recompute reads the running statistics only where they normalised the
+    # forward (no batch statistics: then they are not updated either); a layer
+    # on batch statistics saves nothing of them — its buffers get the op's
+    # updated values copied in after the call (edge_mlp2_call), which would
+    # invalidate a saved reference
+    e = x.new_empty((0,), dtype=_F32)
+    rms = [rm if not ub else e for rm, ub in zip((rm1, rm2), ctx.use_batch)]
+    rvs = [rv if not ub else e for rv, ub in zip((rv1, rv2), ctx.use_batch)]
+    ctx.save_for_backward(x, w1, g1, b1, rms[0], rvs[0], w2, g2, b2, rms[1], rvs[1],
+                          *([knn_src] if ctx.has_src else []))
+
+
+def _emlp_bwd(ctx, gout, *_stats):
+    t = ctx.saved_tensors
+    x, w1, g1, b1, rm1, rv1, w2, g2, b2, rm2, rv2 = t[:11]
+    knn_src = t[11] if ctx.has_src else None
+    if gout is None:
+        gout = torch.zeros((x.shape[0], w2.shape[0], x.shape[2]), dtype=_F32, device=x.device)
+    dx, gw1, dg1, db1, gw2, dg2, db2 = torch.ops.dgx.edge_mlp2_backward(
+        gout, x, ctx.k, w1, g1, b1, rm1, rv1, w2, g2, b2, rm2, rv2, ctx.use_batch, ctx.eps, ctx.slopes, ctx.bf16,
+        knn_src, ctx.needs_input_grad[0])
+    return ((dx if ctx.needs_input_grad[0] else None), None, gw1, dg1, db1, None, None, None, gw2, dg2, db2, None,
+            None, None, None, None, None, None, None, None, None)
+
+
+torch.library.register_autograd("dgx::edge_mlp2", _emlp_bwd, setup_context=_emlp_setup)
+
+
+def edge_mlp2_call(x, k, conv1, conv2, knn_src=None):
+    """models.layers.PositionEmbedding's edge stage through dgx::edge_mlp2 (the
+    module BatchNorms' buffers updated from the op's outputs)."""
+    (cv1, bn1, act1), (cv2, bn2, act2) = (conv1[0], conv1[1], conv1[2]), (conv2[0], conv2[1], conv2[2])
+    dev = x.device
+    a1, a2 = _bn_args(bn1, dev), _bn_args(bn2, dev)
+    out, rm1, rv1, nb1, rm2, rv2, nb2 = torch.ops.dgx.edge_mlp2(
+        x.float(), k, cv1.weight, bn1.weight, bn1.bias, a1[0], a1[1], a1[2], cv2.weight, bn2.weight, bn2.bias, a2[0],
+        a2[1], a2[2], [a1[3], a2[3]], [a1[4], a2[4]], [a1[5], a2[5]], [a1[6], a2[6]],
+        [float(act1.negative_slope), float(act2.negative_slope)], prec.get() == "bf16",
+        None if knn_src is None else knn_src.detach().float())
+    _store_bn([(bn1, rm1, rv1, nb1), (bn2, rm2, rv2, nb2)])
+    return out
+
+
+# -------------------------------------------------------------- attention ----
+# dgx::attention: Net's attention core (reference models/model_partseg.py:
+# 167-171, 187-191 via nn.MultiheadAttention): dropout(softmax(scale q k^T)) v
+# per head on the engine kernels. The dropout seed is an input drawn by the
+# caller on the device (dgx.attention.new_seed), so the op is a pure function
+# of its inputs; the log-sum-exp comes back for the backward op.
+@torch.library.custom_op("dgx::attention", mutates_args=(), device_types="cuda")
+def attention_op(q: Tensor, k: Tensor, v: Tensor, heads: int, p: float, scale: float, dtype_code: int,
+                 seed: Optional[Tensor]) -> tuple[Tensor, Tensor]:
+    from . import attention as A
+    return A.attn_forward(q, k, v, heads, p, scale, A.CODE_DTYPES[dtype_code], seed)
+
+
+@attention_op.register_fake
+def _(q, k, v, heads, p, scale, dtype_code, seed):
+    from . import attention as A
+    B, Nq, E = q.shape
+    return q.new_empty((B, Nq, E), dtype=A.CODE_DTYPES[dtype_code]), q.new_empty((B * heads * Nq,), dtype=_F32)
+
+
+@torch.library.custom_op("dgx::attention_backward", mutates_args=(), device_types="cuda")
+def attention_backward(do: Tensor, q: Tensor, k: Tensor, v: Tensor, o: Tensor, lse: Tensor, heads: int, p: float,
+                       scale: float, seed: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor]:
+    from . import attention as A
+    return A.attn_backward(do, q, k, v, o, lse, heads, p, scale, seed)
+
+
+@attention_backward.register_fake
+def _(do, q, k, v, o, lse, heads, p, scale, seed):
+    return torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+
+
+def _attn_setup(ctx, inputs, output):
+    q, k, v, heads, p, scale, dtype_code, seed = inputs
+    ctx.set_materialize_grads(False)
+    ctx.meta = (heads, p, scale)
+    ctx.save_for_backward(q, k, v, output[0], output[1], *([seed] if seed is not None else []))
+
+
+def _attn_bwd(ctx, do, _glse):
+    heads, p, scale = ctx.meta
+    t = ctx.saved_tensors
+    q, k, v, o, lse = t[:5]
+    seed = t[5] if len(t) > 5 else None
+    if do is None:
+        return None, None, None, None, None, None, None, None
+    dq, dk, dv = torch.ops.dgx.attention_backward(do, q, k, v, o, lse, heads, p, scale, seed)
+    return dq, dk, dv, None, None, None, None, None
+
+
+torch.library.register_autograd("dgx::attention", _attn_bwd, setup_context=_attn_setup)
+
+
+# ---------------------------------------------------------------------- HOG ----
+# dgx::hog_1x1: compute_hog_1x1 after its kNN call (reference
+# models/model_partseg.py:28-92). No gradient (the reference detaches into numpy).
+@torch.library.custom_op("dgx::hog_1x1", mutates_args=(), device_types="cuda")
+def hog_1x1_op(x: Tensor, idx: Tensor) -> Tensor:
+    from . import hog as H
+    return H.hog_1x1(x, idx)
+
+
+@hog_1x1_op.register_kernel("cpu")
+def _(x, idx):
+    return cpu.hog_1x1(x, idx)
+
+
+@hog_1x1_op.register_fake
+def _(x, idx):
+    B, _, N = x.shape
+    return x.new_empty((B, N, 18), dtype=_F32)

@@ -69,25 +69,6 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
     vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
     stream = nat.stream_of(x)
-    if prepared is None and L.dgx_knn_grid_ok(C, N, k):
-        # coordinate clouds: one launch over a cell grid built in LDS (no
-        # prepare pass, no operand image; |x|^2 of <= 3 channels rounds the same
-        # in either torch order)
-        timing = getattr(_tls, "timing", None)
-        with torch.cuda.device(x.device):
-            if timing is not None:
-                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ev0.record()
-            rc = L.dgx_knn_grid_f32(nat.f32(x), sB, sC, sN, B, C, N, k,
-                                    nat.ptr(idx, torch.int64) if out_dtype == torch.int64 else None,
-                                    nat.i32(idx) if out_dtype == torch.int32 else None, nat.f32(vals), stream)
-            if timing is not None:
-                ev1.record()
-                timing.append((ev0, ev1, 2.0 * B * N * N * C, (B, C, N, k)))
-        nat.check(rc, "knn (grid)")
-        if key is not None:
-            cache[key] = (idx, x)
-        return (idx, vals) if return_values else idx
     img_bytes = L.dgx_knn_image_bytes(B, C, N)
     if prepared is not None:
         xx, img = prepared
@@ -148,6 +129,9 @@ def set_knn_timing(lst):
 def knn(x, k):
     """Drop-in for reference ``knn(x, k)`` (models/dgcnn.py:6-12): int64 (B,N,k)
     local indices, nearest first; ties in canonical (index ascending) order."""
+    if torch.compiler.is_compiling():   # traced as one dgx::knn op (dgx.library)
+        from . import library  # noqa: F401
+        return torch.ops.dgx.knn(x, k)
     if cpu.is_cpu(x):   # host tensors: the CPU path (dgx.cpu), same canonical result
         return cpu.knn(x, k)
     x = _as_f32(x.detach())
@@ -195,6 +179,10 @@ def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
     Default: (B,2C,N,k) fp32 contiguous, channels [0,C) = x_j, [C,2C) = x_i
     (dgcnn.py:42). knn_only: (B,N,k,C) neighbour rows (dgcnn.py:37-38).
     disp_only: (B,C,N,k) x_j - x_i (dgcnn.py:39-40). Differentiable w.r.t. x."""
+    mode = nat.GF_KNN_ONLY if knn_only else (nat.GF_DISP if disp_only else nat.GF_CAT)
+    if torch.compiler.is_compiling() and idx is None:   # traced as one dgx::graph_feature op
+        from . import library  # noqa: F401
+        return torch.ops.dgx.graph_feature(x, k, mode)[0]
     if cpu.is_cpu(x):
         return cpu.graph_feature(x, k, knn_only, disp_only, idx)
     nat.require_device(x)
@@ -203,5 +191,4 @@ def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
         idx = knn_raw(x.detach(), k, out_dtype=torch.int32)
     elif idx.dtype != torch.int32:
         idx = idx.to(torch.int32)
-    mode = nat.GF_KNN_ONLY if knn_only else (nat.GF_DISP if disp_only else nat.GF_CAT)
     return _GraphFeature.apply(x, idx.contiguous(), mode)

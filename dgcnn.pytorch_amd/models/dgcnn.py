@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from dgx import gemm as _gemm
+from dgx import host as _host
 from dgx import library as _library
 from dgx import ops as _ops
 from dgx import precision as _prec
@@ -90,6 +91,9 @@ class DGCNN(nn.Module):
             # CPU path of every block (dgx.cpu), same modules and state
             feats, _ = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training)
             return pointconv_bn_lrelu(feats, x.shape[0], x.shape[2], self.conv5, self.training)
+        if _host.applies(self, x):
+            # train step of the reference's scripts: one C++ op + C++ autograd node (libdgx_torch.so)
+            return _host.dgcnn_train(self, x)
         if _library.enabled_for(self):
             # the same kernels behind torch.ops.dgx custom ops (torch.compile / export see one node each)
             return _library.dgcnn_forward(self, x)

@@ -25,6 +25,7 @@ downstream numbers depend on them:
   * the histogram's device follows ``use_cpu`` / ``LOCAL_RANK`` as the
     reference's does (model_partseg.py:66-73); the work runs on x's device.
 """
+import contextlib
 import os
 
 import torch
@@ -106,8 +107,10 @@ class Net(nn.Module):
         self.head = MLPHead(args)
 
     def forward(self, src, lbl):
-        # the input cloud's kNN is computed once for its three call sites (dgx.ops.knn_cache)
-        with knn_cache():
+        # the input cloud's kNN is computed once for its three call sites
+        # (dgx.ops.knn_cache); a torch.compile trace runs the three dgx::knn
+        # calls (pure functions of the same input: identical results)
+        with (contextlib.nullcontext() if torch.compiler.is_compiling() else knn_cache()):
             src_emb = self.emb_nn(src)                                 # (B,emb,N), 4 engine kNN
             tgt_emb = self.grads_emb(compute_hog_1x1(src, k=self.k).transpose(1, 2).contiguous())
             canonical = self.pos_mlp(src)                              # the same layer-1 kNN

@@ -57,22 +57,6 @@ int dgx_knn_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                 int64_t* idx64, int32_t* idx32,
                 void* workspace, size_t workspace_bytes, void* stream);
 
-/* Coordinate clouds (C <= 3, N <= 4096, k <= 64; the xyz kNN of
- * models/dgcnn.py:84 block 1, models/layers.py:45 and
- * models/model_partseg.py:26): the same output as dgx_knn_f32 in ONE launch
- * that needs no workspace — every workgroup sorts its cloud into a cell grid in
- * LDS and each query visits only the cells around it; a query whose k-th value
- * the visited cells cannot certify is recomputed over the whole cloud, so the
- * result never depends on the grid. |x|^2 of C <= 3 channels has the same
- * rounding in both of torch's orders, so there is no `order` argument.
- * vals (nullable) as dgx_knn_select_f32's. dgx_knn_grid_ok says whether
- * (C, N, k) is supported (else DGX_EUNSUPPORTED); dgx_knn_f32 takes this path
- * itself when it is. */
-int dgx_knn_grid_ok(int C, int N, int k);
-int dgx_knn_grid_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N, int k,
-                     int64_t* idx64, int32_t* idx32, float* vals, void* stream);
-const char* dgx_knn_grid_kernel_name(int C, int k);
-
 /* The stages of dgx_knn_f32, separately. dgx_sqnorm_f32: |x_i|^2 in the
  * reference's rounding order into xx (B*N fp32, dgcnn.py:8).
  * dgx_knn_prepare_f32: the same xx plus the MFMA operand image of x in
@@ -81,10 +65,9 @@ const char* dgx_knn_grid_kernel_name(int C, int k);
  * prepared image and its xx; vals (B,N,k), nullable, receives the selected pd
  * values (what pd.topk(k)[0] would hold). */
 size_t dgx_knn_image_bytes(int B, int C, int N);
-/* Name of the selection kernel a kNN call launches for (C, k, N), as rocprofv3
- * prints it (host-side query; lets profiles be matched to the kernels that
- * actually ran): dgx_knn_grid_f32's where dgx_knn_grid_ok, else
- * dgx_knn_select_f32's. "" for unsupported (C, k, N). */
+/* Name of the selection kernel dgx_knn_select_f32 launches for (C, k, N), as
+ * rocprofv3 prints it (host-side query; lets profiles be matched to the
+ * kernels that actually ran). "" for unsupported (C, k, N). */
 const char* dgx_knn_kernel_name(int C, int k, int N);
 /* dgx_bn_lrelu_apply_f32 for an EdgeConv block whose output feeds the next
  * block's kNN (dgcnn.py:84-98, the feature-space knn of x_l): writes

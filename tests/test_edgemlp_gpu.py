@@ -219,11 +219,11 @@ def test_edge_mlp_bf16_kernels_equal_fp32_kernels(cuda):
     assert rel_err(d32.view(M, k, C2).cpu(), ref.cpu()) < 1e-6
 
 
-def test_edge_mlp_rejects_cpu_and_bad_shapes(cuda):
+def test_edge_mlp_mixed_devices_and_bad_shapes(cuda):
     from dgx.edgemlp import edge_mlp2
     conv1, conv2 = _convs(1)
-    with pytest.raises(RuntimeError):
-        edge_mlp2(torch.zeros(1, 3, 64), 8, conv1, conv2, True)  # CPU tensor: no fallback
     conv1, conv2 = conv1.to(cuda), conv2.to(cuda)
+    with pytest.raises(RuntimeError):
+        edge_mlp2(torch.rand(1, 3, 64), 8, conv1, conv2, True)  # host cloud, device weights
     with pytest.raises(RuntimeError):
         edge_mlp2(torch.zeros(1, 4, 64, device=cuda), 8, conv1, conv2, True)  # conv1 expects 2*3 channels

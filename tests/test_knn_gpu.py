@@ -99,8 +99,11 @@ def test_knn_errors(cuda):
     x = torch.zeros(1, 3, 8, device=cuda)
     with pytest.raises(RuntimeError):
         knn(x, 9)
-    with pytest.raises(RuntimeError):
-        knn(torch.zeros(1, 3, 8), 2)  # CPU tensors are not silently served
+    # a host tensor takes the CPU path (dgx.cpu) and gives the device's answer
+    pts = synth.cube_clouds(2, 300, 9)
+    host = knn(torch.from_numpy(pts).permute(0, 2, 1), 12)
+    dev = knn(torch.from_numpy(pts).to(cuda).permute(0, 2, 1), 12)
+    assert host.device.type == "cpu" and torch.equal(host, dev.cpu())
 
 
 def _lane_clustered(N, C, seed):

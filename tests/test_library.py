@@ -40,15 +40,22 @@ def test_version_and_errors():
     assert L.dgx_knn_image_bytes(2, 3, 1000) == 2 * (63 * 64 * 1 + 63 * 16) * 4
 
 
-def test_cpu_tensors_rejected():
+def test_host_tensors_take_the_cpu_path_without_libdgx(monkeypatch):
+    """Host tensors are served by dgx.cpu and never reach the
+    HIP library: with libdgx.so made unloadable the drop-in still runs on the
+    CPU, while the device-only entry points keep rejecting host tensors."""
+    from dgx import _native as nat
     from models.dgcnn import DGCNN, knn, get_graph_feature
+
+    def no_lib():
+        raise ImportError("libdgx.so unavailable (test)")
+    monkeypatch.setattr(nat, "lib", no_lib)
     x = torch.rand(2, 3, 32)
+    assert knn(x, 4).shape == (2, 32, 4)
+    assert get_graph_feature(x, k=4).shape == (2, 6, 32, 4)
+    assert DGCNN(types.SimpleNamespace(emb_dim=64, k=4))(x).shape == (2, 64, 32)
     with pytest.raises(RuntimeError, match="ROCm device"):
-        knn(x, 4)
-    with pytest.raises(RuntimeError, match="ROCm device"):
-        get_graph_feature(x, k=4)
-    with pytest.raises(RuntimeError, match="ROCm device"):
-        DGCNN(types.SimpleNamespace(emb_dim=64, k=4))(x)
+        nat.require_device(x)
 
 
 def test_state_dict_keys_match_reference():
@@ -60,3 +67,14 @@ def test_state_dict_keys_match_reference():
         keys = json.load(f)["state_dict_keys"]
     assert list(DGCNN(types.SimpleNamespace(emb_dim=1024, k=20)).state_dict().keys()) == keys["DGCNN"]
     assert list(PositionEmbedding(types.SimpleNamespace(k=20)).state_dict().keys()) == keys["PositionEmbedding"]
+
+
+def test_host_op_library_loads():
+    """libdgx_torch.so (the C++ op + autograd layer over libdgx.so) loads and
+    registers torch.ops.dgx_host.dgcnn_train; host tensors never take it."""
+    from dgx import host
+    from models.dgcnn import DGCNN
+    host.load()
+    schema = str(torch.ops.dgx_host.dgcnn_train.default._schema)
+    assert schema.startswith("dgx_host::dgcnn_train(Tensor x, Tensor[] params, Tensor[] bufs, Tensor? idx0")
+    assert not host.applies(DGCNN(types.SimpleNamespace(emb_dim=64, k=4)).train(), torch.rand(2, 3, 32))

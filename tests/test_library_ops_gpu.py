@@ -73,7 +73,8 @@ def test_knn_and_graph_feature_ops(cuda):
 def test_dgcnn_op_path_equals_function_path(cuda, monkeypatch, precision):
     """DGCNN through torch.ops.dgx == through the autograd Functions: train
     step (output, every gradient, every BN buffer) and eval forward."""
-    from dgx import library, precision as prec
+    from dgx import host, library, precision as prec
+    monkeypatch.setattr(host, "ENABLED", False)   # the C++ train op is checked in test_host_ext_gpu
     base = _model()
     x = _cloud(cuda)
     gout = torch.randn((4, 128, 512), device=cuda)
@@ -153,3 +154,116 @@ def test_bn_cumulative_average_op_path(cuda, monkeypatch):
         b = _step(mb, x, gout)
         _assert_same(a, b)
     assert int(ma.conv1[1].num_batches_tracked) == 3
+
+
+def _net_step(m, x, lbl, gout, call=None):
+    m.zero_grad(set_to_none=True)
+    y = (call if call is not None else m)(x, lbl)
+    y.backward(gout)
+    return (y.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
+            {n: b.clone() for n, b in m.named_buffers()})
+
+
+@pytest.mark.parametrize("backend", ["eager", "aot_eager"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_torch_compile_net_fullgraph(cuda, precision, backend):
+    """torch.compile(Net, fullgraph=True) — the partseg model main_partseg_dist.py
+    trains (reference models/model_partseg.py:142-194): the engine stages are
+    dgx::knn / dgx::edgeconv_chain / dgx::pointconv / dgx::edge_mlp2 /
+    dgx::hog_1x1 / dgx::attention ops, so the trace has no graph break and
+    every one of them is a node of the captured graph. Dynamo's capture run
+    as-is ("eager" backend) equals two eager train steps bit for bit (outputs,
+    every buffer, every engine-stage gradient; the stock layers' gradients to
+    1e-5, see assert_net_grads_same). Through AOTAutograd ("aot_eager") the
+    stock layers are decomposed (nn.Transformer's linear / LayerNorm pieces run
+    as other ATen kernels, whose fp32 rounding differs from the fused eager
+    modules'; measured 1.3e-4 normwise at the output), so that run is held to
+    the parity bars instead: 1e-3 on the output and buffers, 2e-2 on gradients.
+    Dropout 0 (the seeds would differ)."""
+    from conftest import load_golden, rel_err
+    from dgx import precision as prec
+    from test_host_ext_gpu import assert_net_grads_same
+    from test_partseg import _net
+    g = load_golden("partseg_small.npz")
+    base = _net(g)
+    x = torch.from_numpy(g["x"]).to(cuda)
+    lbl = torch.from_numpy(g["lbl"]).to(cuda)
+    gout = torch.from_numpy(g["gout"]).to(cuda)
+    targets = set()
+
+    def capture(gm, example_inputs):
+        targets.update(str(n.target) for n in gm.graph.nodes if n.op == "call_function")
+        if backend == "eager":
+            return gm.forward
+        return torch._dynamo.backends.debugging.aot_eager(gm, example_inputs)
+    prec.set(precision)
+    try:
+        me = copy.deepcopy(base).to(cuda).train()
+        mc = copy.deepcopy(base).to(cuda).train()
+        # a throwaway step: MIOpen picks the stock convs' algorithms on first call
+        _net_step(copy.deepcopy(base).to(cuda).train(), x, lbl, gout)
+        compiled = torch.compile(mc, backend=capture, fullgraph=True)
+        for _ in range(2):
+            e = _net_step(me, x, lbl, gout)
+            c = _net_step(mc, x, lbl, gout, call=compiled)
+            if backend == "eager":
+                assert torch.equal(e[0], c[0])
+                assert_net_grads_same(e[1], c[1])
+                for n in e[2]:
+                    assert torch.equal(e[2][n], c[2][n]), n
+            else:
+                assert rel_err(e[0].cpu(), c[0].cpu()) < 1e-3
+                assert e[1].keys() == c[1].keys()
+                for n in e[1]:
+                    assert rel_err(e[1][n].cpu(), c[1][n].cpu()) < 2e-2, n
+                for n in e[2]:
+                    if e[2][n].is_floating_point():
+                        assert rel_err(e[2][n].cpu(), c[2][n].cpu()) < 1e-3, n
+                    else:
+                        assert torch.equal(e[2][n], c[2][n]), n
+        for op in ("dgx.knn", "dgx.edgeconv_chain", "dgx.pointconv", "dgx.edge_mlp2", "dgx.hog_1x1",
+                   "dgx.attention"):
+            assert any(op in t for t in targets), (op, sorted(targets))
+    finally:
+        prec.set("fp32")
+        torch._dynamo.reset()
+
+
+def test_net_stage_ops_match_function_path(cuda):
+    """dgx::edge_mlp2 (forward + its recomputing backward op), dgx::attention
+    and dgx::hog_1x1 called directly equal the eager engine paths bit for bit."""
+    from dgx import synth
+    from dgx.attention import _Attention
+    from dgx.edgemlp import edge_mlp2
+    from dgx.hog import hog_1x1
+    from dgx.library import edge_mlp2_call
+    from models.dgcnn import knn
+    torch.manual_seed(3)
+    mk = lambda: (torch.nn.Sequential(torch.nn.Conv2d(6, 64, 1, bias=False), torch.nn.BatchNorm2d(64),  # noqa: E731
+                                      torch.nn.LeakyReLU(0.2)),
+                  torch.nn.Sequential(torch.nn.Conv2d(64, 128, 1, bias=False), torch.nn.BatchNorm2d(128),
+                                      torch.nn.LeakyReLU(0.2)))
+    c1, c2 = mk()
+    d1, d2 = copy.deepcopy(c1).to(cuda), copy.deepcopy(c2).to(cuda)
+    c1, c2 = c1.to(cuda), c2.to(cuda)
+    pts = torch.from_numpy(synth.cube_clouds(2, 512, 8)).to(cuda).permute(0, 2, 1).contiguous()
+    xa, xb = pts.clone().requires_grad_(True), pts.clone().requires_grad_(True)
+    ya, yb = edge_mlp2(xa, 16, c1, c2), edge_mlp2_call(xb, 16, d1, d2)
+    assert torch.equal(ya, yb)
+    go = torch.randn_like(ya)
+    ya.backward(go)
+    yb.backward(go)
+    assert torch.equal(xa.grad, xb.grad)
+    for pa, pb in zip(list(c1.parameters()) + list(c2.parameters()), list(d1.parameters()) + list(d2.parameters())):
+        assert torch.equal(pa.grad, pb.grad)
+    for ba, bb in zip(list(c1.buffers()) + list(c2.buffers()), list(d1.buffers()) + list(d2.buffers())):
+        assert torch.equal(ba, bb)
+    q, k, v = (torch.randn(2, 256, 128, device=cuda, dtype=torch.float16, requires_grad=True) for _ in range(3))
+    oa = _Attention.apply(q, k, v, 2, 0.0, 0.125)
+    ob, _ = torch.ops.dgx.attention(q, k, v, 2, 0.0, 0.125, 0, None)
+    assert torch.equal(oa, ob)
+    ga = torch.autograd.grad(oa, (q, k, v), torch.ones_like(oa))
+    gb = torch.autograd.grad(ob, (q, k, v), torch.ones_like(ob))
+    assert all(torch.equal(a, b) for a, b in zip(ga, gb))
+    idx = knn(pts, 20)
+    assert torch.equal(torch.ops.dgx.hog_1x1(pts, idx), hog_1x1(pts, idx))

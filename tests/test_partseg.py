@@ -129,9 +129,13 @@ def test_hog_use_cpu_places_output(cuda, monkeypatch):
     from models.model_partseg import compute_hog_1x1
     monkeypatch.delenv("LOCAL_RANK", raising=False)
     x = torch.rand((2, 3, 128), device=cuda)
-    assert compute_hog_1x1(x, 8, use_cpu=True).device.type == "cpu"
-    with pytest.raises(RuntimeError):
-        compute_hog_1x1(x.cpu(), 8)
+    h = compute_hog_1x1(x, 8, use_cpu=True)
+    assert h.device.type == "cpu"
+    # a host cloud without use_cpu: the histogram lands on the GPU, as the
+    # reference's does (model_partseg.py:66-73), computed on the host path
+    hc = compute_hog_1x1(x.cpu(), 8)
+    assert hc.device.type == "cuda"
+    torch.testing.assert_close(hc.cpu(), h, rtol=0, atol=1e-5)
 
 
 @pytest.mark.gpu
