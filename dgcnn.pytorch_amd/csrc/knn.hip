@@ -43,6 +43,12 @@ constexpr int KQ_THREADS = 64 * KQ_WAVES;
 constexpr int KQ_QPW = 16;                      // queries per wave
 constexpr int KQ_QPB = KQ_GROUPS * KQ_QPW;      // queries per block
 constexpr int KQ_QCAP = 16;                     // per-lane pending-candidate FIFO
+// register-ring depth (operand units in flight) of the selection kernel: four
+// at NSTEP = 16 while the lists leave the registers for it (k <= 20: 128 VGPRs,
+// 4 waves per SIMD; from k = 32 on the two extra slots would spill)
+#ifndef KNN_RING
+#define KNN_RING(ns, kb) (((ns) == 16 && (kb) <= 20) ? 4 : 2)
+#endif
 constexpr int KQ_LISTS = 4 * KQ_HALVES;         // top-k lists (lanes) per query
 static_assert(KQ_HALVES == 2, "the threshold exchange and the final merge pair two halves");
 
@@ -649,18 +655,24 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         S.cnt += pass ? 1 : 0;
     };
 
-    // Operand stream: units of SW MFMA k-steps (a whole tile when NSTEP <= 16,
-    // a quarter tile at NSTEP = 32) through a two-slot register ring; the load
-    // of unit u+2 is issued as soon as unit u's MFMAs have read their slot, so
-    // a unit's L2 latency hides behind two units of MFMA + selection work.
+    // Operand stream: units of SW MFMA k-steps (half a tile at NSTEP = 16, a
+    // quarter tile at NSTEP = 32, a whole tile below) through a RING-slot
+    // register ring; the load of unit u+RING is issued as soon as unit u's
+    // MFMAs have read their slot, so a unit's L2 latency hides behind RING-1
+    // units of MFMA + selection work. (With two slots at NSTEP = 16 the wave
+    // waited for its next tile right after issuing it: SQ_WAIT_INST_ANY was
+    // 52 % of the wave cycles, r04j_pmc_cfg2.json.)
     constexpr int SW = NSTEP <= 8 ? NSTEP : 8;
     constexpr int SPT = NSTEP / SW;          // units per tile
-    constexpr int UB = SPT < 2 ? 2 : SPT;    // units per loop trip (static ring slots)
-    static_assert(NSTEP % SW == 0 && UB % SPT == 0, "unit split");
+    constexpr int RING = KNN_RING(NSTEP, KB);
+    constexpr int UB = RING > SPT ? RING : SPT;   // units per loop trip (static ring slots)
+    static_assert(NSTEP % SW == 0 && UB % SPT == 0 && UB % RING == 0, "unit split");
     const int ntl = (ntile - h + KQ_HALVES - 1) / KQ_HALVES;  // this half's tiles: h + 2*tl
     const int nunits = ntl * SPT;
-    float a[2][SW];
-    float4 xq[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    float a[RING][SW];
+    float4 xq[RING];
+#pragma unroll
+    for (int r = 0; r < RING; ++r) xq[r] = make_float4(0.f, 0.f, 0.f, 0.f);
     // Every load is unconditional (a unit past the end re-reads this half's
     // last tile, unused): with a data-dependent skip the compiler cannot count
     // the loads in flight and drains them all (vmcnt(0)) every trip. sl = u %
@@ -670,15 +682,15 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         ld_vec<SW>(ib + ((int64_t)s * 64 + lane) * NSTEP + sl * SW, a[slot]);
         if (sl == 0) xq[slot] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
     };
-    load(0, 0, 0);
-    load(1, 1, 1 % SPT);
+#pragma unroll
+    for (int r = 0; r < RING; ++r) load(r, r, r % SPT);
     float4 xc = xq[0];
 #pragma unroll 1
     for (int u = 0; u < nunits; u += UB) {
 #pragma unroll
         for (int ub = 0; ub < UB; ++ub) {
-            const int slot = ub & 1, sl = ub % SPT;
-            const bool live = SPT > 1 || u + ub < nunits;   // wave-uniform
+            const int slot = ub % RING, sl = ub % SPT;
+            const bool live = UB == SPT || u + ub < nunits;   // wave-uniform
             if (live) {
                 if (sl == 0) {
                     each([&](Grp& S, int) { S.acc = f32x4{0.f, 0.f, 0.f, 0.f}; });
@@ -691,7 +703,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                         S.acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][t], S.bq[sl * SW + t], S.acc, 0, 0, 0);
                     });
             }
-            load(slot, u + ub + 2, (ub + 2) % SPT);
+            load(slot, u + ub + RING, (ub + RING) % SPT);
             if (live && sl == SPT - 1) {
                 // lane holds rows 4g..4g+3 = candidates g, g+4, g+8, g+12 of the tile
                 const int j0 = (h + KQ_HALVES * ((u + ub) / SPT)) * 16 + g;
