@@ -131,8 +131,40 @@ Tensor lds_xwt(const Ctx& c, const Tensor& x16, const Tensor& w16, Tensor* part_
   return out;
 }
 
+// Weight-gradient slab sums of one backward, deferred to a single launch at its
+// end (dgx_slab_reduce_multi_f32: each element summed in dgx_slab_reduce_f32's
+// order, so the gradients are those of the per-GEMM reduces)
+struct SlabJobs {
+  std::vector<Tensor> slab, out;
+  std::vector<int> S, rows, cols, split;
+  std::vector<int64_t> ldo;
+  void add(const Tensor& sl, int s, int r, int cl, int sp, const Tensor& o) {
+    slab.push_back(sl);
+    out.push_back(o);
+    S.push_back(s);
+    rows.push_back(r);
+    cols.push_back(cl);
+    split.push_back(sp);
+    ldo.push_back(o.stride(0));
+  }
+  void flush(void* stream) {
+    const int n = (int)slab.size();
+    if (n == 0) return;
+    std::vector<const float*> sp(n);
+    std::vector<float*> op(n);
+    for (int j = 0; j < n; ++j) {
+      sp[j] = static_cast<const float*>(slab[j].data_ptr());
+      op[j] = static_cast<float*>(out[j].data_ptr());
+    }
+    check(dgx_slab_reduce_multi_f32(n, sp.data(), S.data(), rows.data(), cols.data(), split.data(), op.data(),
+                                    ldo.data(), stream),
+          "slab reduce (multi)");
+  }
+};
+
 // dgx.gemm.lds_atb: out = a16^T b16 (split-K slabs, fixed-order sum); split_rows un-stacks [W1;W2]
-void lds_atb(const Ctx& c, const Tensor& a16, const Tensor& b16, Tensor& out, int split_rows) {
+void lds_atb(const Ctx& c, const Tensor& a16, const Tensor& b16, Tensor& out, int split_rows,
+             SlabJobs* defer = nullptr) {
   const int R = (int)a16.size(0), M = (int)a16.size(1), N = (int)b16.size(1);
   int S = dgx_gemm_splits(M, N, R);
   const int64_t bytes = (int64_t)M * N * 4;
@@ -144,13 +176,17 @@ void lds_atb(const Ctx& c, const Tensor& a16, const Tensor& b16, Tensor& out, in
   check(dgx_gemm_lds_bf16(a16.data_ptr(), ld_of(a16), b16.data_ptr(), ld_of(b16), 1, M, N, R, R, kEpiSlab, S,
                           P(slab), N, nullptr, nullptr, 0, c.stream),
         "gemm lds tn");
+  if (defer) {
+    defer->add(slab, used, M, N, split_rows > 0 ? split_rows : M, out);
+    return;
+  }
   check(dgx_slab_reduce_f32(P(slab), used, M, N, split_rows > 0 ? split_rows : M, P(out), out.stride(0), c.stream),
         "slab reduce");
 }
 
 // dgx.gemm.mm_atb with a bf16 (R, M) and an fp32 (R, N) operand (block 1's
 // weight gradient: dPQ^T x, K = 3 raw coordinates)
-void mm_atb(const Ctx& c, const Tensor& a, const Tensor& b, Tensor& out, int split_rows) {
+void mm_atb(const Ctx& c, const Tensor& a, const Tensor& b, Tensor& out, int split_rows, SlabJobs* defer = nullptr) {
   const int R = (int)a.size(0), M = (int)a.size(1), N = (int)b.size(1);
   const int S = dgx_gemm_splits(M, N, R);
   Tensor slab = c.empty({S, M, N}, c.f32);
@@ -161,6 +197,10 @@ void mm_atb(const Ctx& c, const Tensor& a, const Tensor& b, Tensor& out, int spl
   int64_t chunk = cdiv(R, S);
   chunk = cdiv(chunk, 32) * 32;
   const int used = (int)cdiv(R, chunk);
+  if (defer) {
+    defer->add(slab, used, M, N, split_rows > 0 ? split_rows : M, out);
+    return;
+  }
   check(dgx_slab_reduce_f32(P(slab), used, M, N, split_rows > 0 ? split_rows : M, P(out), out.stride(0), c.stream),
         "slab reduce");
 }
@@ -396,8 +436,9 @@ class DgcnnTrain : public torch::autograd::Function<DgcnnTrain> {
     check(dgx_pointconv_bwd_bf16(P(dout), Z.data_ptr(), B, N, emb, P(st5.scale), P(st5.shift), nullptr, nullptr,
                                  (float)hyper[14], P(c05), P(c15), nullptr, dZ.data_ptr(), 1, c.stream),
           "pointconv bwd dZ");
+    SlabJobs slabs;   // every weight gradient's slab sum, one launch at the end
     Tensor dW5 = c.empty({emb, total}, c.f32);
-    lds_atb(c, dZ, xcat16, dW5, 0);
+    lds_atb(c, dZ, xcat16, dW5, 0, &slabs);
     Tensor dxcat = lds_xwt(c, dZ, tn[3], nullptr);   // (M, total) fp32
 
     // ---- EdgeConv chain backward (dgx.edgeconv._EdgeConvStack.backward, bf16) ----
@@ -459,7 +500,7 @@ class DgcnnTrain : public torch::autograd::Function<DgcnnTrain> {
       // dW = dPQ^T X, un-stacked to the reference layout [W1 | W2]
       Tensor gw = c.empty({co[l], 2 * cin[l]}, c.f32);
       if (l > 0) {
-        lds_atb(c, dPQ, xcat16.narrow(1, prev, cin[l]), gw, co[l]);
+        lds_atb(c, dPQ, xcat16.narrow(1, prev, cin[l]), gw, co[l], &slabs);
         // block l-1's dY = dxcat slice + dPQ [W1;W2], its LeakyReLU' + packed dz + BN partials in the epilogue
         const Tensor &ysel_p = S[9 * (l - 1) + 2], &arg_p = S[9 * (l - 1) + 3];
         Stats sp{S[9 * (l - 1) + 5], S[9 * (l - 1) + 6], S[9 * (l - 1) + 7], S[9 * (l - 1) + 8]};
@@ -475,7 +516,7 @@ class DgcnnTrain : public torch::autograd::Function<DgcnnTrain> {
         pre_rows = rows;
         have_pre = true;
       } else {
-        mm_atb(c, dPQ, x_pm, gw, co[0]);
+        mm_atb(c, dPQ, x_pm, gw, co[0], &slabs);
         if (ctx->needs_input_grad(0)) {
           // dx = dPQ [W1; W2] (M, C0) -> (B, C0, N)
           Tensor w = params[0].reshape({co[0], 2 * cin[0]});
@@ -490,6 +531,7 @@ class DgcnnTrain : public torch::autograd::Function<DgcnnTrain> {
       }
       out_grads[1 + 3 * l] = gw.view(params[3 * l].sizes());
     }
+    slabs.flush(c.stream);
     out_grads[0] = dx_in;
     out_grads[1 + 12] = dW5.view(params[12].sizes());
     out_grads[1 + 13] = dg5;

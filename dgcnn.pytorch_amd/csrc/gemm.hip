@@ -310,6 +310,50 @@ __global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_kernel(const float* _
     }
 }
 
+// slab_reduce_kernel for up to SRM_MAXJ independent reductions in one launch
+// (the weight gradients of a backward pass, reduced together at its end): job j
+// owns blocks [first[j], first[j+1]); every output element is summed exactly as
+// slab_reduce_kernel sums it (same groups, same order), so results are identical.
+constexpr int SRM_MAXJ = 8;
+struct SlabJobs {
+    const float* slab[SRM_MAXJ];
+    float* out[SRM_MAXJ];
+    int64_t ldo[SRM_MAXJ];
+    int S[SRM_MAXJ], rows[SRM_MAXJ], cols[SRM_MAXJ], split[SRM_MAXJ], first[SRM_MAXJ + 1];
+    int n;
+};
+__global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi_kernel(SlabJobs jobs) {
+    __shared__ float red[SR_G][SR_E];
+    int j = 0;
+    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+    const float* __restrict__ slab = jobs.slab[j];
+    const int S = jobs.S[j], cols = jobs.cols[j], split = jobs.split[j];
+    const int64_t total = (int64_t)jobs.rows[j] * cols;
+    const int el = threadIdx.x % SR_E, g = threadIdx.x / SR_E;
+    const int64_t e = (int64_t)(blockIdx.x - jobs.first[j]) * SR_E + el;
+    float acc = 0.f;
+    if (e < total) {
+        int s = g;
+        for (; s + (SR_U - 1) * SR_G < S; s += SR_U * SR_G) {
+            float v[SR_U];
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) v[u] = slab[(int64_t)(s + u * SR_G) * total + e];
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) acc += v[u];
+        }
+        for (; s < S; s += SR_G) acc += slab[(int64_t)s * total + e];
+    }
+    red[g][el] = acc;
+    __syncthreads();
+    if (g == 0 && e < total) {
+        const float sum = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
+        const int r = (int)(e / cols), c = (int)(e - (int64_t)r * cols);
+        const int orow = r < split ? r : r - split;
+        const int ocol = r < split ? c : c + cols;
+        jobs.out[j][(int64_t)orow * jobs.ldo[j] + ocol] = sum;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // bf16-operand GEMMs staged by LDS-DMA (global_load_lds_dwordx4).
 // Both operands bf16 in HBM, either both k-contiguous ("NT": C = A B^T, the
@@ -1492,6 +1536,32 @@ int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, cons
     }
     jobs.first[n] = blocks;
     hipLaunchKernelGGL(weight_prep_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, dgx_stream(stream), jobs);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_slab_reduce_multi_f32(int n, const float* const* slab, const int* S, const int* rows, const int* cols,
+                              const int* split, float* const* out, const int64_t* ldo, void* stream) {
+    if (n < 1 || n > SRM_MAXJ || !slab || !S || !rows || !cols || !split || !out || !ldo) return DGX_EINVAL;
+    SlabJobs jobs;
+    jobs.n = n;
+    int blocks = 0;
+    for (int j = 0; j < n; ++j) {
+        if (!slab[j] || !out[j] || S[j] < 1 || rows[j] < 0 || cols[j] < 0 || split[j] < 0 || split[j] > rows[j])
+            return DGX_EINVAL;
+        jobs.slab[j] = slab[j];
+        jobs.out[j] = out[j];
+        jobs.ldo[j] = ldo[j];
+        jobs.S[j] = S[j];
+        jobs.rows[j] = rows[j];
+        jobs.cols[j] = cols[j];
+        jobs.split[j] = split[j];
+        jobs.first[j] = blocks;
+        blocks += (int)(((int64_t)rows[j] * cols[j] + SR_E - 1) / SR_E);
+    }
+    jobs.first[n] = blocks;
+    if (blocks == 0) return DGX_OK;
+    hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3((unsigned)blocks), dim3(SR_E * SR_G), 0, dgx_stream(stream),
+                       jobs);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -81,6 +81,7 @@ _SIGS = {
     "dgx_gemm_smallk_split_f32": [_vp, _i64, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_gemm_smallk_f32": [_vp, _i64, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     "dgx_slab_reduce_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp],
+    "dgx_slab_reduce_multi_f32": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dgx_gemm_lds_bf16": [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp,
                           _i64, _vp],
     "dgx_weight_prep_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],

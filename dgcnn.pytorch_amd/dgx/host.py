@@ -26,7 +26,7 @@ from . import precision as prec
 
 ENABLED = os.environ.get("DGX_HOST_EXT", "1") == "1"
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdgx_torch.so")
+LIB_PATH = os.environ.get("DGX_TORCH_LIB", os.path.join(_HERE, "libdgx_torch.so"))
 _lock = threading.Lock()
 _loaded = False
 

@@ -345,6 +345,12 @@ int dgx_gemm_smallk_split_f32(const float* X, int64_t ldx, const float* Wref, in
  * un-stacking (reference conv weight layout (Co, 2C, 1, 1)). */
 int dgx_slab_reduce_f32(const float* slab, int S, int rows, int cols, int split,
                         float* out, int64_t ldo, void* stream);
+/* dgx_slab_reduce_f32 for n <= 8 independent slabs in one launch (job j:
+ * slab[j], S[j], rows[j], cols[j], split[j] -> out[j] with row stride ldo[j];
+ * host arrays of length n): the weight gradients of one backward pass reduced
+ * together at its end, each element summed in dgx_slab_reduce_f32's order. */
+int dgx_slab_reduce_multi_f32(int n, const float* const* slab, const int* S, const int* rows, const int* cols,
+                              const int* split, float* const* out, const int64_t* ldo, void* stream);
 /* The same GEMMs with bf16 operands in HBM, staged by LDS-DMA
  * (global_load_lds) into swizzled LDS images. tn = 0: C = A B^T with A (M,K)
  * and B (N,K) k-contiguous, K % 64 == 0, epi 0/1/2. tn = 1: C = A^T B with A
