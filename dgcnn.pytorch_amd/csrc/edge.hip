@@ -2,7 +2,8 @@
 //
 // Materialises the reference's edge tensor for API callers (PositionEmbedding,
 // user code): out(b, c, n, kk) = x_j for c < C and x_i for c >= C, with the
-// knn_only / disp_only variants, plus its backward (scatter-add into dx).
+// knn_only / disp_only variants and the paper's / test.ipynb:131 form
+// (x_j - x_i, x_i) (DGX_GF_DIFFCAT), plus its backward (scatter-add into dx).
 // DGCNN's own blocks never call this: they gather straight from P/Q
 // (edgeconv.hip).
 #include <math.h>
@@ -15,7 +16,7 @@ namespace {
 __global__ void graph_feature_kernel(const float* __restrict__ x, int64_t sB, int64_t sC, int64_t sN, int B,
                                      int C, int N, const int32_t* __restrict__ idx, int k, int mode,
                                      float* __restrict__ out) {
-    const int64_t per_b = (mode == DGX_GF_CAT ? 2LL : 1LL) * C * N * k;
+    const int64_t per_b = (mode == DGX_GF_CAT || mode == DGX_GF_DIFFCAT ? 2LL : 1LL) * C * N * k;
     const int64_t total = per_b * B;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
@@ -35,7 +36,7 @@ __global__ void graph_feature_kernel(const float* __restrict__ x, int64_t sB, in
             int n = (int)(cn % N);
             int c2 = (int)(cn / N);
             int j = ib[(int64_t)n * k + kk];
-            if (mode == DGX_GF_DISP) {
+            if (mode == DGX_GF_DISP || (mode == DGX_GF_DIFFCAT && c2 < C)) {
                 out[t] = xb[c2 * sC + (int64_t)j * sN] - xb[c2 * sC + (int64_t)n * sN];
             } else {
                 out[t] = c2 < C ? xb[c2 * sC + (int64_t)j * sN] : xb[(c2 - C) * sC + (int64_t)n * sN];
@@ -62,14 +63,15 @@ __global__ void graph_feature_bwd_kernel(const float* __restrict__ dout, int B, 
             const float* d = dout + (((int64_t)b * N + n) * k) * C + c;
             for (int kk = 0; kk < k; ++kk) atomicAdd(dxb + (int64_t)c * N + row[kk], d[(int64_t)kk * C]);
         } else {
-            const int Cp = mode == DGX_GF_CAT ? 2 * C : C;
+            const bool two = mode == DGX_GF_CAT || mode == DGX_GF_DIFFCAT;
+            const int Cp = two ? 2 * C : C;
             const float* d = dout + (((int64_t)b * Cp + c) * N + n) * k;
             for (int kk = 0; kk < k; ++kk) {
                 float g = d[kk];
                 atomicAdd(dxb + (int64_t)c * N + row[kk], g);
-                if (mode == DGX_GF_DISP) centre -= g;
+                if (mode == DGX_GF_DISP || mode == DGX_GF_DIFFCAT) centre -= g;
             }
-            if (mode == DGX_GF_CAT) {
+            if (two) {
                 const float* dc = dout + (((int64_t)b * Cp + C + c) * N + n) * k;
                 for (int kk = 0; kk < k; ++kk) centre += dc[kk];
             }
@@ -101,8 +103,8 @@ const char* dgx_strerror(int code) {
 
 int dgx_graph_feature_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, int B, int C, int N,
                           const int32_t* idx, int k, int mode, float* out, void* stream) {
-    if (!x || !idx || !out || B < 0 || C < 1 || N < 1 || k < 1 || mode < 0 || mode > 2) return DGX_EINVAL;
-    int64_t total = (int64_t)B * C * N * k * (mode == DGX_GF_CAT ? 2 : 1);
+    if (!x || !idx || !out || B < 0 || C < 1 || N < 1 || k < 1 || mode < 0 || mode > 3) return DGX_EINVAL;
+    int64_t total = (int64_t)B * C * N * k * (mode == DGX_GF_CAT || mode == DGX_GF_DIFFCAT ? 2 : 1);
     if (total == 0) return DGX_OK;
     hipLaunchKernelGGL(graph_feature_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), x, sB, sC,
                        sN, B, C, N, idx, k, mode, out);
@@ -111,7 +113,7 @@ int dgx_graph_feature_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, in
 
 int dgx_graph_feature_bwd_f32(const float* dout, int B, int C, int N, const int32_t* idx, int k, int mode,
                               float* dx, void* stream) {
-    if (!dout || !idx || !dx || B < 0 || C < 1 || N < 1 || k < 1 || mode < 0 || mode > 2) return DGX_EINVAL;
+    if (!dout || !idx || !dx || B < 0 || C < 1 || N < 1 || k < 1 || mode < 0 || mode > 3) return DGX_EINVAL;
     int64_t total = (int64_t)B * C * N;
     if (total == 0) return DGX_OK;
     hipLaunchKernelGGL(graph_feature_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), dout,

@@ -592,7 +592,13 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const T* __restric
 // whose range holds more than RG_CAP edges (degenerate clouds, e.g. all points
 // equal) places them in HBM and sorts each list there instead.
 constexpr int RG_THREADS = 512;
-constexpr int RG_CAP = 12288;
+#ifndef RG_CAP_DEF
+#define RG_CAP_DEF 12288
+#endif
+#ifndef RG_MIN_WG
+#define RG_MIN_WG 512
+#endif
+constexpr int RG_CAP = RG_CAP_DEF;
 constexpr int RG_U = 8;  // independent index loads in flight per thread
 
 __device__ __forceinline__ int32_t block_sum_rg(int32_t v, int32_t* red) {
@@ -1312,7 +1318,7 @@ int dgx_graph_reverse_multi(int n, const int32_t* const* idx, int B, int N, int 
     // (every workgroup of a cloud scans it twice); a range's edges (about
     // N*k/P) stay well inside the LDS list capacity
     int P = 1;
-    while (P < N && ((int64_t)n * B * P < 512 || (int64_t)N * k / P > RG_CAP / 2)) P *= 2;
+    while (P < N && ((int64_t)n * B * P < RG_MIN_WG || (int64_t)N * k / P > RG_CAP / 2)) P *= 2;
     const int R = (N + P - 1) / P;
     // list capacity 1.75x a range's mean edge count (two workgroups per CU at
     // cfg2); a range beyond it (degenerate clouds) sorts its lists in HBM

@@ -1237,7 +1237,10 @@ bool aligned_to(const void* p, int bytes) { return (reinterpret_cast<uintptr_t>(
 // work (2*M*N*K flops) is a few microseconds of HBM writes, not a GEMM.
 // Block = 64 rows; W and the rows' X staged in LDS; each thread writes 4
 // consecutive columns (16-B stores along the row).
-constexpr int SK_ROWS = 64;
+#ifndef SK_ROWS_DEF
+#define SK_ROWS_DEF 64
+#endif
+constexpr int SK_ROWS = SK_ROWS_DEF;
 constexpr int SK_MAXK = 16;
 // split != 0: W is a conv weight in the reference layout (N/2, 2K) = [W1 | W2]
 // and row n of the product's weight is W1[n] (n < N/2) or W2[n - N/2]: the

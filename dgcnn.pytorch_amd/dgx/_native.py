@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("DGX_LIB", os.path.join(_HERE, "libdgx.so"))
 
 ORDER_STRIDED = 0
 ORDER_VEC8X4 = 1
-GF_CAT, GF_DISP, GF_KNN_ONLY = 0, 1, 2
+GF_CAT, GF_DISP, GF_KNN_ONLY, GF_DIFFCAT = 0, 1, 2, 3
 
 _lock = threading.Lock()
 _lib = None
@@ -34,6 +34,8 @@ _SIGS = {
     "dgx_knn_prepare_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _sz, _vp],
     "dgx_knn_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
     "dgx_sqnorm_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp],
+    "dgx_knn_generic_workspace_bytes": [_i32, _i32, _i32],
+    "dgx_knn_generic_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp],
     "dgx_knn_select_f32": [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp],
     "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
@@ -123,6 +125,7 @@ _RESTYPES = {
     "dgx_knn_kernel_name": ctypes.c_char_p,
     "dgx_knn_workspace_bytes": _sz,
     "dgx_knn_image_bytes": _sz,
+    "dgx_knn_generic_workspace_bytes": _sz,
 }
 
 

@@ -47,8 +47,9 @@ def knn(x, k):
     return pd.sort(dim=-1, descending=True, stable=True)[1][..., :k].contiguous()
 
 
-def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
-    """Edge features of reference dgcnn.py:15-44 (differentiable in x)."""
+def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None, mode="cat"):
+    """Edge features of reference dgcnn.py:15-44 (differentiable in x);
+    mode "diff": (x_j - x_i, x_i) of test.ipynb:131."""
     if x.dtype != torch.float32:
         x = x.float()
     B, C, N = x.shape
@@ -63,7 +64,8 @@ def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
     ctr = rows.view(B, N, 1, C).repeat(1, 1, k, 1)
     if disp_only:
         return (nbr - ctr).permute(0, 3, 1, 2).contiguous()
-    return torch.cat((nbr, ctr), dim=3).permute(0, 3, 1, 2).contiguous()
+    first = nbr - ctr if mode == "diff" else nbr
+    return torch.cat((first, ctr), dim=3).permute(0, 3, 1, 2).contiguous()
 
 
 def _edge_values(x, idx, weight):
@@ -81,17 +83,18 @@ def _edge_values(x, idx, weight):
     return (Pj + Q.unsqueeze(2)).permute(0, 3, 1, 2)               # (B, Co, N, k)
 
 
-def edgeconv_block(x, k, seq):
+def edgeconv_block(x, k, seq, weight=None):
     """max_k LeakyReLU(BN(Conv2d_1x1(get_graph_feature(x, k)))), reference
-    dgcnn.py:84-98, with the block's own modules; x (B, C, N) -> (B, Co, N)."""
+    dgcnn.py:84-98, with the block's own modules; x (B, C, N) -> (B, Co, N).
+    ``weight``: the conv weight to use instead of the module's (edge_mode "diff")."""
     conv, bn, act = seq[0], seq[1], seq[2]
-    y = _edge_values(x, knn(x, k), conv.weight)
+    y = _edge_values(x, knn(x, k), conv.weight if weight is None else weight)
     if conv.bias is not None:
         y = y + conv.bias.view(1, -1, 1, 1)
     return act(bn(y)).max(dim=-1, keepdim=False)[0]
 
 
-def edgeconv_stack_pair(x, k, convs, training=None, preps=None):
+def edgeconv_stack_pair(x, k, convs, training=None, preps=None, weights=None):
     """The engine's chain contract (dgx.edgeconv.edgeconv_stack_pair): the
     blocks' outputs concatenated point-major (B*N, sum Co), and an empty bf16
     twin. Block l > 1 searches its neighbours on the previous block's
@@ -100,8 +103,8 @@ def edgeconv_stack_pair(x, k, convs, training=None, preps=None):
         x = x.float()
     B, _, N = x.shape
     h, outs = x, []
-    for seq in convs:
-        h = edgeconv_block(h, k, seq)
+    for li, seq in enumerate(convs):
+        h = edgeconv_block(h, k, seq, None if weights is None else weights[li])
         outs.append(h)
     cat = torch.cat(outs, dim=1)                                    # (B, sum Co, N)  dgcnn.py:100
     return cat.permute(0, 2, 1).reshape(B * N, -1), torch.empty(0, dtype=torch.bfloat16)

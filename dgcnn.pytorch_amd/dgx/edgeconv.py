@@ -361,33 +361,35 @@ class _EdgeConvStack(torch.autograd.Function):
         return (dx_in, None, None, None, None, *grads)
 
 
-def _layers_and_params(convs):
+def _layers_and_params(convs, weights=None):
     layers, params = [], []
-    for seq in convs:
+    for li, seq in enumerate(convs):
         conv, bn, act = seq[0], seq[1], seq[2]
         co, c2 = conv.weight.shape[0], conv.weight.shape[1]
         if conv.bias is not None or bn.weight is None:
             raise NotImplementedError("dgx EdgeConv expects Conv2d(bias=False) + affine BatchNorm "
                                       "(as the reference builds them, dgcnn.py:54-73)")
         layers.append(_Layer(c2 // 2, co, bn, act.negative_slope))
-        params += [conv.weight, bn.weight, bn.bias]
+        params += [conv.weight if weights is None else weights[li], bn.weight, bn.bias]
     return layers, params
 
 
-def edgeconv_stack_pair(x, k, convs, training=None, preps=None):
+def edgeconv_stack_pair(x, k, convs, training=None, preps=None, weights=None):
     """As edgeconv_stack, also returning the bf16 twin of the concat buffer
     (empty unless precision "bf16" produced it): conv5's GEMM operand.
     ``preps``: optional per-block bf16 weight copies (gemm.prep_weights) made
     by the caller in one launch with other layers' (None for block 1).
     ``training`` is accepted for call compatibility only: every BatchNorm
     decides batch vs running statistics by its own flags, as nn.BatchNorm does.
-    A host tensor takes the CPU path (dgx.cpu)."""
+    ``weights``: per-block conv weights used instead of the modules' (the
+    re-parameterised weights of DGCNN's edge_mode "diff"). A host tensor takes
+    the CPU path (dgx.cpu)."""
     if cpu.is_cpu(x):
-        return cpu.edgeconv_stack_pair(x, k, convs, training)
+        return cpu.edgeconv_stack_pair(x, k, convs, training, weights=weights)
     nat.require_device(x)
     if x.dtype != torch.float32:
         x = x.float()
-    layers, params = _layers_and_params(convs)
+    layers, params = _layers_and_params(convs, weights)
     # whether this forward will be differentiated (inside Function.forward grad
     # mode is always off, so it is decided here)
     need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))

@@ -76,9 +76,10 @@ def dgcnn_train(model, x):
     """DGCNN.forward (train mode) through torch.ops.dgx_host.dgcnn_train."""
     load()
     params, bufs, hyper = [], [], []
-    for seq in model.edge_blocks() + [model.conv5]:
+    weights = model.edge_weights() + [model.conv5[0].weight]   # re-parameterised in edge_mode "diff"
+    for w, seq in zip(weights, model.edge_blocks() + [model.conv5]):
         conv, bn, act = seq[0], seq[1], seq[2]
-        params += [conv.weight, bn.weight, bn.bias]
+        params += [w, bn.weight, bn.bias]
         bufs += [bn.running_mean, bn.running_var, bn.num_batches_tracked]
         hyper += [float(bn.momentum), float(bn.eps), float(act.negative_slope)]
     idx0 = None

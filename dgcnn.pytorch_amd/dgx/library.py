@@ -145,7 +145,7 @@ torch.library.register_autocast("dgx::knn", "cuda", torch.float32)
 # --------------------------------------------------------- graph feature ----
 def _gf_shape(x, k, mode):
     B, C, N = x.shape
-    if mode == ops.nat.GF_CAT:
+    if mode in (ops.nat.GF_CAT, ops.nat.GF_DIFFCAT):
         return (B, 2 * C, N, k)
     if mode == ops.nat.GF_DISP:
         return (B, C, N, k)
@@ -166,7 +166,8 @@ def graph_feature(x: Tensor, k: int, mode: int) -> tuple[Tensor, Tensor]:
 def _(x, k, mode):
     xf = x.float().detach()
     idx = cpu.knn(xf, k)
-    out = cpu.graph_feature(xf, k, knn_only=mode == ops.nat.GF_KNN_ONLY, disp_only=mode == ops.nat.GF_DISP, idx=idx)
+    out = cpu.graph_feature(xf, k, knn_only=mode == ops.nat.GF_KNN_ONLY, disp_only=mode == ops.nat.GF_DISP, idx=idx,
+                            mode="diff" if mode == ops.nat.GF_DIFFCAT else "cat")
     return out, idx.to(_I32)
 
 
@@ -197,6 +198,9 @@ def _(grad, idx, C, mode):
     elif mode == ops.nat.GF_DISP:                         # (B, C, N, k) = x_j - x_i
         g = grad.permute(0, 2, 3, 1).reshape(B * N * k, C)
         gn, gc = g, -g
+    elif mode == ops.nat.GF_DIFFCAT:                      # (B, 2C, N, k) = cat(x_j - x_i, x_i)
+        g = grad.permute(0, 2, 3, 1).reshape(B * N * k, 2 * C)
+        gn, gc = g[:, :C], g[:, C:] - g[:, :C]
     else:                                                 # (B, 2C, N, k) = cat(x_j, x_i)
         g = grad.permute(0, 2, 3, 1).reshape(B * N * k, 2 * C)
         gn, gc = g[:, :C], g[:, C:]
@@ -544,17 +548,18 @@ def dgcnn_forward(model, x):
     for conv, bn in zip(convs + [c5], bns + [bn5]):
         if conv.bias is not None or bn.weight is None:
             raise NotImplementedError("dgx DGCNN expects Conv(bias=False) + affine BatchNorm (dgcnn.py:54-78)")
-    params = [p for c, bn in zip(convs + [c5], bns + [bn5]) for p in (c.weight, bn.weight, bn.bias)]
+    eff = model.edge_weights()   # per-block conv weights (re-parameterised in edge_mode "diff")
+    params = [p for w, bn in zip(eff + [c5.weight], bns + [bn5]) for p in (w, bn.weight, bn.bias)]
     need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
     prep = None
     if bf16:   # one launch for every bf16 operand copy of the step (blocks 2-4, conv5)
-        ws = [c.weight.detach() for c in convs[1:]] + [c5.weight.detach()]
+        ws = [w.detach() for w in eff[1:]] + [c5.weight.detach()]
         shapes = _dgcnn_prep_shapes(ws)
         prep = torch.ops.dgx.weight_prep(ws, [s[0] for s in shapes], [s[1] for s in shapes],
                                          [s[2] for s in shapes], [s[3] for s in shapes])
     bn_in = [_bn_args(bn, dev) for bn in bns]
     xcat, xcat16, rms, rvs, nbs, _ = torch.ops.dgx.edgeconv_chain(
-        x, model.k, [c.weight for c in convs], [bn.weight for bn in bns], [bn.bias for bn in bns],
+        x, model.k, eff, [bn.weight for bn in bns], [bn.bias for bn in bns],
         [a[0] for a in bn_in], [a[1] for a in bn_in], [a[2] for a in bn_in], [a[3] for a in bn_in],
         [a[4] for a in bn_in], [a[5] for a in bn_in], [a[6] for a in bn_in],
         [float(b[2].negative_slope) for b in blocks], bf16, need_grad, prep)
@@ -562,7 +567,7 @@ def dgcnn_forward(model, x):
     prep5 = None
     if prep is not None:
         # conv5's copies are the last entry of the shared buffer: pass them as their own view
-        _, lay = G.prep_layout(_dgcnn_prep_shapes([c.weight for c in convs[1:]] + [c5.weight]))
+        _, lay = G.prep_layout(_dgcnn_prep_shapes(eff[1:] + [c5.weight]))
         off = lay[3][0]
         prep5 = prep[off:]
     out, rm5, rv5, nb5, _ = torch.ops.dgx.pointconv(xcat, xcat16, B, N, c5.weight, bn5.weight, bn5.bias, a5[0], a5[1],

@@ -42,6 +42,38 @@ def knn_image_buffers(B, C, N, dev):
     return xx, img
 
 
+# shapes of the fused selection kernel (csrc/knn.hip); the rest take the
+# generic path (csrc/knn_generic.hip): same values, same canonical order
+FAST_MAXC, FAST_MAXK, FAST_MAXN = 128, 64, 12288
+GENERIC_MAXK = 8192
+
+
+def fast_shape(C, k, N):
+    return C <= FAST_MAXC and k <= FAST_MAXK and N <= FAST_MAXN
+
+
+def _knn_generic(x, strides, shape, k, order, idx, vals, stream):
+    """dgx_knn_generic_f32 on a (B,C,N) view; a view with neither inner
+    stride 1 is read from a contiguous copy (the rounding order was taken from
+    the caller's strides)."""
+    B, C, N = shape
+    sB, sC, sN = strides
+    if k > GENERIC_MAXK:
+        raise NotImplementedError(f"dgx knn: k = {k} > {GENERIC_MAXK} neighbours")
+    if sN != 1 and sC != 1:
+        x = torch.as_strided(x, shape, strides).contiguous()
+        sB, sC, sN = x.stride()
+    L = nat.lib()
+    ws_bytes = L.dgx_knn_generic_workspace_bytes(B, C, N)
+    ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=x.device)
+    i64 = idx.dtype == torch.int64
+    with torch.cuda.device(x.device):
+        nat.check(L.dgx_knn_generic_f32(nat.f32(x), sB, sC, sN, B, C, N, k, order,
+                                        nat.ptr(idx, torch.int64) if i64 else None,
+                                        nat.i32(idx) if not i64 else None, nat.f32(vals), nat.f32(ws), ws_bytes,
+                                        stream), "knn (generic)")
+
+
 def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, return_values=False, prepared=None):
     """kNN on a (B,C,N) fp32 view. ``strides``/``shape`` let callers describe a
     strided slice of a larger buffer (the engine's point-major concat buffer).
@@ -55,8 +87,9 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
         order = reduction_order(x)
     if not (1 <= k <= N):
         raise RuntimeError(f"knn: selected index k out of range (k={k}, N={N})")
-    if C > 128 or k > 64:
-        raise NotImplementedError(f"dgx knn kernels are built for C <= 128 and k <= 64 (C={C}, k={k})")
+    generic = not fast_shape(C, k, N)
+    if generic and prepared is not None:
+        raise RuntimeError("knn: prepared operands exist for the fused kernel's shapes only")
     cache = getattr(_tls, "cache", None)
     key = None
     if cache is not None and not return_values:
@@ -69,6 +102,11 @@ def knn_raw(x, k, order=None, out_dtype=torch.int64, strides=None, shape=None, r
     idx = torch.empty((B, N, k), dtype=out_dtype, device=x.device)
     vals = torch.empty((B, N, k), dtype=torch.float32, device=x.device) if return_values else None
     stream = nat.stream_of(x)
+    if generic:
+        _knn_generic(x, (sB, sC, sN), (B, C, N), k, order, idx, vals, stream)
+        if key is not None:
+            cache[key] = (idx, x)
+        return (idx, vals) if return_values else idx
     img_bytes = L.dgx_knn_image_bytes(B, C, N)
     if prepared is not None:
         xx, img = prepared
@@ -144,7 +182,7 @@ class _GraphFeature(torch.autograd.Function):
         x = x.float()
         B, C, N = x.shape
         k = idx32.shape[-1]
-        if mode == nat.GF_CAT:
+        if mode in (nat.GF_CAT, nat.GF_DIFFCAT):
             out = torch.empty((B, 2 * C, N, k), dtype=torch.float32, device=x.device)
         elif mode == nat.GF_DISP:
             out = torch.empty((B, C, N, k), dtype=torch.float32, device=x.device)
@@ -173,18 +211,23 @@ class _GraphFeature(torch.autograd.Function):
         return dx, None, None
 
 
-def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None):
+def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None, mode="cat"):
     """Drop-in for reference ``get_graph_feature`` (models/dgcnn.py:15-44).
 
     Default: (B,2C,N,k) fp32 contiguous, channels [0,C) = x_j, [C,2C) = x_i
     (dgcnn.py:42). knn_only: (B,N,k,C) neighbour rows (dgcnn.py:37-38).
-    disp_only: (B,C,N,k) x_j - x_i (dgcnn.py:39-40). Differentiable w.r.t. x."""
-    mode = nat.GF_KNN_ONLY if knn_only else (nat.GF_DISP if disp_only else nat.GF_CAT)
+    disp_only: (B,C,N,k) x_j - x_i (dgcnn.py:39-40). ``mode="diff"`` (engine
+    extension): channels [0,C) = x_j - x_i, the paper's / test.ipynb:131 form.
+    Differentiable w.r.t. x."""
+    if mode not in ("cat", "diff"):
+        raise ValueError(f"get_graph_feature: mode must be 'cat' or 'diff', got {mode!r}")
+    diff = mode == "diff"
+    mode = nat.GF_KNN_ONLY if knn_only else (nat.GF_DISP if disp_only else (nat.GF_DIFFCAT if diff else nat.GF_CAT))
     if torch.compiler.is_compiling() and idx is None:   # traced as one dgx::graph_feature op
         from . import library  # noqa: F401
         return torch.ops.dgx.graph_feature(x, k, mode)[0]
     if cpu.is_cpu(x):
-        return cpu.graph_feature(x, k, knn_only, disp_only, idx)
+        return cpu.graph_feature(x, k, knn_only, disp_only, idx, mode="diff" if diff else "cat")
     nat.require_device(x)
     x = _as_f32(x)
     if idx is None:

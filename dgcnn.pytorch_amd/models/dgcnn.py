@@ -30,9 +30,11 @@ def knn(x, k):
     return _ops.knn(x, k)
 
 
-def get_graph_feature(x, k=20, knn_only=False, disp_only=False):
-    """Edge features of reference dgcnn.py:15-44 (differentiable in x)."""
-    return _ops.graph_feature(x, k=k, knn_only=knn_only, disp_only=disp_only)
+def get_graph_feature(x, k=20, knn_only=False, disp_only=False, mode="cat"):
+    """Edge features of reference dgcnn.py:15-44 (differentiable in x).
+    ``mode="diff"`` (engine extension) gives the paper's (x_j - x_i, x_i)
+    form of test.ipynb:131 instead of dgcnn.py:42's (x_j, x_i)."""
+    return _ops.graph_feature(x, k=k, knn_only=knn_only, disp_only=disp_only, mode=mode)
 
 
 def _edge_block(c_in, c_out):
@@ -42,17 +44,24 @@ def _edge_block(c_in, c_out):
                          nn.LeakyReLU(negative_slope=0.2, inplace=True))
 
 
+def _diff_weight(w):
+    """The conv weight that applied to (x_j, x_i) equals ``w`` applied to
+    (x_j - x_i, x_i): [W1 | W2] -> [W1 | W2 - W1] (differentiable, so the
+    module's gradient follows by autograd)."""
+    c = w.shape[1] // 2
+    return torch.cat([w[:, :c], w[:, c:] - w[:, :c]], dim=1)
+
+
 def _bf16_weight_copies(model):
     """bf16 operand copies ([W1;W2] / W and transposes) of conv2..conv5 for the
     engine's bf16 GEMMs, all in one launch per step (precision "bf16" only)."""
     if _prec.get() != "bf16":
         return None
     jobs = []
-    for conv in (model.conv2, model.conv3, model.conv4):
+    for w in model.edge_weights()[1:]:
         # EdgeConv weights in the split (hi + lo) form: BN normalises edge values
         # y = P_j + Q_i whose batch spread is small next to their size, so the
         # weights' bf16 rounding is the largest error term the blocks can shed cheaply
-        w = conv[0].weight
         jobs.append((w, w.shape[0], w.shape[1] // 2, True, True))
     w5 = model.conv5[0].weight
     jobs.append((w5, w5.shape[0], w5.shape[1], False))
@@ -63,10 +72,13 @@ def _bf16_weight_copies(model):
 class DGCNN(nn.Module):
     """4 EdgeConv blocks (3->64->64->128->256) + conv5 (512->emb); input
     (B,3,N), output (B,emb,N). Reads ``args.emb_dim`` and ``args.k``
-    (reference dgcnn.py:47-78). Engine extension: an optional ``args.in_dims``
+    (reference dgcnn.py:47-78). Engine extensions: an optional ``args.in_dims``
     (default 3, the reference's) sets the input channels, e.g. 9 for the S3DIS
-    block layout (prepare_data/indoor3d_util.py:238-261); the default model's
-    parameters and state_dict are the reference's."""
+    block layout (prepare_data/indoor3d_util.py:238-261); an optional
+    ``args.edge_mode`` "diff" makes each block see the paper's edge feature
+    (x_j - x_i, x_i) (test.ipynb:131) instead of dgcnn.py:42's (x_j, x_i) — the
+    same kernels on the re-parameterised weight [W1 | W2 - W1]. The default
+    model's parameters and state_dict are the reference's."""
 
     WIDTHS = (64, 64, 128, 256)
 
@@ -74,6 +86,9 @@ class DGCNN(nn.Module):
         super().__init__()
         self.emb_dims = args.emb_dim
         self.k = args.k
+        self.edge_mode = getattr(args, "edge_mode", "cat")
+        if self.edge_mode not in ("cat", "diff"):
+            raise ValueError(f"DGCNN: edge_mode must be 'cat' or 'diff', got {self.edge_mode!r}")
         c_in = getattr(args, "in_dims", 3)
         for i, c_out in enumerate(self.WIDTHS, start=1):
             setattr(self, f"conv{i}", _edge_block(c_in, c_out))
@@ -85,11 +100,16 @@ class DGCNN(nn.Module):
     def edge_blocks(self):
         return [self.conv1, self.conv2, self.conv3, self.conv4]
 
+    def edge_weights(self):
+        """The blocks' conv weights as the engine applies them to (x_j, x_i)."""
+        ws = [b[0].weight for b in self.edge_blocks()]
+        return [_diff_weight(w) for w in ws] if self.edge_mode == "diff" else ws
+
     def forward(self, x):
         if x.device.type == "cpu":
             # host tensors (reference dgcnn.py:19-20 runs on either device): the
             # CPU path of every block (dgx.cpu), same modules and state
-            feats, _ = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training)
+            feats, _ = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training, weights=self.edge_weights())
             return pointconv_bn_lrelu(feats, x.shape[0], x.shape[2], self.conv5, self.training)
         if _host.applies(self, x):
             # train step of the reference's scripts: one C++ op + C++ autograd node (libdgx_torch.so)
@@ -101,7 +121,8 @@ class DGCNN(nn.Module):
         preps = _bf16_weight_copies(self) if self.training else None
         # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)
         feats, feats16 = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training,
-                                             preps=None if preps is None else preps[:4])   # (B*N, 512)
+                                             preps=None if preps is None else preps[:4],
+                                             weights=self.edge_weights())   # (B*N, 512)
         # conv5 -> BN -> LeakyReLU (dgcnn.py:100-102), written as (B, emb, N)
         return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training, X16=feats16,
                                   wprep=None if preps is None else preps[4])

@@ -39,6 +39,7 @@ extern "C" {
 #define DGX_GF_CAT 0      /* (B,2C,N,k): [x_j ; x_i]          dgcnn.py:42-44 */
 #define DGX_GF_DISP 1     /* (B,C,N,k):  x_j - x_i            dgcnn.py:39-40 */
 #define DGX_GF_KNN_ONLY 2 /* (B,N,k,C):  x_j                  dgcnn.py:37-38 */
+#define DGX_GF_DIFFCAT 3  /* (B,2C,N,k): (x_j - x_i, x_i)    test.ipynb:131 (the paper's form) */
 
 const char* dgx_version(void);
 const char* dgx_strerror(int code);
@@ -89,6 +90,19 @@ int dgx_knn_select_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                        const float* xx, int B, int C, int N, int k,
                        int64_t* idx64, int32_t* idx32, float* vals,
                        const void* image, size_t image_bytes, void* stream);
+
+/* The same kNN for every shape the fused selection kernel is not built for
+ * (C > 128, k > 64, N > 12288; the reference, dgcnn.py:6-12, takes any C,
+ * k <= N and N): |x|^2 in the reference's order for any C, the Gram chain on
+ * dgx_gemm_f32 (one fp32 MFMA accumulation chain per output, c in order), and
+ * an exact radix select + bitonic sort per query row — identical values and
+ * canonical order. x needs sN == 1 or sC == 1; k <= 8192. Workspace:
+ * dgx_knn_generic_workspace_bytes(B,C,N) (|x|^2 + one chunk of dot rows). */
+size_t dgx_knn_generic_workspace_bytes(int B, int C, int N);
+int dgx_knn_generic_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
+                        int B, int C, int N, int k, int order,
+                        int64_t* idx64, int32_t* idx32, float* vals,
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- a2: edge features, replaces models/dgcnn.py:15-44 (get_graph_feature)
  * after the knn call: idx (B,N,k) int32 local indices. out is contiguous in

@@ -78,3 +78,14 @@ def test_host_op_library_loads():
     schema = str(torch.ops.dgx_host.dgcnn_train.default._schema)
     assert schema.startswith("dgx_host::dgcnn_train(Tensor x, Tensor[] params, Tensor[] bufs, Tensor? idx0")
     assert not host.applies(DGCNN(types.SimpleNamespace(emb_dim=64, k=4)).train(), torch.rand(2, 3, 32))
+
+
+def test_knn_shape_routing():
+    """Shapes outside the fused kNN kernel route to the generic path (any C,
+    k up to 8192, any N) instead of failing; its workspace query is exported."""
+    from dgx import _native, ops
+    assert ops.fast_shape(128, 64, 12288) and not ops.fast_shape(129, 20, 1024)
+    assert not ops.fast_shape(3, 65, 1024) and not ops.fast_shape(3, 20, 12289)
+    L = _native.lib()
+    # |x|^2 (B*N, 16-byte rounded) + one chunk of dot rows (min(N, 2^24 / N rounded to 64) x N)
+    assert L.dgx_knn_generic_workspace_bytes(2, 256, 1000) == (2000 + 1000 * 1000) * 4
