@@ -44,19 +44,39 @@ def _reference_diff(m, x):
 
 
 def test_dgcnn_diff_mode_fp32(cuda):
+    """Output vs the stock-module restatement (fp32), and every parameter
+    gradient vs the fp64 oracle routed by the engine's own decisions (neighbour
+    sets, max slots, LeakyReLU signs) — the bar of test_edgeconv_gpu's
+    test_dgcnn_train_routed, which a plain fp32-vs-fp32 comparison cannot hold:
+    near-tied maxima route a gradient to different edges in two fp32 orders."""
     from dgx import synth
+    from models.dgcnn import _diff_weight
+    from oracle import reference as R
+    from test_edgeconv_gpu import ROUTED_GRAD_TOL, Capture
     torch.manual_seed(4)
     base = DGCNN_diff()
+    init = {n: t.detach().clone() for n, t in base.state_dict().items()}
     x = torch.from_numpy(synth.cube_clouds(2, 512, 3)).to(cuda).permute(0, 2, 1)
     ma, mb = copy.deepcopy(base).to(cuda).train(), copy.deepcopy(base).to(cuda).train()
-    ya = ma(x)
+    with Capture() as cap:
+        ya = ma(x)
     yb = _reference_diff(mb, x)
     assert rel_err(ya.detach().cpu(), yb.detach().cpu()) < 1e-4
     g = torch.randn_like(ya)
     ya.backward(g)
-    yb.backward(g)
-    for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
-        assert rel_err(pa.grad.cpu(), pb.grad.cpu()) < 1e-3, n
+    decisions = [tuple(t for t in cap[("fwd", l)]) for l in range(4)]
+    p64 = {n: t.to(cuda).double() if t.is_floating_point() else t.to(cuda) for n, t in init.items()}
+    for n, t in p64.items():
+        if t.is_floating_point() and "running" not in n:
+            t.requires_grad_(True)
+    routed = dict(p64)
+    for i in range(1, 5):
+        routed[f"conv{i}.0.weight"] = _diff_weight(p64[f"conv{i}.0.weight"])
+    ref = R.dgcnn_routed(x.double(), routed, [(i.long(), a, z) for (i, a, z) in decisions], ya.detach() > 0)
+    assert rel_err(ya.detach().cpu(), ref.detach().cpu()) < 1e-4
+    ref.backward(g.double())
+    for n, p in ma.named_parameters():
+        assert rel_err(p.grad.cpu(), p64[n].grad.cpu()) < ROUTED_GRAD_TOL, n
 
 
 def DGCNN_diff():
