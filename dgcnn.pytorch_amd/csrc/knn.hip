@@ -30,6 +30,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -400,8 +402,7 @@ template <int KB, int QG>
 constexpr int knn_smem_floats_qg() {
     constexpr int qpb = KQ_GROUPS * KQ_QPW * QG;
     constexpr int stream = KQ_HALVES * qpb                              // published admission bounds
-                           + KQ_WAVES * QG * KQ_QCAP * 64               // FIFO values
-                           + KQ_WAVES * QG * KQ_QCAP * 32;              // FIFO indices (u16)
+                           + KQ_WAVES * QG * KQ_QCAP * 64 * 2;          // FIFO (value, index) pairs
     constexpr int merge = KQ_HALVES * qpb * KB * 2 + 2 * qpb;          // half lists | k-th | flags
     constexpr int fix = merge + 2 * FX_CAP + 8 + FIX_MAXN / 32;         // ... | fix-up candidates, counters, tie bitmap
     return stream > fix ? stream : fix;
@@ -423,8 +424,9 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     constexpr int QPB = KQ_GROUPS * QPW;       // queries per block
     __shared__ __attribute__((aligned(16))) float smem[knn_smem_floats_qg<KB, QG>()];
     float* pub = smem;                         // [KQ_HALVES][QPB] admission bounds
-    float* fval = smem + KQ_HALVES * QPB;      // per (wave, group) [KQ_QCAP][64] pending values
-    uint16_t* fidx = reinterpret_cast<uint16_t*>(fval + KQ_WAVES * QG * KQ_QCAP * 64);  // ... and indices
+    // per (wave, group) [KQ_QCAP][64] pending (value, index) pairs: one 8-byte
+    // LDS store per considered candidate and a single address computation
+    float2* fifo = reinterpret_cast<float2*>(smem + KQ_HALVES * QPB);
 
     int b, qb;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
@@ -453,8 +455,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         float xxq, tseed, thr;
         float lv[KL];            // the lane's sorted list (value desc, index asc)
         int li[KL];
-        float* fv;               // the lane's FIFO of admitted candidates (LDS)
-        uint16_t* fj;
+        float2* fq;              // the lane's FIFO of admitted candidates (LDS, stride 64)
         int cnt;
         f32x4 acc;
         float last;
@@ -487,8 +488,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         S.thr = S.tseed;
 #pragma unroll
         for (int t = 0; t < KL; ++t) { S.lv[t] = -INFINITY; S.li[t] = 0x7fffffff; }
-        S.fv = fval + (wave * QG + e) * (KQ_QCAP * 64);
-        S.fj = fidx + (wave * QG + e) * (KQ_QCAP * 64);
+        S.fq = fifo + (wave * QG + e) * (KQ_QCAP * 64) + lane;
         S.cnt = 0;
     });
     // Each lane keeps, per group, the KL best of ITS candidates (sorted,
@@ -593,11 +593,13 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         // branch-free rounds: slots past a lane's count read stale entries and
         // are replaced by -inf, so every round is the same straight-line code;
         // the groups' lists are independent (two interleaved dependency chains)
-        float cv0 = G0.cnt > 0 ? G0.fv[lane] : -INFINITY, cv1 = 0.f;
-        int cj0 = G0.fj[lane], cj1 = 0;
+        float2 c0 = G0.fq[0], c1 = make_float2(0.f, 0.f);
+        float cv0 = G0.cnt > 0 ? c0.x : -INFINITY, cv1 = 0.f;
+        int cj0 = __float_as_int(c0.y), cj1 = 0;
         if constexpr (QG == 2) {
-            cv1 = G1.cnt > 0 ? G1.fv[lane] : -INFINITY;
-            cj1 = G1.fj[lane];
+            c1 = G1.fq[0];
+            cv1 = G1.cnt > 0 ? c1.x : -INFINITY;
+            cj1 = __float_as_int(c1.y);
         }
         const int cm = cmax();
         // fully unrolled with an early exit: no loop-carried copies of the list
@@ -608,16 +610,16 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
             ++n_rounds;
 #endif
             const int nx = min(t + 1, KQ_QCAP - 1);
-            float nv0 = G0.fv[nx * 64 + lane];
-            const int nj0 = G0.fj[nx * 64 + lane];
-            nv0 = t + 1 < G0.cnt ? nv0 : -INFINITY;
+            const float2 n0 = G0.fq[nx * 64];
+            const float nv0 = t + 1 < G0.cnt ? n0.x : -INFINITY;
+            const int nj0 = __float_as_int(n0.y);
             list_insert_ordered<KL>(G0.lv, G0.li, cv0 >= G0.thr ? cv0 : -INFINITY, cj0);
             cv0 = nv0;
             cj0 = nj0;
             if constexpr (QG == 2) {
-                float nv1 = G1.fv[nx * 64 + lane];
-                const int nj1 = G1.fj[nx * 64 + lane];
-                nv1 = t + 1 < G1.cnt ? nv1 : -INFINITY;
+                const float2 n1 = G1.fq[nx * 64];
+                const float nv1 = t + 1 < G1.cnt ? n1.x : -INFINITY;
+                const int nj1 = __float_as_int(n1.y);
                 list_insert_ordered<KL>(G1.lv, G1.li, cv1 >= G1.thr ? cv1 : -INFINITY, cj1);
                 cv1 = nv1;
                 cj1 = nj1;
@@ -644,14 +646,15 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         });
     };
 
-    auto consider = [&](Grp& S, float dot, float xc, int j) {
+    // TAIL: the cloud's last tile when N % 16 != 0 (wave-uniform), the only
+    // one whose rows can be padding (j >= N)
+    auto consider = [&](Grp& S, float dot, float xc, int j, auto tail) {
         const float tq = dot - xc;  // dot is already 2 x (query operand doubled)
         const float v = tq - S.xxq;
-        const bool pass = j < N && v >= S.thr;
+        const bool pass = (!decltype(tail)::value || j < N) && v >= S.thr;
         // unconditional store: a rejected candidate's slot is reused by the
         // next one (a tile adds at most 4 entries to a FIFO holding <= QCAP-4)
-        S.fv[S.cnt * 64 + lane] = v;
-        S.fj[S.cnt * 64 + lane] = (uint16_t)j;
+        S.fq[S.cnt * 64] = make_float2(v, __int_as_float(j));
         S.cnt += pass ? 1 : 0;
     };
 
@@ -706,13 +709,20 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
             load(slot, u + ub + RING, (ub + RING) % SPT);
             if (live && sl == SPT - 1) {
                 // lane holds rows 4g..4g+3 = candidates g, g+4, g+8, g+12 of the tile
-                const int j0 = (h + KQ_HALVES * ((u + ub) / SPT)) * 16 + g;
-                each([&](Grp& S, int) {
-                    consider(S, S.acc[0], xc.x, j0);
-                    consider(S, S.acc[1], xc.y, j0 + 4);
-                    consider(S, S.acc[2], xc.z, j0 + 8);
-                    consider(S, S.acc[3], xc.w, j0 + 12);
-                });
+                const int st = h + KQ_HALVES * ((u + ub) / SPT);
+                const int j0 = st * 16 + g;
+                auto cons4 = [&](auto tail) {
+                    each([&](Grp& S, int) {
+                        consider(S, S.acc[0], xc.x, j0, tail);
+                        consider(S, S.acc[1], xc.y, j0 + 4, tail);
+                        consider(S, S.acc[2], xc.z, j0 + 8, tail);
+                        consider(S, S.acc[3], xc.w, j0 + 12, tail);
+                    });
+                };
+                // (the two-group kernel keeps the check everywhere: its split
+                // code measured 2 us slower, r04u)
+                if (QG == 2 || (st + 1) * 16 > N) cons4(std::true_type{});
+                else cons4(std::false_type{});
                 if (__any(cmax() > KQ_QCAP - 4)) flush();
             }
         }
