@@ -32,25 +32,9 @@
 
 #include <type_traits>
 
-// diagnostics builds only (tools/r04v.sh): 1 = half the Gram chain, 2 = no
-// selection, 3 = both; results are wrong, the fix-up is skipped
-#ifndef KNN_PROBE
-#define KNN_PROBE 0
-#endif
-// C > 32 selects through knn_bf_kernel (0: the exact-chain knn_kernel, A/B builds)
-#ifndef KNN_BF
-#define KNN_BF 1
-#endif
-// diagnostics builds only (tools/r04x.sh): bit 1 = no exact phase, 2 = no
-// per-tile bound refresh, 4 = no candidate selection; results are wrong, no fix-up
-#ifndef KNN_BF_PROBE
-#define KNN_BF_PROBE 0
-#endif
-
 #include "common.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8_k __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -668,10 +652,6 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         const float tq = dot - xc;  // dot is already 2 x (query operand doubled)
         const float v = tq - S.xxq;
         const bool pass = (!decltype(tail)::value || j < N) && v >= S.thr;
-        if constexpr ((KNN_PROBE & 2) != 0) {
-            S.cnt += v > 1e30f ? 1 : 0;
-            return;
-        }
         // unconditional store: a rejected candidate's slot is reused by the
         // next one (a tile adds at most 4 entries to a FIFO holding <= QCAP-4)
         S.fq[S.cnt * 64] = make_float2(v, __int_as_float(j));
@@ -721,7 +701,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                 }
                 // the groups' chains interleaved: independent MFMAs back to back
 #pragma unroll
-                for (int t = 0; t < ((KNN_PROBE & 1) ? SW / 2 : SW); ++t)
+                for (int t = 0; t < SW; ++t)
                     each([&](Grp& S, int) {
                         S.acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][t], S.bq[sl * SW + t], S.acc, 0, 0, 0);
                     });
@@ -859,7 +839,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     float* fixa = smem + KQ_HALVES * QPB * KB * 2 + 2 * QPB;
     for (int f = 0; f < QPB; ++f) {
         const int qf = qb * QPB + f;
-        if (KNN_PROBE == 0 && flg[f] != 0 && qf < N)
+        if (flg[f] != 0 && qf < N)
             knn_fix_row<NSTEP>(fixa, ib, xib, xx + (int64_t)b * N, N, k, qf, kth[f], (int64_t)b * N + qf, idx64,
                                idx32, vals);
     }
@@ -868,406 +848,6 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
 #ifdef DGX_KNN_STATS
 uint32_t* g_knn_stats = nullptr;   // diagnostics build: device buffer set by dgx_knn_stats_buffer
 #endif
-
-// ------------------------------------------------- bf16-filtered kNN ----
-// C = 64 / 128 (NSTEP 16 / 32): the exact f32 Gram chain is most of the
-// selection kernel's time (r04v probes: 75 of 93 us at C = 64 run the MFMA
-// chain alone). This kernel streams the same operand image but forms
-// APPROXIMATE distances on the bf16 MFMA (v_mfma_f32_16x16x32_bf16, 16x the
-// f32 rate), keeps only the candidates the approximation cannot rule out, and
-// recomputes those exactly — the same fmaf chain the f32 MFMA runs (channel
-// order 4t + kk), so every value and the final top-k are bit-identical to
-// knn_kernel's.
-//
-// The bound. With hi = bf16(x) (round to nearest even: |x - hi| <= 2^-8 |x|),
-// pd' = fl(fl(2 hi_q.hi_j - xx_j) - xx_q) and the exact pd differ by at most
-//     eps_q = 1.02 (2^-6 + C 2^-20) |x_q| M + 2^-20 (2 |x_q| M + M^2 + xx_q)
-// (M = max_j |x_j| over the cloud; Cauchy-Schwarz on the rounding of both
-// operands, fp32 accumulation of both chains, the two subtractions). Let A_k
-// be the k-th largest pd' of the row and T <= A_k any value reached by k
-// candidates' pd' (here: the min over the row's 8 lists of their m-th pd',
-// m = ceil(k/8), lists only growing). k candidates have pd >= A_k - eps, so the
-// exact k-th value is >= T - eps and any member of the exact top-k (or tie with
-// its k-th) has pd' >= T - 2 eps. Candidates below the running T - 2 eps are
-// dropped; T only rises, so nothing dropped ever qualifies later.
-//
-// Per lane: the m best pd' (values only, v_med3 chain) give T; admitted
-// (pd', j) pairs wait in an LDS FIFO (CAP entries, compacted against the
-// current bound when it fills; a lane that still overflows flags its row for
-// the exact fix-up); after the stream the survivors of the final bound are
-// recomputed exactly (doubled query row from LDS, candidate row from the f32
-// image in L2) and inserted into the lane's exact list (KL), then the two-stage
-// canonical merge, the overflow flags and the fix-up of knn_kernel follow.
-constexpr int BF_CAP = 32;   // per-lane FIFO entries
-// FIFO entry: pd' rounded UP to bf16 precision (high half; a larger value only
-// keeps more candidates) | candidate index (low half, N <= 65535)
-__device__ __forceinline__ uint32_t bf_pack(float v, int j) {
-    const uint32_t u = __float_as_uint(v);
-    const uint32_t r = (int32_t)u < 0 ? (u & 0xffff0000u) : ((u + 0xffffu) & 0xffff0000u);
-    return r | (uint32_t)j;
-}
-__device__ __forceinline__ float bf_val(uint32_t e) { return __uint_as_float(e & 0xffff0000u); }
-// values kept per lane: a wave's 4 lists hold at least k (the half merge below)
-template <int KB>
-struct BfList {
-    static constexpr int MM = (KB + 3) / 4 + 1;
-};
-
-__device__ __forceinline__ bf16x8_k cvt8(const float* v, float s) {
-    bf16x8_k r;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = (__bf16)(v[e] * s);
-    return r;
-}
-
-template <int NSTEP, int KB>
-constexpr int knn_bf_smem_floats() {
-    constexpr int QPB = KQ_QPB;
-    constexpr int stream = KQ_HALVES * QPB + 8 + KQ_HALVES * QPB * KB + QPB * (4 * NSTEP + 4) +
-                           KQ_WAVES * BF_CAP * 64;
-    constexpr int merge = KQ_HALVES * QPB * KB * 2 + 2 * QPB;
-    constexpr int fix = merge + 2 * FX_CAP + 8 + FIX_MAXN / 32;
-    return stream > fix ? stream : fix;
-}
-
-template <int NSTEP, int KB>
-__global__ __launch_bounds__(KQ_THREADS, KB <= 40 ? 3 : 2)
-void knn_bf_kernel(const float* __restrict__ img, const float* __restrict__ xximg, const float* __restrict__ xx,
-                   int B, int N, int k, int nqb, int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
-                   float* __restrict__ vals) {
-#pragma clang fp contract(off)
-    static_assert(NSTEP % 8 == 0, "whole 32-channel MFMA chunks");
-    constexpr int NCH = NSTEP / 8;             // bf16 MFMAs per tile
-    constexpr int CP = 4 * NSTEP;              // padded channels
-    constexpr int XQS = CP + 4;                // LDS query-row stride (floats)
-    constexpr int KL = KnnList<KB>::KL;
-    constexpr int RPL = KnnList<KB>::RPL;
-    constexpr int MM = BfList<KB>::MM;
-    constexpr int QPB = KQ_QPB;
-    __shared__ __attribute__((aligned(16))) float smem[knn_bf_smem_floats<NSTEP, KB>()];
-    float* pub = smem;                                        // [KQ_HALVES][QPB] bounds T
-    float* red = smem + KQ_HALVES * QPB;                      // [KQ_WAVES] cloud max |x|^2
-    float* hl = red + 8;                                      // [KQ_HALVES][QPB][KB] half top-k of pd'
-    float* xqs = hl + KQ_HALVES * QPB * KB;                   // [QPB][XQS] doubled query rows
-    uint32_t* fifo = reinterpret_cast<uint32_t*>(xqs + QPB * XQS);  // [KQ_WAVES][BF_CAP][64]
-
-    int b, qb;
-    if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave % KQ_GROUPS;
-    const int h = wave / KQ_GROUPS;
-    const int g = lane >> 4;
-    const int ql = lane & 15;
-    const int ntile = (N + 15) >> 4;
-    const float* __restrict__ ib = img + (int64_t)b * ntile * 64 * NSTEP;
-    const float* __restrict__ xib = xximg + (int64_t)b * ntile * 16;
-    const float* __restrict__ xxb = xx + (int64_t)b * N;
-    const int m = (k + KQ_LISTS - 1) / KQ_LISTS;
-    const int qq = grp * KQ_QPW + ql;
-    const int q = qb * QPB + qq;
-
-    // cloud max |x_j|^2 (NaN rows are skipped by fmaxf; their own rows are
-    // flagged through a non-finite bound)
-    {
-        float mx = 0.f;
-        for (int e = tid; e < N; e += KQ_THREADS) mx = fmaxf(mx, xxb[e]);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-        if (lane == 0) red[wave] = mx;
-    }
-    // the query: bf16 B operand (doubled), doubled f32 row in LDS (written once per group)
-    const int qs = min(q, N - 1);
-    bf16x8_k bq[NCH];
-    {
-        float r[NSTEP];
-        ld_vec<NSTEP>(ib + ((int64_t)(qs >> 4) * 64 + g * 16 + knn_row(qs & 15)) * NSTEP, r);
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) bq[c] = cvt8(r + 8 * c, 2.0f);
-        if (h == 0) {
-#pragma unroll
-            for (int t = 0; t < NSTEP; ++t) xqs[qq * XQS + 4 * t + g] = 2.0f * r[t];
-        }
-    }
-    const float xxq = q < N ? xxb[q] : 0.f;
-    if (tid < KQ_HALVES * QPB) pub[tid] = -INFINITY;
-    for (int e = tid; e < KQ_HALVES * QPB * KB; e += KQ_THREADS) hl[e] = -INFINITY;
-    __syncthreads();
-    const float M2 = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    const float Mn = sqrtf(M2), nq = sqrtf(xxq);
-    const float eps = 1.02f * ((0x1p-6f + (float)CP * 0x1p-20f) * nq * Mn) +
-                      0x1p-20f * (2.0f * nq * Mn + M2 + xxq);
-    const float eps2 = 2.0f * eps;
-    auto bound = [&](float T) __attribute__((always_inline)) { return T - (eps2 + fabsf(T) * 0x1p-20f); };
-
-    float p[MM];   // the lane's MM best pd' (values only)
-#pragma unroll
-    for (int t = 0; t < MM; ++t) p[t] = -INFINITY;
-    uint32_t* fq = fifo + (int64_t)wave * BF_CAP * 64 + lane;
-    int cnt = 0;
-    bool ovf = false;
-    float athr = -INFINITY;
-    // T from the 8 lists: own m-th, the wave's other 3 lanes, the other half's last published value
-    auto refresh = [&]() __attribute__((always_inline)) {
-        float tm = p[0];
-#pragma unroll
-        for (int t = 1; t < MM; ++t) tm = (t == m - 1) ? p[t] : tm;
-        tm = fminf(tm, __shfl_xor(tm, 16));
-        tm = fminf(tm, __shfl_xor(tm, 32));
-        if (g == 0) __hip_atomic_store(pub + h * QPB + qq, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const float tp = __hip_atomic_load(pub + (1 - h) * QPB + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return fminf(tm, tp);
-    };
-    // Tighter bound from the k best pd' of the row seen so far: merge the wave's
-    // 4 value lists (k rounds of a 4-way arg-max, ties to the lowest lane group
-    // so exactly one entry pops), publish the half's top-k in hl, and take the
-    // k-th largest of its union with the other half's published top-k:
-    //   kth(a u b) = max(b[k-1], max_r min(a[r], b[k-2-r]))   (b[-1] = +inf).
-    // Entries only rise, so a stale (or torn) read of b is still a lower bound.
-    auto half_merge = [&]() __attribute__((always_inline)) {
-        float tp[MM];
-#pragma unroll
-        for (int t = 0; t < MM; ++t) tp[t] = p[t];
-        const float* ob = hl + ((1 - h) * QPB + qq) * KB;
-        float* own = hl + (h * QPB + qq) * KB;
-        float best = __hip_atomic_load(ob + k - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-        for (int r = 0; r < KB; ++r) {
-            if (r < k) {
-                float hv = tp[0];
-                int hg = g;
-                float pv = __shfl_xor(hv, 16);
-                int pg = __shfl_xor(hg, 16);
-                if (pv > hv || (pv == hv && pg < hg)) { hv = pv; hg = pg; }
-                pv = __shfl_xor(hv, 32);
-                pg = __shfl_xor(hg, 32);
-                if (pv > hv || (pv == hv && pg < hg)) { hv = pv; hg = pg; }
-                const bool pop = hg == g;
-#pragma unroll
-                for (int t = 0; t < MM - 1; ++t) tp[t] = pop ? tp[t + 1] : tp[t];
-                tp[MM - 1] = pop ? -INFINITY : tp[MM - 1];
-                if ((r & 3) == g) __hip_atomic_store(own + r, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const float bo = r == k - 1 ? INFINITY
-                                            : __hip_atomic_load(ob + (k - 2 - r), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-                best = fmaxf(best, fminf(hv, bo));
-            }
-        }
-        return best;
-    };
-    auto compact = [&]() __attribute__((always_inline)) {
-        athr = bound(fmaxf(refresh(), half_merge()));
-        int w = 0;
-#pragma unroll
-        for (int t = 0; t < BF_CAP; ++t) {
-            if (!__any(t < cnt)) break;
-            const uint32_t e = fq[t * 64];
-            const bool keep = t < cnt && bf_val(e) >= athr;
-            fq[w * 64] = e;
-            w += keep ? 1 : 0;
-        }
-        cnt = w;
-        if (cnt > BF_CAP - 4) {   // still full: drop the newest, the row takes the exact fix-up
-            ovf = true;
-            cnt = BF_CAP - 4;
-        }
-    };
-    auto consider = [&](float d, float xcj, int j, auto tail) __attribute__((always_inline)) {
-        float v = (d - xcj) - xxq;   // d = 2 hi_q . hi_j
-        if constexpr ((KNN_BF_PROBE & 4) != 0) {
-            cnt += v > 1e30f ? 1 : 0;
-            return;
-        }
-        if constexpr (decltype(tail)::value) v = j < N ? v : -INFINITY;
-#pragma unroll
-        for (int t = MM - 1; t > 0; --t) p[t] = __builtin_amdgcn_fmed3f(p[t - 1], p[t], v);
-        p[0] = fmaxf(p[0], v);
-        const bool pass = v >= athr;
-        fq[cnt * 64] = bf_pack(v, j);   // unconditional: a rejected slot is reused
-        cnt += pass ? 1 : 0;
-    };
-
-    // stream this half's tiles s = h, h + 2, ... with the next tile's operands in flight
-    const int ntl = (ntile - h + KQ_HALVES - 1) / KQ_HALVES;
-    float a[2][NSTEP];
-    float4 xc[2];
-    auto load = [&](int buf, int tl) __attribute__((always_inline)) {
-        const int s = h + KQ_HALVES * min(tl, ntl - 1);
-        ld_vec<NSTEP>(ib + ((int64_t)s * 64 + lane) * NSTEP, a[buf]);
-        xc[buf] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
-    };
-    auto tile = [&](int buf, int tl) __attribute__((always_inline)) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cvt8(a[buf] + 8 * c, 1.0f), bq[c], acc, 0, 0, 0);
-        const int st = h + KQ_HALVES * tl;
-        const int j0 = st * 16 + g;
-        auto cons4 = [&](auto tail) __attribute__((always_inline)) {
-            consider(acc[0], xc[buf].x, j0, tail);
-            consider(acc[1], xc[buf].y, j0 + 4, tail);
-            consider(acc[2], xc[buf].z, j0 + 8, tail);
-            consider(acc[3], xc[buf].w, j0 + 12, tail);
-        };
-        if ((st + 1) * 16 > N) cons4(std::true_type{});
-        else cons4(std::false_type{});
-        if constexpr ((KNN_BF_PROBE & 2) == 0) athr = bound(refresh());
-        if (__any(cnt > BF_CAP - 4)) compact();
-    };
-    if (ntl > 0) load(0, 0);
-#pragma unroll 1
-    for (int tl = 0; tl < ntl; tl += 2) {
-        load(1, tl + 1);
-        tile(0, tl);
-        if (tl + 1 < ntl) {
-            load(0, tl + 2);
-            tile(1, tl + 1);
-        }
-    }
-    // final bound: both halves' complete top-k (the k-th largest pd' of the row
-    // whenever every list holds all of its members of the top-k)
-    half_merge();
-    __syncthreads();
-    athr = bound(half_merge());
-
-    // exact values of the survivors, in the lane's (ascending) candidate order
-    float lv[KL];
-    int li[KL];
-#pragma unroll
-    for (int t = 0; t < KL; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
-    const float* __restrict__ xq2 = xqs + qq * XQS;
-#pragma unroll 1
-    for (int t = 0; t < ((KNN_BF_PROBE & 1) ? 0 : BF_CAP); ++t) {
-        if (!__any(t < cnt)) break;
-        const uint32_t e = fq[t * 64];
-        if (t < cnt && bf_val(e) >= athr) {
-            const int j = (int)(e & 0xffffu);
-            const int s = j >> 4, i = knn_row(j & 15);
-            const float* __restrict__ jr = ib + ((int64_t)s * 64 + i) * NSTEP;   // run kk at jr + 16 kk NSTEP
-            float dot = 0.f;
-#pragma unroll
-            for (int t0 = 0; t0 < NSTEP; t0 += 4) {
-                float4 r[4];
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) r[kk] = *reinterpret_cast<const float4*>(jr + 16 * kk * NSTEP + t0);
-                float qv[16];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float4 w = *reinterpret_cast<const float4*>(xq2 + 4 * (t0 + u));
-                    qv[4 * u] = w.x; qv[4 * u + 1] = w.y; qv[4 * u + 2] = w.z; qv[4 * u + 3] = w.w;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float rv[4] = {r[0][u], r[1][u], r[2][u], r[3][u]};
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) dot = fmaf(rv[kk], qv[4 * u + kk], dot);
-                }
-            }
-            const float v = (dot - xib[s * 16 + i]) - xxq;
-            list_insert_ordered<KL>(lv, li, v, j);
-        }
-    }
-
-    // merge the wave's 4 lists of each query, then the two halves (as knn_kernel)
-    const float last = lv[KL - 1];
-    float ov[RPL];
-    int oj[RPL], rk[RPL];
-#pragma unroll
-    for (int r = 0; r < KB; ++r) {
-        if (r < k) {
-            float hv = lv[0];
-            int hj = li[0];
-            float pv = __shfl_xor(hv, 16);
-            int pj = __shfl_xor(hj, 16);
-            if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
-            pv = __shfl_xor(hv, 32);
-            pj = __shfl_xor(hj, 32);
-            if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
-            const bool pop = li[0] == hj && lv[0] == hv;
-#pragma unroll
-            for (int t = 0; t < KL - 1; ++t) {
-                lv[t] = pop ? lv[t + 1] : lv[t];
-                li[t] = pop ? li[t + 1] : li[t];
-            }
-            lv[KL - 1] = pop ? -INFINITY : lv[KL - 1];
-            li[KL - 1] = pop ? 0x7fffffff : li[KL - 1];
-            if ((r & 3) == g) { ov[r >> 2] = hv; oj[r >> 2] = hj; }
-        }
-    }
-    __syncthreads();  // every wave is done with its FIFO and the query rows
-    float2* lists = reinterpret_cast<float2*>(smem);          // [KQ_HALVES][QPB][KB]
-    float* kth = smem + KQ_HALVES * QPB * KB * 2;             // [QPB] merged k-th value
-    int* flg = reinterpret_cast<int*>(kth + QPB);             // [QPB] row needs the fix-up
-#pragma unroll
-    for (int t = 0; t < RPL; ++t) {
-        const int r = 4 * t + g;
-        if (r < k) lists[(h * QPB + qq) * KB + r] = make_float2(ov[t], __int_as_float(oj[t]));
-    }
-    if (tid < QPB) {
-        kth[tid] = -INFINITY;
-        flg[tid] = 0;
-    }
-    __syncthreads();
-    {
-        const float2* other = lists + ((1 - h) * QPB + qq) * KB;
-#pragma unroll
-        for (int t = 0; t < RPL; ++t) {
-            const int r = 4 * t + g;
-            if (r < k) {
-                int lo = 0, hi = k;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    const float2 o = other[mid];
-                    if (canon_better(o.x, __float_as_int(o.y), ov[t], oj[t])) lo = mid + 1;
-                    else hi = mid;
-                }
-                rk[t] = r + lo;
-                if (rk[t] == k - 1) kth[qq] = ov[t];
-            }
-        }
-    }
-    __syncthreads();
-    {
-        const float kv = kth[qq];
-        // a full exact list reaching the k-th may have dropped a member; an
-        // overflowed FIFO dropped candidates; a non-finite bound admits nothing
-        if ((last != -INFINITY && last >= kv) || ovf) flg[qq] = 1;
-        if (!(eps < INFINITY)) flg[qq] = 1;
-    }
-    __syncthreads();
-#ifdef KNN_BF_DIAG
-    {   // diagnostics build: per row {flag reasons, eps, final bound, k-th, FIFO count} in vals, no fix-up
-        const float kv = kth[qq];
-        int why = ((last != -INFINITY && last >= kv) ? 1 : 0) | (ovf ? 2 : 0) | (!(eps < INFINITY) ? 4 : 0);
-        why |= __shfl_xor(why, 16) | __shfl_xor(why, 32);
-        const int cm = max(max(cnt, __shfl_xor(cnt, 16)), __shfl_xor(cnt, 32));
-        if (q < N && h == 0 && g == 0 && vals) {
-            float* vr = vals + ((int64_t)b * N + q) * k;
-            vr[0] = (float)why; vr[1] = eps; vr[2] = athr; vr[3] = kv; vr[4] = (float)cm;
-        }
-        return;
-    }
-#endif
-    if (q < N && flg[qq] == 0) {
-        const int64_t row = ((int64_t)b * N + q) * k;
-#pragma unroll
-        for (int t = 0; t < RPL; ++t) {
-            const int r = rk[t];
-            if (4 * t + g < k && r < k) {
-                if (idx64) idx64[row + r] = oj[t];
-                if (idx32) idx32[row + r] = oj[t];
-                if (vals) vals[row + r] = ov[t];
-            }
-        }
-    }
-    float* fixa = smem + KQ_HALVES * QPB * KB * 2 + 2 * QPB;
-    for (int f = 0; f < QPB; ++f) {
-        const int qf = qb * QPB + f;
-        if (KNN_BF_PROBE == 0 && flg[f] != 0 && qf < N)
-            knn_fix_row<NSTEP>(fixa, ib, xib, xxb, N, k, qf, kth[f], (int64_t)b * N + qf, idx64, idx32, vals);
-    }
-}
 
 // image floats per cloud, then |x|^2 image floats per cloud
 inline size_t knn_image_floats(int C, int N) { return (size_t)knn_ntile(N) * 64 * knn_nstep(C); }
@@ -1381,14 +961,6 @@ template <int NSTEP, int KB>
 int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* xx, int B, int C, int N,
                int k, int64_t* idx64, int32_t* idx32, float* vals, const float* img, const float* xximg,
                hipStream_t st) {
-    if constexpr (NSTEP >= 16) {
-        if (KNN_BF) {   // C > 32: bf16-filtered selection (exact refine)
-            const int nqb = (N + KQ_QPB - 1) / KQ_QPB;
-            hipLaunchKernelGGL((knn_bf_kernel<NSTEP, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS), 0, st,
-                               img, xximg, xx, B, N, k, nqb, idx64, idx32, vals);
-            return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
-        }
-    }
     // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
     // the lists of two groups fit in registers); one where the selection does
     if constexpr (KB <= 40 && NSTEP >= 16) {
@@ -1431,11 +1003,7 @@ const char* dgx_knn_kernel_name(int C, int k, int N) {
             for (int a = 0; a < 5; ++a)
                 for (int b = 0; b < 5; ++b)
                     for (int q = 0; q < 2; ++q)
-                        if (KNN_BF && NS[a] >= 16)
-                            snprintf(s[a][b][q], sizeof(s[a][b][q]), "knn_bf_kernel<%d, %d>", NS[a], KBS[b]);
-                        else
-                            snprintf(s[a][b][q], sizeof(s[a][b][q]), "knn_kernel<%d, %d, %d>", NS[a], KBS[b],
-                                     q + 1);
+                        snprintf(s[a][b][q], sizeof(s[a][b][q]), "knn_kernel<%d, %d, %d>", NS[a], KBS[b], q + 1);
         }
     };
     static const Names names;  // thread-safe one-time initialisation
