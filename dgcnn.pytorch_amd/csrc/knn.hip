@@ -944,6 +944,13 @@ inline int knn_qg(int nstep, int kb, int N) {
     return 1;
 }
 
+// Grids of fewer than 512 workgroups at 32 queries per workgroup (few clouds:
+// a strong-scaling shard) keep one query group per wave at C = 128 too: the
+// two-group kernel would leave three quarters of the CUs idle (4 clouds: C = 128
+// selection 93 -> 66 us, r05b). Splitting each group's candidates over four
+// waves instead (knn_split_kernel, r05a/b) measured slower at every C.
+inline bool knn_small(int B, int N) { return (int64_t)B * ((N + KQ_QPB - 1) / KQ_QPB) < 512; }
+
 template <int NSTEP, int KB, int QG>
 int launch_knn_qg(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* idx32, float* vals,
                   const float* img, const float* xximg, hipStream_t st) {
@@ -964,8 +971,8 @@ int launch_knn(const float* x, int64_t sB, int64_t sC, int64_t sN, const float* 
     // two query groups per wave where the MFMA chain dominates (C > 64, k <= 40:
     // the lists of two groups fit in registers); one where the selection does
     if constexpr (KB <= 40 && NSTEP >= 16) {
-        if (knn_qg(NSTEP, KB, N) == 2) return launch_knn_qg<NSTEP, KB, 2>(xx, B, N, k, idx64, idx32, vals, img, xximg,
-                                                                          st);
+        if (knn_qg(NSTEP, KB, N) == 2 && !knn_small(B, N))
+            return launch_knn_qg<NSTEP, KB, 2>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
     }
     return launch_knn_qg<NSTEP, KB, 1>(xx, B, N, k, idx64, idx32, vals, img, xximg, st);
 }
@@ -994,7 +1001,8 @@ void dgx_knn_stats_buffer(void* dev) { g_knn_stats = static_cast<uint32_t*>(dev)
 #endif
 
 const char* dgx_knn_kernel_name(int C, int k, int N) {
-    // the selection kernel dgx_knn_select_f32 launches for (C, k, N), as profilers print it
+    // the selection kernel dgx_knn_select_f32 launches for (C, k, N) on grids of at least
+    // 512 workgroups (knn_small: fewer clouds keep one query group per wave), as profilers print it
     struct Names {
         char s[5][5][2][40];
         Names() {

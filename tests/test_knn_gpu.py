@@ -85,11 +85,13 @@ def test_knn_full_size_hashes(cuda):
             assert hashlib.sha256(idx.astype(np.int32).tobytes()).hexdigest() == h["idx_sha256"], name
 
 
-def test_knn_feature_space_sizes(cuda):
-    """Feature-space kNN shapes of DGCNN blocks 2-4 (C=64/128, contiguous) at cfg2 N."""
+@pytest.mark.parametrize("B", [4, 16])
+def test_knn_feature_space_sizes(cuda, B):
+    """Feature-space kNN shapes of DGCNN blocks 2-4 (C=64/128, contiguous) at cfg2 N;
+    4 clouds keep one query group per wave at C = 128 (knn_small), 16 take two."""
     from models.dgcnn import knn
     for C in (64, 128):
-        pts = synth.relu_normal(3 + C, (4, 1024, C))
+        pts = synth.relu_normal(3 + C + B, (B, 1024, C))
         idx = knn(_view(pts, "bcn", cuda), 20).cpu().numpy()
         np.testing.assert_array_equal(idx, oracle.knn(_cpu_view(pts, "bcn"), 20))
 
