@@ -459,13 +459,18 @@ def make_input(args, clouds, seed):
     return synth.cube_clouds(clouds, args.points, seed=seed)
 
 
-def pmc_traffic(args, shapes):
+def pmc_traffic(args, shapes, per_gpu):
     """HBM bytes per kNN selection launch from the committed rocprofv3 PMC
     summary of this config (profiles/*_pmc_<config>.json, newest round first),
     averaged over this step's launches. Returns (bytes or None, note): a file
     whose kernel names do not include every selection kernel this build
     launches for the step's layers is refused."""
     from dgx import _native as nat
+    pb, pn, pk, _ = PRESETS[args.config]
+    if (per_gpu, args.points, args.k) != (pb, pn, pk):
+        # the committed counters are per launch of the preset's shapes; other
+        # batch sizes launch other grids (and, for few clouds, other kernels)
+        return None, f"no PMC profile for B={per_gpu} N={args.points} k={args.k} (committed: {args.config} preset)"
     names = [nat.lib().dgx_knn_kernel_name(c, args.k, args.points).decode() for c in shapes]
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{args.config}.json")), reverse=True)
     if not files:
@@ -658,7 +663,7 @@ def main():
             per_layer.setdefault(f"C{shape[1]}", []).append(ms)
         per_layer = {c: round(sum(v) / len(v), 4) for c, v in per_layer.items()}
         shapes = [s[1] for (_, _, _, s) in timing[:4]]
-        traffic, tnote = pmc_traffic(args, shapes)
+        traffic, tnote = pmc_traffic(args, shapes, per_gpu)
         result["roofline"] = {
             "kernel": "knn_kernel (fused fp32 Gram on MFMA + top-k selection)", "bound": "mfma",
             "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
