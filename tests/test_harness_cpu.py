@@ -127,3 +127,14 @@ def test_color_palettes_as_scripts_read_them(monkeypatch, tmp_path):
     sc = data.S3DIS(4096, "test").semseg_colors
     assert pc.shape == (50, 3) and sc.shape == (13, 3)
     assert pc.min() >= 0 and pc.max() <= 255 and tuple(pc[0]) == (152, 223, 138) and tuple(sc[12]) == (112, 128, 144)
+
+
+def test_bench_pmc_traffic_only_for_preset_shapes():
+    """bench.py's roofline `traffic` comes from committed PMC counters of the
+    preset's launches; another batch size launches other grids (and, for few
+    clouds, another kNN kernel), so the lookup refuses it."""
+    import types
+    import bench
+    args = types.SimpleNamespace(config="cfg2", points=1024, k=20, batch=4)
+    traffic, note = bench.pmc_traffic(args, [3, 64, 64, 128], 4)
+    assert traffic is None and "no PMC profile for B=4" in note
