@@ -575,11 +575,29 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # the same step with every launch issued from Python (autograd + ctypes):
-    # ~60 launches per step, so a slow or contended host can starve the GPU
+    # the same step launched eagerly (one C++ op + C++ autograd node issue the
+    # ~60 launches of a step: dgx.host)
     elapsed_eager = reduce_elapsed(timed_region(step, args.steps, world), world, dev)
     launch = "eager"
     run = step
+    elapsed_amp = None
+    if world == 1:
+        # the reference's own training configuration (main_partseg_dist.py:253): the
+        # eager step under fp16 autocast with the engine's global mode at fp32 — the
+        # GEMMs follow autocast to the bf16 path (dgx.precision.effective), issued
+        # through the one-op C++ layer
+        dgx_prec.set("fp32")
+
+        def amp_step():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.float16):
+                y = net(x)
+            y.backward(gy)
+            opt.step()
+        for _ in range(3):
+            amp_step()
+        elapsed_amp = timed_region(amp_step, args.steps, world)
+        dgx_prec.set(args.precision)
     if world == 1 and not args.no_graph:
         # one HIP graph per train step (fwd + bwd + SGD, the same kernels and
         # buffers as the eager step, captured once): replay issues the whole step
@@ -632,6 +650,8 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "launch": launch,
         "eager_launch_ms_per_step": round(elapsed_eager / args.steps * 1e3, 3),
+        "autocast_eager_ms_per_step": (round(elapsed_amp / args.steps * 1e3, 3) if elapsed_amp is not None
+                                       else None),
         "replicas_in_sync": replicas_in_sync(model, world, dev),
         "higher_is_better": True,
         "scaling": args.scaling,

@@ -35,6 +35,23 @@ def mode(bn):
     return use_batch, update
 
 
+def op_args(bn):
+    """One BN layer's arguments for the C++ schedule (libdgx_torch.so,
+    dgx_host::chain_* / pointconv_* / dgcnn): ([running_mean, running_var,
+    num_batches_tracked, and the three update targets of a functional caller
+    (``bn.stats_out``) or None for in place], [momentum (-1 = None), eps],
+    [training, track_running_stats], SyncBatchNorm process-group name or "").
+    The C++ side takes every decision of ``mode`` / ``batch_stats`` /
+    ``running_stats`` / ``backward_consts`` from these, as nn.BatchNorm does."""
+    out = getattr(bn, "stats_out", None)
+    rm_o, rv_o, nb_o = out if out is not None else (None, None, None)
+    sync, group = dist_.sync_group(bn)
+    return ([bn.running_mean, bn.running_var, bn.num_batches_tracked, rm_o, rv_o, nb_o],
+            [-1.0 if bn.momentum is None else float(bn.momentum), float(bn.eps)],
+            [int(bool(bn.training)), int(bool(bn.track_running_stats))],
+            group.group_name if sync else "")
+
+
 def _factor(bn):
     """(exponential-average factor nn.BatchNorm uses this step, num_batches_tracked
     tensor for the finalize kernel to increment or None). With a momentum the

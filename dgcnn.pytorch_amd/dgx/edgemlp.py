@@ -58,7 +58,13 @@ def _capture(idx, PQ, st1, st2, ysel, arg, bf16, fused):
 class _EdgeMLP2(torch.autograd.Function):
     @staticmethod
     @prec.no_autocast
-    def forward(ctx, x, k, bn1, bn2, slope1, slope2, need_grad, knn_src, w1, g1, b1, w2, g2, b2):
+    def forward(ctx, x, k, bn1, bn2, slope1, slope2, need_grad, knn_src, bf16, w1, g1, b1, w2, g2, b2):
+        # the GEMM precision the caller's entry resolved (precision.effective: bf16 mode or autocast)
+        with prec.mode("bf16" if bf16 else "fp32"):
+            return _EdgeMLP2._forward(ctx, x, k, bn1, bn2, slope1, slope2, need_grad, knn_src, w1, g1, b1, w2, g2, b2)
+
+    @staticmethod
+    def _forward(ctx, x, k, bn1, bn2, slope1, slope2, need_grad, knn_src, w1, g1, b1, w2, g2, b2):
         x = x.float()
         dev = x.device
         B, C, N = x.shape
@@ -171,6 +177,12 @@ class _EdgeMLP2(torch.autograd.Function):
     @staticmethod
     @prec.no_autocast
     def backward(ctx, dout):
+        with prec.mode("bf16" if ctx.bf16 else "fp32"):
+            grads = _EdgeMLP2._backward(ctx, dout)
+        return grads[:8] + (None,) + tuple(grads[8:])
+
+    @staticmethod
+    def _backward(ctx, dout):
         st1, st2 = ctx.st
         X, idx, PQ, sumP1, H1, Z2, ysel, arg, w1, w2 = ctx.saved_tensors
         B, C, N, k, C1, C2 = ctx.dims
@@ -321,4 +333,6 @@ def edge_mlp2(x, k, conv1, conv2, training=None, knn_src=None):
         knn_src = knn_src.detach()
         if knn_src.shape[0] != x.shape[0] or knn_src.shape[2] != x.shape[2]:
             raise RuntimeError("dgx edge MLP: knn_src must be (B, C', N) with the input's B and N")
-    return _EdgeMLP2.apply(x, k, bn1, bn2, act1.negative_slope, act2.negative_slope, need_grad, knn_src, *params)
+    bf16 = prec.effective() == "bf16"
+    return _EdgeMLP2.apply(x, k, bn1, bn2, act1.negative_slope, act2.negative_slope, need_grad, knn_src, bf16,
+                           *params)

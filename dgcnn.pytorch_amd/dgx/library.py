@@ -22,11 +22,12 @@ The ops are functional: BatchNorm running statistics come back as outputs (the
 finalize kernels read the module buffers and write the new values straight
 into the outputs: no private copy first) and the caller copies them into the
 module buffers (what a compiled graph does with a buffer mutation anyway;
-torch does not allow an autograd formula on an op that mutates its inputs). Each op's device kernel runs the same code as the
-engine's autograd Functions (dgx.edgeconv, dgx.pointconv), so eager results
-are identical either way; ``models.dgcnn.DGCNN`` takes this path unless a
-BatchNorm is a SyncBatchNorm (process groups cannot cross the op boundary) —
-then the Function path runs, with its collectives.
+torch does not allow an autograd formula on an op that mutates its inputs).
+The chain and conv5 ops run the C++ schedule (libdgx_torch.so,
+dgx_host::chain_* / pointconv_*) that the eager DGCNN op and the engine's
+autograd Functions run too, so eager results are identical either way;
+``models.dgcnn.DGCNN`` takes this path while torch.compile traces it, unless a
+BatchNorm is a SyncBatchNorm (process groups cannot cross the op boundary).
 """
 from typing import Optional
 
@@ -38,7 +39,6 @@ from . import cpu
 from . import edgeconv as E
 from . import gemm as G
 from . import ops
-from . import pointconv as PC
 from . import precision as prec
 
 ENABLED = True
@@ -265,20 +265,8 @@ def _dgcnn_prep_shapes(weights5):
 _PER_LAYER = 9   # idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd
 
 
-def _chain_prep_shapes(weights):
-    """(rows, cols, stacked, split) of blocks 2..n's bf16 copies (split, stacked)."""
-    return [(w.shape[0], w.shape[1] // 2, True, True) for w in weights[1:]]
-
-
 def _chain_layers(weights, specs, slopes):
     return [E._Layer(w.shape[1] // 2, w.shape[0], s, sl) for w, s, sl in zip(weights, specs, slopes)]
-
-
-def _chain_prep_used(li, bf16, selecting, cin):
-    """Whether block li's GEMMs take the bf16 weight copies (dgx.edgeconv:
-    its input is the bf16 twin written by a selecting block and the operand
-    qualifies for the LDS-DMA path)."""
-    return bf16 and li > 0 and selecting[li - 1] and cin % 64 == 0
 
 
 @torch.library.custom_op("dgx::edgeconv_chain", mutates_args=(), device_types="cuda")
@@ -287,34 +275,28 @@ def edgeconv_chain(x: Tensor, k: int, weights: list[Tensor], gammas: list[Tensor
                    track: list[bool], momentum: list[float], eps: list[float], slopes: list[float], bf16: bool,
                    need_grad: bool, prep: Optional[Tensor]) -> tuple[Tensor, Tensor, list[Tensor], list[Tensor],
                                                                      list[Tensor], list[Tensor]]:
-    """DGCNN's EdgeConv blocks (dgcnn.py:84-100) as dgx.edgeconv runs them:
-    returns (concat buffer (B*N, sum Co), its bf16 twin or empty, updated
-    running means / vars / batch counters, the state the backward reads)."""
+    """DGCNN's EdgeConv blocks (dgcnn.py:84-100) on the C++ schedule
+    (dgx_host::chain_forward): returns (concat buffer (B*N, sum Co), its bf16
+    twin or empty, updated running means / vars / batch counters, the state the
+    backward reads)."""
+    from . import host
+    host.load()
     outs = _stat_outputs(training, track, running_means, running_vars, nbts)
     rms, rvs, nbs = [o[0] for o in outs], [o[1] for o in outs], [o[2] for o in outs]
     specs = [_BNSpec(*a, out=o) for a, o in zip(zip(training, track, running_means, running_vars, nbts, momentum, eps),
                                                   outs)]
-    layers = _chain_layers(weights, specs, slopes)
-    params = [t for trip in zip(weights, gammas, betas) for t in trip]
-    preps = None
-    if prep is not None:   # blocks 2.. : the first entries of the shared bf16 buffer (dgcnn_forward)
-        preps = [None] + G.prep_views(prep, _chain_prep_shapes(weights))
-    rec = _Rec()
-    with prec.mode("bf16" if bf16 else "fp32"):
-        xcat, xcat16 = E._EdgeConvStack.forward(rec, x, k, layers, preps, need_grad, *params)
-    x_pm = rec.saved_tensors[0]
+    bn_t, bn_f, bn_i, groups, sl = E._bn_lists(_chain_layers(weights, specs, slopes))
+    idx0 = None
+    if getattr(ops._tls, "cache", None) is not None:
+        idx0 = ops.knn_raw(x.detach().float(), k, order=ops.reduction_order(x), out_dtype=_I32)
+    xcat, xcat16, saved, _ = torch.ops.dgx_host.chain_forward(
+        x.float(), k, weights, gammas, betas, bn_t, bn_f, bn_i, groups, sl, bf16, need_grad, prep, idx0, E.opts())
+    saved = list(saved)
+    x_pm = saved[0]
     if x_pm.untyped_storage().data_ptr() == x.untyped_storage().data_ptr():
-        x_pm = x_pm.clone()
-    saved = [x_pm]
-    selecting = [s is not None for s in rec.layer_state]
-    for li, st in enumerate(rec.layer_state):
-        if st is None:   # distinct placeholders: op outputs may not alias each other
-            saved += [_empty(x.device) for _ in range(_PER_LAYER)]
-            continue
-        idx, PQ, ysel, arg, sumP, stats, wprep = st
-        if (wprep is not None) != _chain_prep_used(li, bf16, selecting, layers[li].cin):
-            raise RuntimeError("dgx::edgeconv_chain: bf16 operand-copy use differs from its static rule")
-        saved += [idx, PQ, ysel, arg, sumP, stats.scale, stats.shift, stats.mean, stats.invstd]
+        saved[0] = x_pm.clone()
+    if idx0 is not None and saved[1].data_ptr() == idx0.data_ptr():
+        saved[1] = idx0.clone()   # a cache entry: never alias it
     return xcat, xcat16, rms, rvs, nbs, saved
 
 
@@ -346,30 +328,11 @@ def edgeconv_chain_backward(dxcat: Tensor, x: Tensor, xcat: Tensor, xcat16: Tens
                             k: int, use_batch: list[bool], slopes: list[float], bf16: bool,
                             x_needs_grad: bool) -> tuple[Tensor, list[Tensor], list[Tensor], list[Tensor]]:
     B, C0, N = x.shape
-    rec = _Rec()
-    params = [t for trip in zip(weights, gammas, betas) for t in trip]
-    rec.saved_tensors = (saved[0], xcat, xcat16 if xcat16.numel() else None, *params)
-    rec.k, rec.shape, rec.bf16, rec.x_needs_grad = k, (B, C0, N), bf16, x_needs_grad
-    rec.layers = _chain_layers(weights, [None] * len(weights), slopes)
-    preps = [None] * len(weights)
-    if prep is not None:
-        preps = [None] + G.prep_views(prep, _chain_prep_shapes(weights))
-    state, selecting = [], []
-    for li in range(len(weights)):
-        t = saved[1 + _PER_LAYER * li: 1 + _PER_LAYER * (li + 1)]
-        sel = t[0].numel() > 0
-        selecting.append(sel)
-        if not sel:
-            raise RuntimeError("dgx::edgeconv_chain_backward: a block ran without its backward state")
-        stats = bn_.Stats(t[5], t[6], t[7], t[8], None, not use_batch[li])
-        wprep = preps[li] if _chain_prep_used(li, bf16, selecting, rec.layers[li].cin) else None
-        state.append((t[0], t[1], t[2], t[3], t[4], stats, wprep))
-    rec.layer_state = state
-    with prec.mode("bf16" if bf16 else "fp32"):
-        res = E._EdgeConvStack.backward(rec, dxcat, None)
-    dx = res[0].contiguous() if res[0] is not None else _empty(x.device)
-    grads = res[5:]
-    return dx, [g.contiguous() for g in grads[0::3]], list(grads[1::3]), list(grads[2::3])
+    dx, dws, dgs, dbs = torch.ops.dgx_host.chain_backward(
+        dxcat, xcat, xcat16, saved, weights, prep, [B, C0, N], k, [int(not u) for u in use_batch],
+        [""] * len(weights), slopes, bf16, x_needs_grad, E.opts())
+    dx = dx.contiguous() if dx.numel() else _empty(x.device)
+    return dx, [g.contiguous() for g in dws], list(dgs), list(dbs)
 
 
 @edgeconv_chain_backward.register_fake
@@ -417,27 +380,31 @@ def _pc_lds(bf16, X16, K):
     return bf16 and X16.numel() > 0 and K % 64 == 0
 
 
+def _pc_prep(prep, Co, K):
+    """conv5's (nt, tn) bf16 views of a weight-prep buffer, or (None, None)."""
+    if prep is not None and prep.numel() == 2 * Co * K:
+        return G.prep_views(prep, [(Co, K, False, False)])[0]
+    return None, None
+
+
 @torch.library.custom_op("dgx::pointconv", mutates_args=(), device_types="cuda")
 def pointconv(X: Tensor, X16: Tensor, B: int, N: int, weight: Tensor, gamma: Tensor, beta: Tensor,
               running_mean: Tensor, running_var: Tensor, nbt: Tensor, training: bool, track: bool, momentum: float,
               eps: float, slope: float, bf16: bool, prep: Optional[Tensor]) -> tuple[Tensor, Tensor, Tensor, Tensor,
                                                                                     list[Tensor]]:
-    """conv5 -> BN -> LeakyReLU on the concat buffer (dgcnn.py:100-102) as
-    dgx.pointconv runs it: (out (B, Co, N), updated running mean / var /
-    batch counter, saved state [Z, scale, shift, mean, invstd])."""
+    """conv5 -> BN -> LeakyReLU on the concat buffer (dgcnn.py:100-102) on the
+    C++ schedule (dgx_host::pointconv_forward): (out (B, Co, N), updated
+    running mean / var / batch counter, saved state [Z, scale, shift, mean,
+    invstd])."""
+    from . import host
+    host.load()
     (rm, rv, nb), = _stat_outputs([training], [track], [running_mean], [running_var], [nbt])
     spec = _BNSpec(training, track, running_mean, running_var, nbt, momentum, eps, out=(rm, rv, nb))
-    wprep = None
-    if prep is not None:
-        Co, K = weight.shape[0], weight.shape[1]
-        wprep = G.prep_views(prep, [(Co, K, False, False)])[0] if prep.numel() == 2 * Co * K else None
-    rec = _Rec()
-    with prec.mode("bf16" if bf16 else "fp32"):
-        out = PC._PointConvBNLReLU.forward(rec, X, X16 if X16.numel() else None, B, N, spec, slope, wprep, weight,
-                                           gamma, beta)
-    Z = rec.saved_tensors[2]
-    st = rec.st
-    return out, rm, rv, nb, [Z, st.scale, st.shift, st.mean, st.invstd]
+    t, f, i, g = bn_.op_args(spec)
+    nt, tn = _pc_prep(prep, weight.shape[0], weight.shape[1])
+    out, saved = torch.ops.dgx_host.pointconv_forward(X.float(), X16, B, N, weight, gamma, beta, t, f + [float(slope)],
+                                                      i, g, bf16, nt, tn)
+    return out, rm, rv, nb, list(saved[1:6])
 
 
 @pointconv.register_fake
@@ -455,22 +422,16 @@ def _(X, X16, B, N, weight, gamma, beta, running_mean, running_var, nbt, trainin
 def pointconv_backward(dout: Tensor, X: Tensor, X16: Tensor, weight: Tensor, saved: list[Tensor],
                        prep: Optional[Tensor], B: int, N: int, slope: float, bf16: bool,
                        use_batch: bool) -> tuple[Tensor, Tensor, Tensor, Tensor]:
-    Z, scale, shift, mean, invstd = saved
     M, K = X.shape
     Co = weight.shape[0]
     lds = _pc_lds(bf16, X16, K)
-    rec = _Rec()
-    rec.saved_tensors = (X16 if lds else X, weight.reshape(Co, K), Z)
-    rec.st = bn_.Stats(scale, shift, mean, invstd, None, not use_batch)
-    rec.meta = (B, N, float(slope), bf16)
-    rec.wprep = None
-    if lds:
-        rec.wprep = (G.prep_views(prep, [(Co, K, False, False)])[0] if prep is not None and prep.numel() == 2 * Co * K
-                     else G.prep_weight(weight, Co, K, False))
-    rec.wshape = weight.shape
-    with prec.mode("bf16" if bf16 else "fp32"):
-        res = PC._PointConvBNLReLU.backward(rec, dout)
-    return res[0].contiguous(), res[7].contiguous(), res[8], res[9]
+    e16 = torch.empty(0, dtype=_BF16, device=X.device)
+    nt, tn = (_pc_prep(prep, Co, K) if lds else (None, None))
+    if lds and nt is None:
+        nt, tn = G.prep_weight(weight, Co, K, False)
+    full = [X16 if lds else X.float(), *saved, nt if lds else e16, tn if lds else e16]
+    dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, full, weight, B, N, slope, not use_batch, "", bf16)
+    return dX.contiguous(), dW.contiguous(), dg, db
 
 
 @pointconv_backward.register_fake
@@ -529,8 +490,8 @@ def _store_bn(pairs):
 
 
 def enabled_for(model):
-    """The op path serves a model whose BatchNorms are plain nn.BatchNorm
-    (SyncBatchNorm needs its process group inside the op)."""
+    """The op path (torch.compile / export) serves a model whose BatchNorms are
+    plain nn.BatchNorm (a process group cannot cross a traced op's boundary)."""
     return ENABLED and not any(isinstance(m, torch.nn.SyncBatchNorm) for m in model.modules())
 
 
@@ -540,7 +501,7 @@ def dgcnn_forward(model, x):
     B, _, N = x.shape
     x = x.float()
     dev = x.device
-    bf16 = prec.get() == "bf16"
+    bf16 = prec.effective() == "bf16"
     blocks = model.edge_blocks()
     convs = [b[0] for b in blocks]
     bns = [b[1] for b in blocks]
@@ -601,8 +562,8 @@ def edge_mlp2(x: Tensor, k: int, w1: Tensor, g1: Tensor, b1: Tensor, rm1: Tensor
     outs = _stat_outputs(training, track, [rm1, rm2], [rv1, rv2], [nbt1, nbt2])
     s1, s2 = _emlp_specs(training, track, [rm1, rm2], [rv1, rv2], [nbt1, nbt2], momentum, eps, outs)
     with prec.mode("bf16" if bf16 else "fp32"):
-        out = EM._EdgeMLP2.forward(_Rec(), x, k, s1, s2, slopes[0], slopes[1], False, knn_src, w1, g1, b1, w2, g2,
-                                   b2)
+        out = EM._EdgeMLP2.forward(_Rec(), x, k, s1, s2, slopes[0], slopes[1], False, knn_src, bf16, w1, g1, b1, w2,
+                                   g2, b2)
     (a1, a2, a3), (c1, c2, c3) = outs
     return out, a1, a2, a3, c1, c2, c3
 
@@ -628,11 +589,11 @@ def edge_mlp2_backward(dout: Tensor, x: Tensor, k: int, w1: Tensor, g1: Tensor, 
     rec = _Rec()
     rec.needs_input_grad = (x_needs_grad,) + (True,) * 63
     with prec.mode("bf16" if bf16 else "fp32"):
-        EM._EdgeMLP2.forward(rec, x, k, specs[0], specs[1], slopes[0], slopes[1], True, knn_src, w1, g1, b1, w2, g2,
-                             b2)
+        EM._EdgeMLP2.forward(rec, x, k, specs[0], specs[1], slopes[0], slopes[1], True, knn_src, bf16, w1, g1, b1,
+                             w2, g2, b2)
         res = EM._EdgeMLP2.backward(rec, dout)
     dx = res[0].contiguous() if res[0] is not None else _empty(x.device)
-    gw1, dg1, db1, gw2, dg2, db2 = res[8:14]
+    gw1, dg1, db1, gw2, dg2, db2 = res[9:15]
     return dx, gw1.contiguous(), dg1, db1, gw2.contiguous(), dg2, db2
 
 
@@ -687,7 +648,7 @@ def edge_mlp2_call(x, k, conv1, conv2, knn_src=None):
     out, rm1, rv1, nb1, rm2, rv2, nb2 = torch.ops.dgx.edge_mlp2(
         x.float(), k, cv1.weight, bn1.weight, bn1.bias, a1[0], a1[1], a1[2], cv2.weight, bn2.weight, bn2.bias, a2[0],
         a2[1], a2[2], [a1[3], a2[3]], [a1[4], a2[4]], [a1[5], a2[5]], [a1[6], a2[6]],
-        [float(act1.negative_slope), float(act2.negative_slope)], prec.get() == "bf16",
+        [float(act1.negative_slope), float(act2.negative_slope)], prec.effective() == "bf16",
         None if knn_src is None else knn_src.detach().float())
     _store_bn([(bn1, rm1, rv1, nb1), (bn2, rm2, rv2, nb2)])
     return out

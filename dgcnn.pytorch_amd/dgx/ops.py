@@ -157,10 +157,32 @@ def knn_cache():
         _tls.cache = prev
 
 
+class _Elapsed:
+    """An already-measured launch (C++ HIP events), shaped like the
+    (start_event, end_event) pair: start.elapsed_time(end) -> ms."""
+
+    def __init__(self, ms):
+        self.ms = ms
+
+    def elapsed_time(self, _end):
+        return self.ms
+
+
 def set_knn_timing(lst):
-    """Optional per-thread instrumentation (tools): when a list, every kNN
-    selection launch of this thread appends (start_event, end_event,
-    gram_flops, shape) recorded on the launch stream."""
+    """Optional per-thread instrumentation (tools, bench.py's roofline leg):
+    when a list, every kNN selection launch of this thread appends
+    (start_event, end_event, gram_flops, shape) recorded on the launch stream —
+    the Python dispatch's launches as they run, the C++ schedule's
+    (libdgx_torch.so) when the timing is switched off again (set_knn_timing(None))."""
+    prev = getattr(_tls, "timing", None)
+    from . import host
+    if lst is not None:
+        host.load()
+        torch.ops.dgx_host.knn_timing(True)
+    elif prev is not None:
+        v = torch.ops.dgx_host.knn_timing(False)
+        for j in range(0, len(v), 6):
+            prev.append((_Elapsed(v[j]), None, v[j + 1], (int(v[j + 2]), int(v[j + 3]), int(v[j + 4]), int(v[j + 5]))))
     _tls.timing = lst
 
 

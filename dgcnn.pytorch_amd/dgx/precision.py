@@ -11,6 +11,16 @@ elementwise stage stay fp32 either way.
 
 Set with ``dgx.precision.set("bf16")`` or the environment variable
 ``DGX_PRECISION=bf16``.
+
+Autocast rule ("kNN upcasts to fp32, GEMMs follow autocast
+dtype"): under ``torch.autocast("cuda", dtype=float16|bfloat16)`` — the
+reference's training loop, main_partseg_dist.py:221, 253 — the engine's GEMMs
+take their reduced-precision path, whatever the global mode says
+(``effective()``). The engine's reduced-precision kernels are bf16 MFMA
+(gfx950's 16-bit MFMA rate is the same for fp16 and bf16; bf16 keeps fp32's
+exponent range, so no loss scaling is needed inside the fused chain); fp16
+autocast therefore routes to them too. kNN, BN statistics and every
+elementwise stage stay fp32, as autocast keeps them in the reference.
 """
 import contextlib
 import functools
@@ -25,6 +35,18 @@ if _mode not in ("fp32", "bf16"):
 
 def get():
     return _mode
+
+
+def autocast_reduced():
+    """Whether CUDA autocast to fp16 / bf16 is active on this thread."""
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") in (torch.float16, torch.bfloat16)
+
+
+def effective():
+    """The GEMM precision an engine op entered now computes in: "bf16" in the
+    bf16 mode or under fp16/bf16 autocast, else "fp32". Read at the op's
+    entry (the engine's autograd Functions run with autocast disabled)."""
+    return "bf16" if (_mode == "bf16" or autocast_reduced()) else "fp32"
 
 
 def set(mode):  # noqa: A001 (mirrors get)
@@ -69,8 +91,9 @@ def no_autocast(fn):
     The reference's DDP script runs the model under torch.cuda.amp.autocast
     (main_partseg_dist.py:253). Inside the engine's Functions every product
     must come back in the dtype its consumer kernel is built for, so autocast
-    must not re-type a torch.mm there; the engine computes in its own
-    precision mode instead, on fp32 inputs (each Function casts its input)."""
+    must not re-type a torch.mm there; each op computes in the precision
+    ``effective()`` gave at its entry, on fp32 inputs (each Function casts its
+    input)."""
     @functools.wraps(fn)
     def wrapped(*args, **kwargs):
         if torch.is_autocast_enabled("cuda"):

@@ -15,11 +15,9 @@ unchanged. The work runs in libdgx.so on the MI355X:
 import torch
 import torch.nn as nn
 
-from dgx import gemm as _gemm
 from dgx import host as _host
 from dgx import library as _library
 from dgx import ops as _ops
-from dgx import precision as _prec
 from dgx.edgeconv import edgeconv_stack_pair
 from dgx.pointconv import pointconv_bn_lrelu
 
@@ -50,23 +48,6 @@ def _diff_weight(w):
     module's gradient follows by autograd)."""
     c = w.shape[1] // 2
     return torch.cat([w[:, :c], w[:, c:] - w[:, :c]], dim=1)
-
-
-def _bf16_weight_copies(model):
-    """bf16 operand copies ([W1;W2] / W and transposes) of conv2..conv5 for the
-    engine's bf16 GEMMs, all in one launch per step (precision "bf16" only)."""
-    if _prec.get() != "bf16":
-        return None
-    jobs = []
-    for w in model.edge_weights()[1:]:
-        # EdgeConv weights in the split (hi + lo) form: BN normalises edge values
-        # y = P_j + Q_i whose batch spread is small next to their size, so the
-        # weights' bf16 rounding is the largest error term the blocks can shed cheaply
-        jobs.append((w, w.shape[0], w.shape[1] // 2, True, True))
-    w5 = model.conv5[0].weight
-    jobs.append((w5, w5.shape[0], w5.shape[1], False))
-    out = _gemm.prep_weights(jobs)
-    return [None] + out
 
 
 class DGCNN(nn.Module):
@@ -111,18 +92,16 @@ class DGCNN(nn.Module):
             # CPU path of every block (dgx.cpu), same modules and state
             feats, _ = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training, weights=self.edge_weights())
             return pointconv_bn_lrelu(feats, x.shape[0], x.shape[2], self.conv5, self.training)
-        if _host.applies(self, x):
-            # train step of the reference's scripts: one C++ op + C++ autograd node (libdgx_torch.so)
-            return _host.dgcnn_train(self, x)
-        if _library.enabled_for(self):
-            # the same kernels behind torch.ops.dgx custom ops (torch.compile / export see one node each)
+        if torch.compiler.is_compiling() and _library.enabled_for(self):
+            # the same schedule behind torch.ops.dgx custom ops (torch.compile / export see one node each)
             return _library.dgcnn_forward(self, x)
+        if _host.applies(self, x):
+            # one C++ op + C++ autograd node (libdgx_torch.so), every precision / BN mode
+            return _host.dgcnn_forward(self, x)
         batch_size, _, num_points = x.size()
-        preps = _bf16_weight_copies(self) if self.training else None
+        # the autograd Functions over the same C++ schedule (debug capture, DGX_HOST_EXT=0):
         # x1..x4 of dgcnn.py:84-98, already concatenated point-major (dgcnn.py:100)
         feats, feats16 = edgeconv_stack_pair(x, self.k, self.edge_blocks(), self.training,
-                                             preps=None if preps is None else preps[:4],
                                              weights=self.edge_weights())   # (B*N, 512)
         # conv5 -> BN -> LeakyReLU (dgcnn.py:100-102), written as (B, emb, N)
-        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training, X16=feats16,
-                                  wprep=None if preps is None else preps[4])
+        return pointconv_bn_lrelu(feats, batch_size, num_points, self.conv5, self.training, X16=feats16)

@@ -24,6 +24,8 @@ def main():
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     posemb = mode.startswith("posemb")
+    if mode == "net_syncbn_amp":
+        return net_syncbn_amp(rank, world, out_dir, dev)
     if posemb:  # PositionEmbedding (a6) as main_partseg_dist.py converts Net's modules
         model = PositionEmbedding(types.SimpleNamespace(k=10))
         with torch.no_grad():
@@ -44,6 +46,47 @@ def main():
     torch.cuda.synchronize()
     res = {"y": y.detach().cpu(),
            "grads": {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None},
+           "running": {n: b.detach().cpu() for n, b in model.named_buffers()}}
+    torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+NET_ARGS = dict(k=40, emb_dim=512, n_heads=4, n_blocks=1, ff_dims=512, dropout=0.0, nclasses=50)
+NET_B, NET_N = 2, 2048   # clouds per rank, points (BASELINE cfg4 geometry, batch reduced)
+
+
+def net_inputs(world):
+    from dgx import synth
+    pts = synth.cube_clouds(NET_B * world, NET_N, 31)
+    lbl = torch.nn.functional.one_hot(torch.arange(NET_B * world) % 16, 16).float()
+    g = torch.from_numpy(synth.uniform(32, (NET_B * world, NET_N, NET_ARGS["nclasses"])) - 0.5).float()
+    return pts, lbl, g
+
+
+def net_syncbn_amp(rank, world, out_dir, dev):
+    """Net as main_partseg_dist.py:189-196, 253-260 trains it: converted with
+    SyncBatchNorm, wrapped in DDP, forward under fp16 autocast, GradScaler-scaled
+    backward. The engine's DGCNN (one C++ op) all-reduces its BN statistics
+    over the module's process group from C++."""
+    from models.model_partseg import Net
+    # both ranks share cuda:0; compute_hog_1x1 moves its histograms to device
+    # LOCAL_RANK as the reference does (model_partseg.py:66-73)
+    os.environ["LOCAL_RANK"] = "0"
+    torch.manual_seed(0)
+    model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(Net(types.SimpleNamespace(**NET_ARGS))).to(dev).train()
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
+    pts, lbl, g = net_inputs(world)
+    sl = slice(rank * NET_B, (rank + 1) * NET_B)
+    x = torch.from_numpy(pts[sl]).to(dev).permute(0, 2, 1).contiguous()
+    scale = 1024.0
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = ddp(x, lbl[sl].to(dev))
+    ((y.float() * g[sl].to(dev).permute(0, 2, 1)).sum() * scale).backward()
+    torch.cuda.synchronize()
+    res = {"y": y.detach().float().cpu(),
+           "grads": {n: (p.grad.detach().float() / scale).cpu() for n, p in model.named_parameters()
+                     if p.grad is not None},
            "running": {n: b.detach().cpu() for n, b in model.named_buffers()}}
     torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()

@@ -22,7 +22,7 @@ from conftest import REPO, rel_err
 pytestmark = pytest.mark.gpu
 
 
-def _run_ranks(tmp_path, mode, precision="fp32"):
+def _run_ranks(tmp_path, mode, precision="fp32", timeout=180):
     env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000))
     procs = []
     for r in range(2):
@@ -30,7 +30,7 @@ def _run_ranks(tmp_path, mode, precision="fp32"):
         procs.append(subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "_ddp_worker.py"), str(tmp_path),
                                        mode, precision], env=e))
     for p in procs:
-        assert p.wait(timeout=180) == 0
+        assert p.wait(timeout=timeout) == 0
     return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
 
 
@@ -108,3 +108,36 @@ def test_ddp_syncbn_position_embedding_matches_full_batch(cuda, tmp_path):
         got = ranks[0]["grads"].get(n, ranks[0]["grads"].get(f"{alias.get(mod, mod)}.{attr}"))
         assert got is not None, n
         assert rel_err(got * 2, full) < 1e-3, n
+
+
+def test_net_syncbn_fp16_autocast_matches_full_batch(cuda, tmp_path):
+    """The reference's own multi-GPU training configuration on two gloo ranks
+    sharing one GPU (main_partseg_dist.py:189-196, 253-260): Net converted with
+    SyncBatchNorm under DDP, forward under fp16 autocast (the engine's GEMMs
+    take the bf16 path, its BN statistics are all-reduced from the C++ op), at
+    the cfg4 geometry (N 2048, k 40, emb 512). Each rank equals its half of a
+    single-process full-batch autocast step within the bf16 bar, gradients
+    (DDP-averaged x world) too. Stock layers: MIOpen / fp16 GEMM rounding."""
+    import _ddp_worker as W
+    from models.model_partseg import Net
+    ranks = _run_ranks(tmp_path, "net_syncbn_amp", timeout=300)
+    torch.manual_seed(0)
+    m = Net(types.SimpleNamespace(**W.NET_ARGS)).to(cuda).train()
+    pts, lbl, g = W.net_inputs(2)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1).contiguous()
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = m(x, lbl.to(cuda))
+    (y.float() * g.to(cuda).permute(0, 2, 1)).sum().backward()
+    yf = y.detach().float().cpu()
+    tol = 2e-2
+    for r in range(2):
+        assert rel_err(ranks[r]["y"], yf[W.NET_B * r:W.NET_B * (r + 1)]) < tol, r
+    worst = {}
+    for n, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        assert torch.equal(ranks[0]["grads"][n], ranks[1]["grads"][n]), n
+        worst[n] = rel_err(ranks[0]["grads"][n] * 2, p.grad.float().cpu())
+    print("worst grads:", sorted(worst.items(), key=lambda t: -t[1])[:5])
+    for n, e in worst.items():
+        assert e < tol, (n, e)

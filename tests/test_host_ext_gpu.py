@@ -1,9 +1,12 @@
-"""The C++ op layer (libdgx_torch.so, dgx.host): DGCNN's train step as one
-custom op with a C++ autograd node equals the Python dispatch of the same
-kernels bit for bit — output, every gradient, every BatchNorm buffer — at the
-BASELINE geometries (cfg2 B=32 N=1024 k=20 emb 1024; the cfg5 9-channel
-S3DIS block; a shard with the input gradient), and inside Net's kNN-sharing
-scope. Reference: models/dgcnn.py:84-103 and its autograd."""
+"""The C++ op layer (libdgx_torch.so, dgx.host): DGCNN.forward as one custom
+op with a C++ autograd node serves every configuration the reference's
+scripts run (bf16 / fp32, fp16 autocast, train / eval / no_grad, momentum or
+cumulative running statistics, SyncBatchNorm) and equals the autograd
+Functions over the same C++ schedule bit for bit — output, every gradient,
+every BatchNorm buffer — at the BASELINE geometries (cfg2 B=32 N=1024 k=20
+emb 1024; the cfg5 9-channel S3DIS block; a shard with the input gradient),
+and inside Net's kNN-sharing scope. Reference: models/dgcnn.py:84-103 and its
+autograd; main_partseg_dist.py:189, 253."""
 import copy
 import types
 
@@ -65,27 +68,40 @@ def assert_net_grads_same(ga, gb):
 def _counting(monkeypatch):
     from dgx import host
     calls = []
-    real = host.dgcnn_train
+    real = host.dgcnn_forward
 
     def wrapped(model, x):
         calls.append(tuple(x.shape))
         return real(model, x)
-    monkeypatch.setattr(host, "dgcnn_train", wrapped)
+    monkeypatch.setattr(host, "dgcnn_forward", wrapped)
     return calls
 
 
-@pytest.mark.parametrize("case", ["cfg2", "cfg5_s3dis", "shard_xgrad"])
-def test_host_op_equals_python_dispatch(cuda, monkeypatch, case):
+CASES = {   # B, N, k, emb, C, precision
+    "cfg2": (32, 1024, 20, 1024, 3, "bf16"),
+    "cfg2_fp32": (32, 1024, 20, 1024, 3, "fp32"),
+    "cfg5_s3dis": (2, 4096, 20, 1024, 9, "bf16"),
+    "shard_xgrad": (4, 1024, 20, 256, 3, "bf16"),
+    "shard_xgrad_fp32": (4, 1024, 20, 256, 3, "fp32"),
+    "momentum_none": (4, 512, 16, 128, 3, "bf16"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_host_op_equals_function_path(cuda, monkeypatch, case):
     from dgx import host, precision as prec
-    B, N, k, emb, C = {"cfg2": (32, 1024, 20, 1024, 3), "cfg5_s3dis": (2, 4096, 20, 1024, 9),
-                       "shard_xgrad": (4, 1024, 20, 256, 3)}[case]
+    B, N, k, emb, C, precision = CASES[case]
     base = _model(emb, k, C, seed=1)
+    if case == "momentum_none":   # cumulative running averages (nn.BatchNorm momentum=None)
+        for mod in base.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.momentum = None
     x = _cloud(cuda, B, N, C, seed=3)
-    if case == "shard_xgrad":
+    if case.startswith("shard_xgrad"):
         x = x.detach().clone().requires_grad_(True)
     gout = torch.randn((B, emb, N), device=cuda)
     calls = _counting(monkeypatch)
-    prec.set("bf16")
+    prec.set(precision)
     try:
         ma, mb = copy.deepcopy(base).to(cuda).train(), copy.deepcopy(base).to(cuda).train()
         oa = torch.optim.SGD(ma.parameters(), lr=0.1, momentum=0.9)
@@ -102,28 +118,71 @@ def test_host_op_equals_python_dispatch(cuda, monkeypatch, case):
             _assert_same(a, b)
         assert len(calls) == 2, "the C++ op did not serve the train step"
         assert int(ma.conv5[1].num_batches_tracked) == 2
+        # inference on the trained state: eval mode, no autograd
+        ma.eval()
+        mb.eval()
+        with torch.no_grad():
+            monkeypatch.setattr(host, "ENABLED", True)
+            ya = ma(x)
+            monkeypatch.setattr(host, "ENABLED", False)
+            yb = mb(x)
+        assert torch.equal(ya, yb)
+        assert len(calls) == 3
     finally:
         prec.set("fp32")
 
 
-def test_host_op_skipped_outside_its_configuration(cuda, monkeypatch):
-    """fp32 parity mode, eval mode and SyncBatchNorm keep the Python dispatch."""
-    from dgx import host, precision as prec
+def test_host_op_serves_every_configuration(cuda, monkeypatch):
+    """fp32 and bf16, eval and no_grad, momentum None and SyncBatchNorm all take
+    the C++ op; only a host tensor, a debug capture or DGX_HOST_EXT=0 do not."""
+    import dgx.edgeconv as E
+    from dgx import host
     m = _model(128, 20).to(cuda)
     x = _cloud(cuda, 2, 512)
-    assert not host.applies(m.train(), x)          # precision fp32 (default)
-    prec.set("bf16")
+    assert host.applies(m.train(), x)
+    assert host.applies(m.eval(), x)
+    m.train()
+    m.conv3[1].momentum = None
+    assert host.applies(m, x)
+    with torch.no_grad():
+        assert host.applies(m, x)
+    assert host.applies(torch.nn.SyncBatchNorm.convert_sync_batchnorm(copy.deepcopy(m)), x)
+    assert not host.applies(m, x.cpu())
+    E.set_debug_capture({})
     try:
-        assert host.applies(m.train(), x)
-        assert not host.applies(m.eval(), x)
-        m.train()
-        m.conv3[1].momentum = None
         assert not host.applies(m, x)
-        m.conv3[1].momentum = 0.1
-        with torch.no_grad():
-            assert not host.applies(m, x)
     finally:
-        prec.set("fp32")
+        E.set_debug_capture(None)
+    monkeypatch.setattr(host, "ENABLED", False)
+    assert not host.applies(m, x)
+
+
+def test_host_op_follows_autocast(cuda, monkeypatch):
+    """Under torch.autocast(float16 | bfloat16) (main_partseg_dist.py:253) the
+    op's GEMMs take the bf16 path (SURVEY §8(b) "GEMMs follow autocast dtype"):
+    the step equals the same step in precision "bf16" without autocast, bit
+    for bit, through the C++ op; without autocast the fp32 mode stays fp32."""
+    from dgx import precision as prec
+    base = _model(256, 20, seed=4)
+    x = _cloud(cuda, 4, 1024, seed=9)
+    gout = torch.randn((4, 256, 1024), device=cuda)
+    calls = _counting(monkeypatch)
+    res = {}
+    for name in ("fp16_autocast", "bf16_autocast", "bf16_mode", "fp32_mode"):
+        m = copy.deepcopy(base).to(cuda).train()
+        if name.endswith("autocast"):
+            dt = torch.float16 if name.startswith("fp16") else torch.bfloat16
+            with torch.autocast("cuda", dtype=dt):
+                res[name] = _step(m, x, gout)
+        elif name == "bf16_mode":
+            with prec.mode("bf16"):
+                res[name] = _step(m, x, gout)
+        else:
+            res[name] = _step(m, x, gout)
+    assert len(calls) == 4
+    _assert_same(res["fp16_autocast"], res["bf16_mode"])
+    _assert_same(res["bf16_autocast"], res["bf16_mode"])
+    assert not torch.equal(res["fp32_mode"][0], res["bf16_mode"][0])
 
 
 def test_host_op_in_net_knn_scope(cuda, monkeypatch):

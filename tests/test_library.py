@@ -70,13 +70,23 @@ def test_state_dict_keys_match_reference():
 
 
 def test_host_op_library_loads():
-    """libdgx_torch.so (the C++ op + autograd layer over libdgx.so) loads and
-    registers torch.ops.dgx_host.dgcnn_train; host tensors never take it."""
+    """libdgx_torch.so (the C++ schedule + autograd layer over libdgx.so) loads
+    and registers the torch.ops.dgx_host ops every device path runs; host
+    tensors never take them."""
     from dgx import host
     from models.dgcnn import DGCNN
     host.load()
-    schema = str(torch.ops.dgx_host.dgcnn_train.default._schema)
-    assert schema.startswith("dgx_host::dgcnn_train(Tensor x, Tensor[] params, Tensor[] bufs, Tensor? idx0")
+    want = {
+        "dgcnn": "dgx_host::dgcnn(Tensor x, Tensor[] params, Tensor?[] bufs, float[] bn_f, int[] bn_i, str[] groups",
+        "chain_forward": "dgx_host::chain_forward(Tensor x, int k, Tensor[] weights",
+        "chain_backward": "dgx_host::chain_backward(Tensor dxcat, Tensor xcat, Tensor xcat16, Tensor[] saved",
+        "pointconv_forward": "dgx_host::pointconv_forward(Tensor X, Tensor X16, int B, int N",
+        "pointconv_backward": "dgx_host::pointconv_backward(Tensor dout, Tensor[] saved",
+        "knn_timing": "dgx_host::knn_timing(bool on) -> float[]",
+    }
+    for name, head in want.items():
+        assert str(getattr(torch.ops.dgx_host, name).default._schema).startswith(head), name
+    assert torch.ops.dgx_host.knn_timing(False) == []
     assert not host.applies(DGCNN(types.SimpleNamespace(emb_dim=64, k=4)).train(), torch.rand(2, 3, 32))
 
 
