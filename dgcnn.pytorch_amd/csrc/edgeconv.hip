@@ -1150,7 +1150,8 @@ int dgx_edge_fwd_gather_f32(const float* PQ, int ldpq, const int32_t* idx, int B
     if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
     const GatherGeom g = gather_geom(B, N, Co);
     if (nrows != B * g.parts) return DGX_EINVAL;
-    if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
+    // beyond EC_LDS_BYTES (N > 16384) a one-channel slice takes up to the CU's 160 KiB (one workgroup per CU)
+    if (g.lds > (size_t)160 * 1024) return DGX_EUNSUPPORTED;
     return launch_gather<false>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
                                 ldpq, idx, B, N, k, Co,
                                 g.parts, gamma, nullptr, 0.f, ysel, arg, sumP, partials, nullptr, 0);
@@ -1160,8 +1161,8 @@ int dgx_edge_fwd_eval_f32(const float* PQ, int ldpq, const int32_t* idx, int B, 
                           const float* scale, const float* shift, float slope, float* out, int ldo, void* stream) {
     if (!PQ || !idx || !scale || !shift || !out) return DGX_EINVAL;
     if (B < 1 || N < 1 || k < 1 || Co < 1 || ldpq < 2 * Co || ldo < Co) return DGX_EINVAL;
-    if ((size_t)N * sizeof(float) > (size_t)EC_LDS_BYTES) return DGX_EUNSUPPORTED;
     const GatherGeom g = gather_geom(B, N, Co);
+    if (g.lds > (size_t)160 * 1024) return DGX_EUNSUPPORTED;
     return launch_gather<true>(g.cs, dim3(dgx_xcd_cloud_grid(B, g.parts * g.slices)), g.lds, dgx_stream(stream), PQ,
                                ldpq, idx, B, N, k, Co,
                                g.parts, scale, shift, slope, nullptr, nullptr, nullptr, nullptr, out, ldo);
@@ -1349,11 +1350,15 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
     const size_t per_pc = packed ? 8 : 9;
     int cs = 8;
     while (cs > 1 && per_pc * N * cs > (size_t)BW_LDS_BYTES) cs >>= 1;
-    if (per_pc * N * cs > (size_t)BW_LDS_BYTES) return DGX_EUNSUPPORTED;
     const int slices = (Co + cs - 1) / cs;
-    const int parts = point_parts(B, slices, N);
+    int parts = point_parts(B, slices, N);
+    // a cloud whose one-channel slices exceed BW_LDS_BYTES (N > 9216) takes up to
+    // the CU's 160 KiB (one workgroup per CU; more point parts shrink the order
+    // array): N <= 20000 packed, 17900 unpacked
+    while (scatter_lds_bytes(N, cs, parts, packed) > (size_t)160 * 1024 && parts * 64 < N) parts *= 2;
     const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
     const size_t lds = scatter_lds_bytes(N, cs, parts, packed);
+    if (lds > (size_t)160 * 1024) return DGX_EUNSUPPORTED;
     hipStream_t st = dgx_stream(stream);
 #define DGX_SCATTER_LAUNCH(CSV, O16, PK)                                                                      \
     hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \

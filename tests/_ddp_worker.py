@@ -57,8 +57,16 @@ NET_B, NET_N = 2, 2048   # clouds per rank, points (BASELINE cfg4 geometry, batc
 
 
 def net_inputs(world):
+    """Clouds arranged so every rank's first cloud is the global batch's first:
+    compute_hog_1x1 gathers neighbourhoods with local ids from x.view(B*N, 3)
+    (reference model_partseg.py:26-30), so a cloud's HOG depends
+    on its batch's cloud 0 — a rank's outputs equal the full batch's only if
+    those coincide."""
+    import numpy as np
     from dgx import synth
-    pts = synth.cube_clouds(NET_B * world, NET_N, 31)
+    assert NET_B == 2 and world == 2
+    c = synth.cube_clouds(3, NET_N, 31)
+    pts = np.ascontiguousarray(np.stack([c[0], c[1], c[0], c[2]]))
     lbl = torch.nn.functional.one_hot(torch.arange(NET_B * world) % 16, 16).float()
     g = torch.from_numpy(synth.uniform(32, (NET_B * world, NET_N, NET_ARGS["nclasses"])) - 0.5).float()
     return pts, lbl, g
@@ -79,7 +87,7 @@ def net_syncbn_amp(rank, world, out_dir, dev):
     pts, lbl, g = net_inputs(world)
     sl = slice(rank * NET_B, (rank + 1) * NET_B)
     x = torch.from_numpy(pts[sl]).to(dev).permute(0, 2, 1).contiguous()
-    scale = 1024.0
+    scale = 1.0
     with torch.autocast("cuda", dtype=torch.float16):
         y = ddp(x, lbl[sl].to(dev))
     ((y.float() * g[sl].to(dev).permute(0, 2, 1)).sum() * scale).backward()

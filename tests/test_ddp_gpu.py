@@ -136,8 +136,10 @@ def test_net_syncbn_fp16_autocast_matches_full_batch(cuda, tmp_path):
     for n, p in m.named_parameters():
         if p.grad is None:
             continue
-        assert torch.equal(ranks[0]["grads"][n], ranks[1]["grads"][n]), n
-        worst[n] = rel_err(ranks[0]["grads"][n] * 2, p.grad.float().cpu())
+        g0, g1 = ranks[0]["grads"][n], ranks[1]["grads"][n]
+        assert torch.isfinite(g0).all() and torch.isfinite(g1).all(), n
+        assert rel_err(g0, g1) < 1e-6, (n, rel_err(g0, g1))   # DDP-averaged: the same on both ranks
+        worst[n] = rel_err(g0 * 2, p.grad.float().cpu())
     print("worst grads:", sorted(worst.items(), key=lambda t: -t[1])[:5])
     for n, e in worst.items():
         assert e < tol, (n, e)

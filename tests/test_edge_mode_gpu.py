@@ -52,6 +52,7 @@ def test_dgcnn_diff_mode_fp32(cuda):
     from dgx import synth
     from models.dgcnn import _diff_weight
     from oracle import reference as R
+    from conftest import validate_dgcnn_decisions
     from test_edgeconv_gpu import ROUTED_GRAD_TOL, Capture
     torch.manual_seed(4)
     base = DGCNN_diff()
@@ -64,6 +65,12 @@ def test_dgcnn_diff_mode_fp32(cuda):
     assert rel_err(ya.detach().cpu(), yb.detach().cpu()) < 1e-4
     g = torch.randn_like(ya)
     ya.backward(g)
+    # every block's neighbour set, max slot and LeakyReLU sign against the
+    # reference's rules, on the equivalent (x_j, x_i) weights [W1 | W2 - W1]
+    init_cat = dict(init)
+    for i in range(1, 5):
+        init_cat[f"conv{i}.0.weight"] = _diff_weight(init[f"conv{i}.0.weight"])
+    print("decision check (gap, flip):", validate_dgcnn_decisions(cap, x, 16, init_cat))
     decisions = [tuple(t for t in cap[("fwd", l)]) for l in range(4)]
     p64 = {n: t.to(cuda).double() if t.is_floating_point() else t.to(cuda) for n, t in init.items()}
     for n, t in p64.items():

@@ -1,5 +1,6 @@
 """a3/a5/a8 parity: fused EdgeConv chain and DGCNN vs the reference's goldens
 (1e-3 relative fp32)."""
+import copy
 import types
 
 import numpy as np
@@ -303,10 +304,12 @@ def test_dgcnn_full_size_train_step(cuda):
 
 
 @pytest.mark.parametrize("B,N,k,emb,in_dims", [(32, 1024, 20, 1024, 3),    # cfg2: the bench headline
+                                               (2, 2048, 40, 1024, 3),     # cfg3 geometry (bench --config cfg3)
                                                (2, 4096, 20, 1024, 9)])    # cfg5 model, S3DIS blocks
 def test_dgcnn_bf16_headline_cfg2_routed(cuda, B, N, k, emb, in_dims):
     """The headline configuration (BASELINE configs[1]: DGCNN(emb 1024), B 32,
-    N 1024, k 20, bf16 GEMMs) at full size, and the cfg5 model bench.py
+    N 1024, k 20, bf16 GEMMs) at full size, the cfg3 geometry (N 2048, k 40;
+    two clouds of the 32), and the cfg5 model bench.py
     --config cfg5 times (DGCNN(in_dims=9) on S3DIS blocks, N 4096, k 20; two
     clouds of the per-GPU 24): train-mode output and every parameter gradient
     within SURVEY §8(c)'s bf16 bar (2e-2) of the fp64 oracle routed by the
@@ -375,3 +378,33 @@ def test_dgcnn_bf16_mode_routed(cuda):
     assert rel_err(y.detach().cpu(), ref.detach()) < 2e-2
     for n, p in m.named_parameters():
         assert rel_err(p.grad.cpu(), params[n].grad) < 2e-2, n
+
+
+def test_dgcnn_large_n_generic_knn(cuda, monkeypatch):
+    """A cloud larger than the fused kNN kernel's N (12288): every block's kNN
+    takes the generic kernel, no block writes a fused kNN image for the next
+    (ADVICE r04), in both dispatch paths (the one-op C++ layer and the
+    autograd Functions), bit-equal to each other, with block 1's neighbours
+    equal to the oracle's and finite gradients."""
+    import oracle as O
+    from dgx import host, ops, synth
+    from models.dgcnn import DGCNN
+    B, N, k = 1, 16384, 20
+    assert not ops.fast_shape(3, k, N)
+    torch.manual_seed(11)
+    base = DGCNN(types.SimpleNamespace(emb_dim=64, k=k))
+    pts = synth.cube_clouds(B, N, 17)
+    x = torch.from_numpy(pts).to(cuda).permute(0, 2, 1)
+    outs = []
+    for enabled in (True, False):
+        monkeypatch.setattr(host, "ENABLED", enabled)
+        m = copy.deepcopy(base).to(cuda).train()
+        y = m(x)
+        y.square().mean().backward()
+        outs.append((y.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for n in outs[0][1]:
+        assert torch.equal(outs[0][1][n], outs[1][1][n]), n
+        assert torch.isfinite(outs[0][1][n]).all(), n
+    got = ops.knn(x, k).cpu().numpy()
+    np.testing.assert_array_equal(got, O.knn(torch.from_numpy(pts).permute(0, 2, 1), k))

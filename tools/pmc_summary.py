@@ -22,6 +22,7 @@ import sys
 def short(name):
     name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"^void ", "", name)
+    name = re.sub(r"^(\w+::)+", "", name)   # e.g. dgx_knn::knn_kernel<...>
     depth, out = 0, []
     for ch in name:  # drop the argument list, keep template arguments
         if ch == "(" and depth == 0:
