@@ -65,6 +65,7 @@ struct Opts {
   bool fuse_image = true;    // blocks' apply writes the next kNN's operand image
   bool fuse_edge_dz = true;  // bf16: block l-1's dz from block l's dX GEMM epilogue
   int64_t slab_cap_mb = 8;   // split-K slab cap of small weight gradients (0 = off)
+  bool split32 = true;       // fp32 mode: conv5 GEMMs as 3-pass split bf16 (hi.hi + hi.lo + lo.hi)
 };
 Opts decode(int64_t o) {
   Opts r;
@@ -73,6 +74,7 @@ Opts decode(int64_t o) {
   r.fuse_image = o & 4;
   r.fuse_edge_dz = o & 8;
   r.slab_cap_mb = (o >> 8) & 0xff;
+  r.split32 = o & 16;
   return r;
 }
 
@@ -419,6 +421,34 @@ void lds_atb(const Dev& d, const Tensor& a16, const Tensor& b16, Tensor& out, in
   reduce_slab(d, slab, used, M, N, split_rows > 0 ? split_rows : M, out, defer);
 }
 
+// out = sum_i a_i^T b_i over the pairs (same shapes): every pair's split-K slabs in
+// one buffer, summed by one fixed-order reduce (the fp32 mode's 3-pass weight gradients)
+void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab, Tensor& out, SlabJobs* defer) {
+  const int R = (int)ab[0].first.size(0), M = (int)ab[0].first.size(1), N = (int)ab[0].second.size(1);
+  const int S = dgx_gemm_splits(M, N, R);
+  int64_t chunk = cdiv(R, S);
+  chunk = cdiv(chunk, 64) * 64;
+  const int used = (int)cdiv(R, chunk);
+  const int n = (int)ab.size();
+  Tensor slab = at::empty({(int64_t)n * used, M, N}, d.f32);
+  for (int i = 0; i < n; ++i) {
+    const Tensor &a16 = ab[i].first, &b16 = ab[i].second;
+    check(dgx_gemm_lds_bf16(a16.data_ptr(), ld16(a16), b16.data_ptr(), ld16(b16), 1, M, N, R, R, kEpiSlab, S,
+                            P(slab) + (int64_t)i * used * M * N, N, nullptr, nullptr, 0, d.stream),
+          "gemm lds tn");
+  }
+  reduce_slab(d, slab, n * used, M, N, M, out, defer);
+}
+
+// fp32 -> (hi, lo) bf16 planes (dgx_split_bf16)
+std::pair<Tensor, Tensor> split16(const Dev& d, const Tensor& x) {
+  const int64_t M = x.size(0), K = x.size(1);
+  Tensor hi = at::empty({M, K}, d.bf16), lo = at::empty({M, K}, d.bf16);
+  check(dgx_split_bf16(P(x), M > 1 ? x.stride(0) : K, M, (int)K, hi.data_ptr(), lo.data_ptr(), K, d.stream),
+        "split bf16");
+  return {hi, lo};
+}
+
 // dgx.gemm.edge_dz_ok
 bool edge_dz_ok(const Tensor& dpq16, int cin) {
   const int64_t K = dpq16.size(1);
@@ -482,6 +512,7 @@ struct PrepJob {
   Tensor w;
   int rows, cols;
   bool stacked, split;
+  bool tsplit = false;   // tn as [hi^T | lo^T] too
 };
 std::vector<std::pair<Tensor, Tensor>> prep_views(const Tensor& buf, const std::vector<PrepJob>& jobs,
                                                   int64_t* total_out = nullptr) {
@@ -489,11 +520,11 @@ std::vector<std::pair<Tensor, Tensor>> prep_views(const Tensor& buf, const std::
   int64_t total = 0;
   for (const auto& j : jobs) {
     const int64_t R = j.stacked ? 2 * j.rows : j.rows;
-    const int64_t n_tn = R * j.cols, n_nt = (j.split ? 2 : 1) * R * j.cols;
+    const int64_t n_tn = (j.tsplit ? 2 : 1) * R * j.cols, n_nt = (j.split ? 2 : 1) * R * j.cols;
     const int64_t p_nt = cdiv(n_nt, 8) * 8, p_tn = cdiv(n_tn, 8) * 8;
     if (buf.defined())
       v.emplace_back(buf.narrow(0, total, n_nt).view({R, j.split ? 2 * j.cols : j.cols}),
-                     buf.narrow(0, total + p_nt, n_tn).view({j.cols, R}));
+                     buf.narrow(0, total + p_nt, n_tn).view({j.cols, j.tsplit ? 2 * R : R}));
     total += p_nt + p_tn;
   }
   if (total_out) *total_out = total;
@@ -520,7 +551,7 @@ std::pair<Tensor, std::vector<std::pair<Tensor, Tensor>>> prep_weights(const Dev
     TN[j] = views[j].second.data_ptr();
     CO[j] = jobs[j].rows;
     CI[j] = jobs[j].cols;
-    ST[j] = (int)jobs[j].stacked | (2 * (int)jobs[j].split);
+    ST[j] = (int)jobs[j].stacked | (2 * (int)jobs[j].split) | (4 * (int)jobs[j].tsplit);
   }
   check(dgx_weight_prep_multi_bf16(n, W.data(), CO.data(), CI.data(), ST.data(), NT.data(), TN.data(), d.stream),
         "weight prep");
@@ -939,6 +970,7 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
 // ---------------------------------------------------------------- conv5 ----
 struct PcState {
   Tensor Xop, W, Z, nt, tn;
+  Tensor xhi, xlo;   // fp32 mode, 3-pass split bf16: X's planes (nt / tn then hold [hi | lo] weights)
   Stats st;
   bool bf16 = false;
   int B = 0, N = 0;
@@ -948,13 +980,13 @@ struct PcState {
 // conv5 -> BN -> LeakyReLU on the point-major concat buffer (dgx.pointconv, dgcnn.py:100-102):
 // out (B, Co, N); bf16: Z stored bf16 with the BN statistics from the GEMM's fp32 sums
 Tensor pointconv_forward_impl(const Dev& d, const Tensor& X_in, const Tensor& X16, int B, int N, const Layer& ly,
-                              bool bf16, Tensor nt, Tensor tn, PcState* state) {
+                              bool bf16, Tensor nt, Tensor tn, PcState* state, bool split32 = false) {
   Tensor X = X_in.scalar_type() == at::kFloat ? X_in : X_in.to(at::kFloat);
   const int64_t M = X.size(0), K = X.size(1);
   const int Co = (int)ly.w.size(0);
   Tensor W = ly.w.reshape({Co, K});
   const bool use_batch = ly.bn.use_batch();
-  Tensor Z, gemm_part, Xop = X;
+  Tensor Z, gemm_part, Xop = X, xhi, xlo;
   if (bf16) {
     if (X16.defined() && X16.numel() && lds_ok(X16, K)) {
       Xop = X16;
@@ -970,6 +1002,18 @@ Tensor pointconv_forward_impl(const Dev& d, const Tensor& X_in, const Tensor& X1
       tn = Tensor();
       Z = mm_xwt(d, X, W, use_batch ? &gemm_part : nullptr);
     }
+  } else if (split32 && K % 64 == 0 && Co % 64 == 0 && Co >= 8) {
+    // fp32 mode, 3-pass split bf16 on the bf16 MFMA: Z = X_hi (W_hi + W_lo)^T + X_lo W_hi^T
+    // (x and w with 16 significant bits each; ~2^-16 relative per product, fp32 sums)
+    auto xs = split16(d, X);
+    xhi = xs.first;
+    xlo = xs.second;
+    auto pw = prep_weights(d, {PrepJob{W, Co, (int)K, false, true, true}});
+    nt = pw.second[0].first;    // (Co, 2K) [W_hi | W_lo]
+    tn = pw.second[0].second;   // (K, 2Co) [W_hi^T | W_lo^T]
+    Z = lds_xwt(d, xhi, nt, nullptr, false);
+    Tensor w_hi = nt.narrow(1, 0, K);
+    lds_xwt(d, xlo, w_hi, nullptr, false, &Z, &Z);
   } else {
     nt = Tensor();
     tn = Tensor();
@@ -997,7 +1041,7 @@ Tensor pointconv_forward_impl(const Dev& d, const Tensor& X_in, const Tensor& X1
   else
     check(dgx_pointconv_apply_f32(P(Z), Co, B, N, Co, P(st.scale), P(st.shift), (float)ly.slope, P(out), d.stream),
           "pointconv apply");
-  if (state) *state = PcState{Xop, W, Z, nt, tn, st, bf16, B, N, ly.slope};
+  if (state) *state = PcState{Xop, W, Z, nt, tn, xhi, xlo, st, bf16, B, N, ly.slope};
   return out;
 }
 
@@ -1043,6 +1087,12 @@ std::array<Tensor, 4> pointconv_backward_impl(const Dev& d, Tensor dout, const P
       dX = at::empty({M, K}, d.f32);
       mm_xw(d, dZ, s.W, dX, false);
     }
+  } else if (s.xhi.defined()) {   // 3-pass split bf16 (the forward's planes and weights)
+    auto zs = split16(d, dZ);
+    lds_atb_sum(d, {{zs.first, s.xhi}, {zs.first, s.xlo}, {zs.second, s.xhi}}, dW, slabs);
+    dX = lds_xwt(d, zs.first, s.tn, nullptr, false);                       // dZ_hi (W_hi + W_lo)
+    Tensor wt_hi = s.tn.narrow(1, 0, Co);
+    lds_xwt(d, zs.second, wt_hi, nullptr, false, &dX, &dX);               // + dZ_lo W_hi
   } else {   // fp32 MFMA GEMMs (dW: split-K over the B*N rows)
     dW = mm32(d, dZ.t(), s.Xop, nullptr, false);
     dX = mm32(d, dZ, s.W, nullptr, false);
@@ -1132,11 +1182,12 @@ std::tuple<Tensor, std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>
   return {g.dx, g.dw, g.dgamma, g.dbeta};
 }
 
-// dgx_host::pointconv_forward -> (out, [Xop, Z, scale, shift, mean, invstd, nt, tn])
+// dgx_host::pointconv_forward -> (out, [Xop, Z, scale, shift, mean, invstd, nt, tn, xhi, xlo])
 std::tuple<Tensor, std::vector<Tensor>> pointconv_forward(
     const Tensor& X, const Tensor& X16, int64_t B, int64_t N, const Tensor& weight, const Tensor& gamma,
-    const Tensor& beta, const c10::List<std::optional<Tensor>>& bn_t_l, std::vector<double> bn_f, std::vector<int64_t> bn_i,
-    std::string group, bool bf16, const std::optional<Tensor>& nt, const std::optional<Tensor>& tn) {
+    const Tensor& beta, const c10::List<std::optional<Tensor>>& bn_t_l, std::vector<double> bn_f,
+    std::vector<int64_t> bn_i, std::string group, bool bf16, const std::optional<Tensor>& nt,
+    const std::optional<Tensor>& tn, int64_t opts) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   Dev d(X);
   auto bn_t = to_vec(bn_t_l);
@@ -1147,16 +1198,20 @@ std::tuple<Tensor, std::vector<Tensor>> pointconv_forward(
   ly.bn = parse_bn(bn_t, bn_f, bn_i, {group}, 1, 6)[0];
   ly.slope = bn_f[2];
   PcState s;
-  Tensor out = pointconv_forward_impl(d, X, X16, (int)B, (int)N, ly, bf16, defined_or_none(nt), defined_or_none(tn), &s);
+  Tensor out = pointconv_forward_impl(d, X, X16, (int)B, (int)N, ly, bf16, defined_or_none(nt), defined_or_none(tn), &s,
+                                      decode(opts).split32);
   auto e16 = [&](const Tensor& t) { return t.defined() ? t : at::empty({0}, d.bf16); };
-  return {out, {s.Xop, s.Z, s.st.scale, s.st.shift, s.st.mean, s.st.invstd, e16(s.nt), e16(s.tn)}};
+  return {out, {s.Xop, s.Z, s.st.scale, s.st.shift, s.st.mean, s.st.invstd, e16(s.nt), e16(s.tn), e16(s.xhi),
+                e16(s.xlo)}};
 }
 
-// dgx_host::pointconv_backward -> (dX, dW, dgamma, dbeta)
+// dgx_host::pointconv_backward -> (dX, dW, dgamma, dbeta). The fp32 mode's split
+// planes and weights are rebuilt from X / the weight when the caller did not keep
+// them (the torch.library op): dgx_split_bf16 is deterministic.
 std::tuple<Tensor, Tensor, Tensor, Tensor> pointconv_backward(const Tensor& dout, std::vector<Tensor> saved,
                                                               const Tensor& weight, int64_t B, int64_t N, double slope,
-                                                              bool eval, std::string group, bool bf16) {
-  TORCH_CHECK(saved.size() == 8, "dgx pointconv backward: 8 saved tensors expected");
+                                                              bool eval, std::string group, bool bf16, int64_t opts) {
+  TORCH_CHECK(saved.size() == 10, "dgx pointconv backward: 10 saved tensors expected");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(saved[1].device());
   Dev d(saved[1]);
   PcState s;
@@ -1165,7 +1220,19 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> pointconv_backward(const Tensor& dout
   s.st = Stats{saved[2], saved[3], saved[4], saved[5], group, eval};
   s.nt = saved[6].numel() ? saved[6] : Tensor();
   s.tn = saved[7].numel() ? saved[7] : Tensor();
-  s.W = weight.reshape({weight.size(0), s.Xop.size(1)});
+  s.xhi = saved[8].numel() ? saved[8] : Tensor();
+  s.xlo = saved[9].numel() ? saved[9] : Tensor();
+  const int64_t K = s.Xop.size(1), Co = weight.size(0);
+  s.W = weight.reshape({Co, K});
+  if (!bf16 && !s.xhi.defined() && decode(opts).split32 && s.Xop.scalar_type() == at::kFloat && K % 64 == 0 &&
+      Co % 64 == 0) {
+    auto xs = split16(d, s.Xop);
+    s.xhi = xs.first;
+    s.xlo = xs.second;
+    auto pw = prep_weights(d, {PrepJob{s.W, (int)Co, (int)K, false, true, true}});
+    s.nt = pw.second[0].first;
+    s.tn = pw.second[0].second;
+  }
   s.bf16 = bf16;
   s.B = (int)B;
   s.N = (int)N;
@@ -1254,7 +1321,7 @@ DgcnnRun dgcnn_run(const Dev& d, const Tensor& x, std::vector<Layer>& all, const
   }
   TORCH_CHECK(c5.w.size(1) == r.chain.xcat.size(1), "dgx dgcnn: conv5 takes the concat of the blocks");
   r.out = pointconv_forward_impl(d, r.chain.xcat, r.chain.have16 ? r.chain.xcat16 : Tensor(), B, N, c5, c.bf16, nt5,
-                                 tn5, &r.pc);
+                                 tn5, &r.pc, o.split32);
   return r;
 }
 
@@ -1275,9 +1342,9 @@ class DgcnnFn : public torch::autograd::Function<DgcnnFn> {
     state.push_back(r.chain.xcat);
     state.push_back(r.chain.xcat16);
     state.push_back(r.chain.prep.defined() ? r.chain.prep : at::empty({0}, d.bf16));
+    auto e16 = [&](const Tensor& t) { return t.defined() ? t : at::empty({0}, d.bf16); };
     state.insert(state.end(), {r.pc.Xop, r.pc.Z, r.pc.st.scale, r.pc.st.shift, r.pc.st.mean, r.pc.st.invstd,
-                               r.pc.nt.defined() ? r.pc.nt : at::empty({0}, d.bf16),
-                               r.pc.tn.defined() ? r.pc.tn : at::empty({0}, d.bf16)});
+                               e16(r.pc.nt), e16(r.pc.tn), e16(r.pc.xhi), e16(r.pc.xlo)});
     ctx->saved_data["state"] = at::IValue(c10::List<Tensor>(state));
     ctx->saved_data["k"] = c.k;
     ctx->saved_data["bf16"] = c.bf16;
@@ -1320,6 +1387,8 @@ class DgcnnFn : public torch::autograd::Function<DgcnnFn> {
     pc.st = Stats{S[nsaved + 5], S[nsaved + 6], S[nsaved + 7], S[nsaved + 8], groups[n], eval[n] != 0};
     pc.nt = S[nsaved + 9].numel() ? S[nsaved + 9] : Tensor();
     pc.tn = S[nsaved + 10].numel() ? S[nsaved + 10] : Tensor();
+    pc.xhi = S[nsaved + 11].numel() ? S[nsaved + 11] : Tensor();
+    pc.xlo = S[nsaved + 12].numel() ? S[nsaved + 12] : Tensor();
     const Tensor& w5 = params[3 * n];
     pc.W = w5.reshape({w5.size(0), pc.Xop.size(1)});
     pc.bf16 = bf16;
@@ -1409,10 +1478,10 @@ TORCH_LIBRARY(dgx_host, m) {
         "int[] shape, int k, int[] eval, str[] groups, float[] slopes, bool bf16, bool x_needs_grad, int opts) "
         "-> (Tensor, Tensor[], Tensor[], Tensor[])");
   m.def("pointconv_forward(Tensor X, Tensor X16, int B, int N, Tensor weight, Tensor gamma, Tensor beta, "
-        "Tensor?[] bn_t, float[] bn_f, int[] bn_i, str group, bool bf16, Tensor? nt, Tensor? tn) "
+        "Tensor?[] bn_t, float[] bn_f, int[] bn_i, str group, bool bf16, Tensor? nt, Tensor? tn, int opts) "
         "-> (Tensor, Tensor[])");
   m.def("pointconv_backward(Tensor dout, Tensor[] saved, Tensor weight, int B, int N, float slope, bool eval, "
-        "str group, bool bf16) -> (Tensor, Tensor, Tensor, Tensor)");
+        "str group, bool bf16, int opts) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("dgcnn(Tensor x, Tensor[] params, Tensor?[] bufs, float[] bn_f, int[] bn_i, str[] groups, Tensor? idx0, "
         "int k, bool bf16, int opts) -> Tensor");
   m.def("knn_timing(bool on) -> float[]", &knn_timing);

@@ -1141,12 +1141,15 @@ struct WeightPrepJobs {
 };
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(WeightPrepJobs jobs) {
     __shared__ bf16 tile[WP_T][WP_T + 2];
+    __shared__ bf16 tlo[WP_T][WP_T + 2];
     int j = 0;
     while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
     const int Co = jobs.Co[j], C = jobs.C[j], stacked = jobs.stacked[j] & 1, split = jobs.stacked[j] & 2;
+    const int tsplit = jobs.stacked[j] & 4;   // tn rows are [hi | lo] too (C x 2 rows)
     const float* __restrict__ W = jobs.W[j];
     const int rows = stacked ? 2 * Co : Co;
     const int ldn = split ? 2 * C : C;  // split: nt rows are [hi | lo], lo = bf16(w - hi)
+    const int ldt = tsplit ? 2 * rows : rows;
     const int ntc = (C + WP_T - 1) / WP_T;
     const int b = blockIdx.x - jobs.first[j];
     const int r0 = (b / ntc) * WP_T, c0 = (b % ntc) * WP_T;
@@ -1158,9 +1161,11 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(WeightPrepJobs j
         if (r < rows && c < C) {
             const float v = stacked ? W[(int64_t)(r % Co) * 2 * C + (r / Co) * C + c] : W[(int64_t)r * C + c];
             const bf16 h = (bf16)v;
+            const bf16 l = (bf16)(v - (float)h);
             jobs.nt[j][(int64_t)r * ldn + c] = h;
-            if (split) jobs.nt[j][(int64_t)r * ldn + C + c] = (bf16)(v - (float)h);
+            if (split) jobs.nt[j][(int64_t)r * ldn + C + c] = l;
             tile[rr][cc] = h;
+            tlo[rr][cc] = l;
         }
     }
     __syncthreads();
@@ -1168,7 +1173,29 @@ __global__ __launch_bounds__(256) void weight_prep_multi_kernel(WeightPrepJobs j
     for (int e = t; e < WP_T * WP_T; e += 256) {
         const int cc = e / WP_T, rr = e - cc * WP_T;
         const int r = r0 + rr, c = c0 + cc;
-        if (r < rows && c < C) jobs.tn[j][(int64_t)c * rows + r] = tile[rr][cc];
+        if (r < rows && c < C) {
+            jobs.tn[j][(int64_t)c * ldt + r] = tile[rr][cc];
+            if (tsplit) jobs.tn[j][(int64_t)c * ldt + rows + r] = tlo[rr][cc];
+        }
+    }
+}
+
+// fp32 -> (hi, lo) bf16 planes: hi = bf16(x), lo = bf16(x - hi) (16 significant
+// bits together): the operands of the fp32 mode's 3-pass GEMMs
+// hi.W_hi + hi.W_lo + lo.W_hi (dgx_split_bf16)
+__global__ __launch_bounds__(256) void split_bf16_kernel(const float* __restrict__ src, int64_t lds, int64_t rows,
+                                                         int cols, bf16* __restrict__ hi, bf16* __restrict__ lo,
+                                                         int64_t ldo) {
+    const int64_t n4 = (int64_t)rows * (cols / 4);
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
+        const int64_t r = e / (cols / 4);
+        const int c = (int)(e - r * (cols / 4)) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(src + r * lds + c);
+        const bf16x4 h = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+        const bf16x4 l = {(bf16)(v.x - (float)h[0]), (bf16)(v.y - (float)h[1]), (bf16)(v.z - (float)h[2]),
+                          (bf16)(v.w - (float)h[3])};
+        if (hi) *reinterpret_cast<bf16x4*>(hi + r * ldo + c) = h;
+        *reinterpret_cast<bf16x4*>(lo + r * ldo + c) = l;
     }
 }
 
@@ -1509,6 +1536,19 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
     if (epi == EPI_STATS16) DGX_G2(EPI_STATS16);
 #undef DGX_G2
     return DGX_EUNSUPPORTED;
+}
+
+int dgx_split_bf16(const float* src, int64_t lds, int64_t rows, int cols, void* hi, void* lo, int64_t ldo,
+                   void* stream) {
+    if (!src || !lo || rows < 0 || cols < 1 || lds < cols || ldo < cols) return DGX_EINVAL;
+    if (cols % 4 || lds % 4 || ldo % 4 || !aligned_to(src, 16) || !aligned_to(lo, 8) || (hi && !aligned_to(hi, 8)))
+        return DGX_EUNSUPPORTED;
+    if (rows == 0) return DGX_OK;
+    const int64_t n4 = rows * (cols / 4);
+    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(split_bf16_kernel, dim3(grid), dim3(256), 0, dgx_stream(stream), src, lds, rows, cols,
+                       static_cast<bf16*>(hi), static_cast<bf16*>(lo), ldo);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
 int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt, void* tn, void* stream) {

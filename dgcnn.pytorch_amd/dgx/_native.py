@@ -71,6 +71,7 @@ _SIGS = {
     "dgx_pointconv_bwd_f32": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp],
     "dgx_pointconv_input_grad": [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_to_bf16": [_vp, _i64, _i64, _i32, _vp, _vp],
+    "dgx_split_bf16": [_vp, _i64, _i64, _i32, _vp, _vp, _i64, _vp],
     "dgx_gemm_stats_rows": [_i32],
     "dgx_gemm_splits": [_i32, _i32, _i32],
     "dgx_gemm_edge_dz_rows": [_i32, _i32],

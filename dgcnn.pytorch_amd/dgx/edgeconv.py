@@ -53,6 +53,11 @@ FUSE_KNN_IMAGE = os.environ.get("DGX_FUSE_KNN_IMAGE", "1") == "1"
 # in its epilogue and writes that block's packed dz + BN partials
 # (dgx_gemm_edge_dz_bf16) instead of dY (DGX_FUSE_EDGE_DZ=0: dY + a dz pass)
 FUSE_EDGE_DZ = os.environ.get("DGX_FUSE_EDGE_DZ", "1") == "1"
+# fp32 parity mode: conv5's GEMMs as 3 passes of the bf16 MFMA on split operands
+# (x = hi + lo, 16 significant bits each: hi.W_hi + hi.W_lo + lo.W_hi, ~2^-16
+# relative per product, fp32 sums) instead of the f32 MFMA, which runs at 1/16
+# of the bf16 rate (DGX_SPLIT32=0: the exact-product f32 MFMA GEMMs)
+SPLIT32 = os.environ.get("DGX_SPLIT32", "1") == "1"
 
 
 def debug_capture():
@@ -122,7 +127,7 @@ def opts():
     ``opts`` word (csrc/dgx_torch.cpp ``decode``)."""
     cap = max(0, min(255, int(G.SLAB_CAP_MB)))
     return (int(SCATTER_PACKED) | 2 * int(FOLD_BN_BWD) | 4 * int(FUSE_KNN_IMAGE) | 8 * int(FUSE_EDGE_DZ)
-            | (cap << 8))
+            | 16 * int(SPLIT32) | (cap << 8))
 
 
 PER_LAYER = 9   # saved per block: idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd

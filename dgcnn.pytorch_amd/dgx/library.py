@@ -403,7 +403,7 @@ def pointconv(X: Tensor, X16: Tensor, B: int, N: int, weight: Tensor, gamma: Ten
     t, f, i, g = bn_.op_args(spec)
     nt, tn = _pc_prep(prep, weight.shape[0], weight.shape[1])
     out, saved = torch.ops.dgx_host.pointconv_forward(X.float(), X16, B, N, weight, gamma, beta, t, f + [float(slope)],
-                                                      i, g, bf16, nt, tn)
+                                                      i, g, bf16, nt, tn, E.opts())
     return out, rm, rv, nb, list(saved[1:6])
 
 
@@ -429,8 +429,10 @@ def pointconv_backward(dout: Tensor, X: Tensor, X16: Tensor, weight: Tensor, sav
     nt, tn = (_pc_prep(prep, Co, K) if lds else (None, None))
     if lds and nt is None:
         nt, tn = G.prep_weight(weight, Co, K, False)
-    full = [X16 if lds else X.float(), *saved, nt if lds else e16, tn if lds else e16]
-    dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, full, weight, B, N, slope, not use_batch, "", bf16)
+    # fp32 mode: the backward op rebuilds the split-bf16 planes and weights from X
+    full = [X16 if lds else X.float(), *saved, nt if lds else e16, tn if lds else e16, e16, e16]
+    dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, full, weight, B, N, slope, not use_batch, "", bf16,
+                                                           E.opts())
     return dX.contiguous(), dW.contiguous(), dg, db
 
 

@@ -33,8 +33,9 @@ class _PointConvBNLReLU(torch.autograd.Function):
         t, f, i, g = bn_.op_args(bn)
         if X16 is None:
             X16 = torch.empty(0, dtype=torch.bfloat16, device=X.device)
+        from .edgeconv import opts
         out, saved = torch.ops.dgx_host.pointconv_forward(X.float(), X16, B, N, weight, gamma, beta, t,
-                                                          f + [float(slope)], i, g, bool(bf16), nt, tn)
+                                                          f + [float(slope)], i, g, bool(bf16), nt, tn, opts())
         ctx.meta = (B, N, float(slope), not bn_.mode(bn)[0], g, bool(bf16))
         ctx.save_for_backward(weight, *saved)
         return out
@@ -44,7 +45,8 @@ class _PointConvBNLReLU(torch.autograd.Function):
     def backward(ctx, dout):
         B, N, slope, ev, g, bf16 = ctx.meta
         weight, *saved = ctx.saved_tensors
-        dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, saved, weight, B, N, slope, ev, g, bf16)
+        from .edgeconv import opts
+        dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, saved, weight, B, N, slope, ev, g, bf16, opts())
         return dX, None, None, None, None, None, None, None, None, dW, dg, db
 
 

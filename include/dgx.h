@@ -393,6 +393,14 @@ int dgx_gemm_lds_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, in
                       int M, int N, int K, int a_k, int epi, int splits, float* C,
                       int64_t ldc, float* partials, const float* addend,
                       int64_t ldd, void* stream);
+/* fp32 (rows x cols, row stride lds) -> two bf16 planes (row stride ldo): hi =
+ * bf16(x) (nullable: skip), lo = bf16(x - hi) — x with 16 significant bits as
+ * hi + lo. The operands of the fp32 parity mode's 3-pass GEMMs (hi.W_hi +
+ * hi.W_lo + lo.W_hi on the bf16 MFMA, ~2^-16 relative per product) that stand
+ * in for the f32-MFMA conv5 GEMMs (dgcnn.py:74-78, 100-102). cols, lds, ldo
+ * multiples of 4, 16-byte aligned src. */
+int dgx_split_bf16(const float* src, int64_t lds, int64_t rows, int cols, void* hi, void* lo, int64_t ldo,
+                   void* stream);
 /* bf16 weight operands per step: nt = [rows][C], tn = its transpose. stacked
  * != 0: W is an EdgeConv weight (Co, 2C) (dgcnn.py:55) and rows = 2Co are
  * [W1; W2]; else W is (Co, C) (conv5, dgcnn.py:74). */
@@ -401,7 +409,8 @@ int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt,
 /* dgx_weight_prep_bf16 for n <= 8 weights in one launch (host arrays of
  * length n: one job per EdgeConv block of a forward). stacked[j] bit 0: an
  * EdgeConv weight as above; bit 1: nt is the split form [rows][2C] = [hi | lo]
- * (lo = bf16(w - hi)) for dgx_gemm_lds_bf16's a_k = C; tn stays hi only. */
+ * (lo = bf16(w - hi)) for dgx_gemm_lds_bf16's a_k = C; tn stays hi only
+ * unless bit 2 (value 4) is set: then tn is [C][2 rows] = [hi^T | lo^T]. */
 int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, const int* C, const int* stacked,
                                void* const* nt, void* const* tn, void* stream);
 
