@@ -11,13 +11,26 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Phase clock marks for tools/knn_lab.hip (compiled out of the library): wave
+// lane 0 records the cycle counter at phase boundaries into DGX_KNN_LAB_BUF.
+#ifdef DGX_KNN_LAB
+#define KNN_MARK(i)                                                                                   \
+    do {                                                                                              \
+        if ((threadIdx.x & 63) == 0)                                                                  \
+            DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (i)] = \
+                (long long)clock64();                                                                 \
+    } while (0)
+#else
+#define KNN_MARK(i) do { } while (0)
+#endif
+
 namespace dgx_knn {
 
-constexpr int KT = 32;                 // candidates per tile = queries per block (32x32 MFMA)
+constexpr int KT = 32;                // candidates per tile = queries per block (32x32 MFMA)
 constexpr int KP = 4;                  // candidate parts = waves per block (part p: tiles p, p+KP, ...)
 constexpr int KQ_THREADS = 64 * KP;
 constexpr int KQ_LISTS = 2 * KP;       // top-k lists per query: 2 lane halves x KP parts
-constexpr int KQ_QCAP = 16;            // per-lane pending-candidate FIFO (a half tile adds <= 8)
+constexpr int KQ_QCAP = 24;            // per-lane pending-candidate FIFO (a tile adds <= 16)
 
 // ------------------------------------------------------------- top-k list ----
 // Sorted (desc) list in registers, static indexing only. Candidates reach a
@@ -52,7 +65,6 @@ __device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[
 template <int KB>
 struct KnnList {
     static constexpr int KL = KB <= 16 ? 10 : (KB <= 20 ? 12 : (KB <= 32 ? 15 : (KB <= 40 ? 17 : 23)));
-    static constexpr int RPL = (KB + 1) / 2;   // ranks per lane of a wave's 2-list merge
 };
 
 // ------------------------------------------------------------ operand image --
@@ -117,7 +129,7 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
     for (int t = 0; t < NS; ++t) bq[t] = 2.0f * ib[img_at<NS>(qf >> 5, hh * 32 + (qf & 31), t)];
     __syncthreads();
     // act(v, j) on every candidate; the lanes of column 0 (lanes 0, 32) hold the tile's 32 rows
-    auto stream = [&](auto&& act) {
+    auto stream = [&](auto&& act) __attribute__((always_inline)) {
         for (int s = wave; s < ntile; s += KP) {
             f32x16 acc = {};
 #pragma unroll
@@ -142,7 +154,7 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
     });
     __syncthreads();
     const int ngt = cnt[0];
-    auto put = [&](int rank, int j, float v) {
+    auto put = [&](int rank, int j, float v) __attribute__((always_inline)) {
         if (idx64) idx64[row * k + rank] = j;
         if (idx32) idx32[row * k + rank] = j;
         if (vals) vals[row * k + rank] = v;
@@ -214,11 +226,14 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
 // The only block-wide synchronisation is the final merge.
 template <int NS>
 struct KnnStream {
-    static constexpr int UNIT = NS <= 8 ? NS : (NS == 64 ? 16 : 8);   // MFMA steps per ring unit
-    static constexpr int NU = NS / UNIT;                               // units per tile
-    static constexpr int RING = NS == 64 ? 2 : 4;                      // units in flight
-    static constexpr int UB = RING > NU ? RING : NU;                   // units per loop trip (static slots)
-    static_assert(UB % RING == 0 && UB % NU == 0, "unit split");
+    static constexpr int UNIT = NS <= 8 ? NS : 8;          // MFMA steps per ring unit
+    static constexpr int NU = NS / UNIT;                   // units per tile
+    static constexpr int RING = 4;                         // ring slots: loads run RING-1 units ahead
+    static constexpr int TT = RING / NU > 2 ? RING / NU : 2;   // tiles per loop trip (static slots, 2 accumulators)
+    // NS = 64: the query operand (64 VGPRs) is read from LDS one unit ahead instead
+    // of held in registers, which keeps the kernel within 256 VGPRs for every k
+    static constexpr bool BQL = NS == 64;
+    static_assert((TT * NU) % RING == 0 && TT % 2 == 0, "unit split");
 };
 
 // LDS after [pub KP x KT | xs ntile x KT]: the FIFO while streaming, then the
@@ -226,11 +241,13 @@ struct KnnStream {
 template <int KB>
 constexpr int knn_f_floats() {
     constexpr int fifo = KP * KQ_QCAP * 64 * 2;
-    constexpr int fix = KP * KT * KB * 2 + 2 * KT + 2 * FX_CAP + 8 + FIX_MAXN / 32;
+    constexpr int fix = KT * KQ_LISTS * (KnnList<KB>::KL + 1) * 2 + 3 * KT + 2 * FX_CAP + 8 + FIX_MAXN / 32;
     return fifo > fix ? fifo : fix;
 }
-template <int KB>
-inline size_t knn_lds_bytes(int N) { return ((size_t)KP * KT + (size_t)knn_ntile(N) * KT + knn_f_floats<KB>()) * 4; }
+template <int NS, int KB>
+inline size_t knn_lds_bytes(int N) {
+    return ((size_t)KP * KT + (size_t)knn_ntile(N) * KT + (NS == 64 ? 64 * NS : 0) + knn_f_floats<KB>()) * 4;
+}
 
 template <int NS, int KB>
 __global__ __launch_bounds__(KQ_THREADS, 2)
@@ -239,16 +256,18 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                 float* __restrict__ vals) {
 #pragma clang fp contract(off)
     constexpr int KL = KnnList<KB>::KL;
-    constexpr int RPL = KnnList<KB>::RPL;
     using SP = KnnStream<NS>;
-    constexpr int UNIT = SP::UNIT, NU = SP::NU, RING = SP::RING, UB = SP::UB;
+    constexpr int UNIT = SP::UNIT, NU = SP::NU, RING = SP::RING;
+    constexpr bool BQL = SP::BQL;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int b, qb;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
+    KNN_MARK(0);
     const int ntile = (N + KT - 1) / KT;
     float* pub = smem;                 // [KP][KT] published admission bounds
     float* xs = smem + KP * KT;        // [ntile][KT] the cloud's |x|^2 in tile row order
-    float* F = xs + ntile * KT;
+    float* bqs = xs + ntile * KT;      // [NS/4][64][4] the doubled query operand (BQL only)
+    float* F = bqs + (BQL ? 64 * NS : 0);
     float2* fifo = reinterpret_cast<float2*>(F);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -268,11 +287,18 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     if (tid < KP * KT) pub[tid] = -INFINITY;
     // B operand: the block's query tile, doubled — every product and partial sum
     // of the fmaf chain doubles exactly, so the MFMA returns fl(2 * dot) (dgcnn.py:7)
-    float bq[NS];
+    float bq[BQL ? 1 : NS];
     if constexpr (NS == 2) {
         const float2 v = *reinterpret_cast<const float2*>(ib + img_at<2>(qb, lane, 0));
         bq[0] = 2.0f * v.x;
         bq[1] = 2.0f * v.y;
+    } else if constexpr (BQL) {
+        // the whole block shares the query tile: staged once, doubled, in LDS
+        const float4* src = reinterpret_cast<const float4*>(ib + (int64_t)qb * 64 * NS);
+        for (int e = tid; e < 16 * NS; e += KQ_THREADS) {
+            const float4 v = src[e];
+            reinterpret_cast<float4*>(bqs)[e] = make_float4(2.0f * v.x, 2.0f * v.y, 2.0f * v.z, 2.0f * v.w);
+        }
     } else {
 #pragma unroll
         for (int c = 0; c < NS / 4; ++c) {
@@ -289,6 +315,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     float tseed = -INFINITY;
     const int ntl = (ntile - wave + KP - 1) / KP;   // this part's tiles: wave + KP * tl
     __syncthreads();
+    KNN_MARK(1);
     auto tile_xc = [&](int s, float (&xc)[16]) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -312,14 +339,14 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         float p[MM];
 #pragma unroll
         for (int t = 0; t < MM; ++t) p[t] = -INFINITY;
-        auto put = [&](float v) {
+        auto put = [&](float v) __attribute__((always_inline)) {
 #pragma unroll
             for (int t = MM - 1; t > 0; --t) p[t] = __builtin_amdgcn_fmed3f(p[t - 1], p[t], v);
             p[0] = fmaxf(p[0], v);
         };
         constexpr int PC = 4;   // tiles per chunk: the next chunk's operands in flight
         float2 av[2][PC];
-        auto fetch = [&](int buf, int tl0) {
+        auto fetch = [&](int buf, int tl0) __attribute__((always_inline)) {
 #pragma unroll
             for (int c = 0; c < PC; ++c) {
                 const int s = wave + KP * min(tl0 + c, ntl - 1);
@@ -365,6 +392,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         __syncthreads();   // every wave has read the pre-pass bounds before the main pass publishes
         if (q < N) tseed = T;
     }
+    KNN_MARK(2);
 
     // Each lane keeps the KL best of ITS candidates (sorted, registers, static
     // indexing). Admission filter thr = max(own KL-th, t2, T, seed): t2 = the
@@ -375,6 +403,9 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     // canonically at the merge. Candidates that pass wait in the lane's FIFO
     // and are inserted in batches, so an insertion round (5*KL VALU ops for the
     // whole wave) is paid once per admitted candidate of the busiest lane.
+#ifdef DGX_KNN_LAB
+    long long lab_flush = 0, lab_nflush = 0;   // in-stream flush cycles / count
+#endif
     float thr = tseed;
     float lv[KL];
     int li[KL];
@@ -382,7 +413,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     for (int t = 0; t < KL; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
     float2* fq = fifo + wave * (KQ_QCAP * 64) + lane;
     int cnt = 0;
-    auto flush = [&]() {
+    auto flush = [&]() __attribute__((always_inline)) {
         // branch-free rounds: slots past a lane's count read stale entries and
         // are replaced by -inf, so every round is the same straight-line code
         float2 c0 = fq[0];
@@ -420,23 +451,42 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     };
     // TAIL: the cloud's last tile when N % 32 != 0 (wave-uniform), the only one
     // whose rows can be padding (j >= N)
-    auto consider = [&](float dot, float xc, int j, auto tail) {
+#ifdef DGX_KNN_LAB_NOSEL
+    float lab_sink = 0.f;   // lab variant: the stream alone (the sink keeps the MFMAs live)
+    auto consider = [&](float dot, float xc, int j, auto tail) __attribute__((always_inline)) {
+        lab_sink = fmaxf(lab_sink, dot - xc);
+    };
+    auto consider_real = [&](float dot, float xc, int j, auto tail) __attribute__((always_inline)) {
+#else
+    auto consider = [&](float dot, float xc, int j, auto tail) __attribute__((always_inline)) {
+#endif
         const float tq = dot - xc;   // dot is already 2 x (query operand doubled)
         const float v = tq - xxq;
         const bool pass = (!decltype(tail)::value || j < N) && v >= thr;
         // unconditional store: a rejected candidate's slot is reused by the
-        // next one (a half tile adds at most 8 entries to a FIFO holding <= QCAP-8)
+        // next one (a tile adds at most 16 entries to a FIFO holding <= QCAP-16)
         fq[cnt * 64] = make_float2(v, __int_as_float(j));
         cnt += pass ? 1 : 0;
     };
 
     if (ntl > 0) {
-        // Every load is unconditional (a unit past the end re-reads this part's
-        // last tile, unused): with a data-dependent skip the compiler cannot count
-        // the loads in flight and drains them all (vmcnt(0)) every trip.
+        // Software pipeline over the part's tiles: the MFMA chain of tile i runs
+        // into one accumulator while the candidates of tile i-1 (the other one)
+        // are filtered into the FIFO in the same scheduling region, so the
+        // selection VALU issues in the shadow of the dependent MFMAs. Operand
+        // units stream through a RING-slot register ring, each loaded RING-1
+        // units ahead; a sched_barrier keeps every load at the head of its unit
+        // (the scheduler otherwise sinks the loads behind the chain, leaving no
+        // distance). Every load is unconditional (past the end it re-reads this
+        // part's last tile, unused), so the compiler counts the loads in flight
+        // exactly. TT tiles per trip keep the ring slot and accumulator static.
+        constexpr int TT = SP::TT;
         float a[RING][UNIT];
-        auto load = [&](int slot, int u, int sl) {
-            const int s = wave + KP * min(u / NU, ntl - 1);
+        f32x16 acc[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[1][r] = __builtin_nanf("");   // "tile -1": every compare fails
+        auto load = [&](int slot, int gu, int sl) __attribute__((always_inline)) {
+            const int s = wave + KP * min(gu / NU, ntl - 1);
             if constexpr (NS == 2) {
                 const float2 v = *reinterpret_cast<const float2*>(ib + img_at<2>(s, lane, 0));
                 a[slot][0] = v.x;
@@ -452,147 +502,221 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                 }
             }
         };
-        const int nunits = ntl * NU;
 #pragma unroll
-        for (int r = 0; r < RING; ++r) load(r, r, r % NU);
-        f32x16 acc = {};
+        for (int r = 0; r < RING - 1; ++r) load(r, r, r % NU);
+        float bqr[2][BQL ? UNIT : 1];   // BQL: the query operand of this unit and the next
+        auto load_bq = [&](int slot, int sl) __attribute__((always_inline)) {
+            if constexpr (BQL) {
+#pragma unroll
+                for (int c = 0; c < UNIT / 4; ++c) {
+                    const float4 v = *reinterpret_cast<const float4*>(bqs + ((sl * UNIT / 4 + c) * 64 + lane) * 4);
+                    bqr[slot][4 * c] = v.x;
+                    bqr[slot][4 * c + 1] = v.y;
+                    bqr[slot][4 * c + 2] = v.z;
+                    bqr[slot][4 * c + 3] = v.w;
+                }
+            }
+        };
+        load_bq(0, 0);
+        constexpr int CPN = 16 / NU;   // candidates of the previous tile filtered per unit
 #pragma unroll 1
-        for (int u = 0; u < nunits; u += UB) {
+        for (int tl0 = 0; tl0 < ntl; tl0 += TT) {
 #pragma unroll
-            for (int ub = 0; ub < UB; ++ub) {
-                const int slot = ub % RING, sl = ub % NU;
-                const bool live = UB == NU || u + ub < nunits;   // wave-uniform
-                if (live) {
-                    if (sl == 0) acc = f32x16{};
+            for (int t2 = 0; t2 < TT; ++t2) {
+                const int i = tl0 + t2;
+                const bool live = i < ntl;          // wave-uniform
+                f32x16& cur = acc[t2 & 1];
+                f32x16& prv = acc[(t2 & 1) ^ 1];
+                const int jb = (wave + KP * (i - 1)) * KT + 4 * hh;   // previous tile's rows
 #pragma unroll
-                    for (int t = 0; t < UNIT; ++t)
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[slot][t], bq[sl * UNIT + t], acc, 0, 0, 0);
-                }
-                load(slot, u + ub + RING, (ub + RING) % NU);
-                if (live && sl == NU - 1) {
-                    const int s = wave + KP * ((u + ub) / NU);
-                    float xc[16];
-                    tile_xc(s, xc);
-                    const int jb = s * KT + 4 * hh;
-                    auto half = [&](int r0, auto tail) {
+                for (int u = 0; u < NU; ++u) {
+                    const int pos = t2 * NU + u;
+                    load((pos + RING - 1) % RING, i * NU + u + RING - 1, (u + RING - 1) % NU);
+                    load_bq((pos + 1) & 1, (u + 1) % NU);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (live) {
+                        // |x_j|^2 of this unit's CPN rows of the previous tile: rows
+                        // acc_row(r, hh) for r in [u CPN, (u+1) CPN) come in runs of 4
+                        // (2 for CPN = 2), contiguous in the tile's xs row order
+                        float xcu[CPN];
+                        {
+                            const float* xr = xs + (wave + KP * max(i - 1, 0)) * KT + 4 * hh;
+                            if constexpr (CPN == 2) {
+                                const float2 v = *reinterpret_cast<const float2*>(xr + acc_row(u * CPN, 0));
+                                xcu[0] = v.x;
+                                xcu[1] = v.y;
+                            } else {
 #pragma unroll
-                        for (int r = r0; r < r0 + 8; ++r) consider(acc[r], xc[r], jb + acc_row(r, 0), tail);
-                        if (__any(cnt > KQ_QCAP - 8)) flush();
-                    };
-                    if ((s + 1) * KT > N) {
-                        half(0, std::true_type{});
-                        half(8, std::true_type{});
-                    } else {
-                        half(0, std::false_type{});
-                        half(8, std::false_type{});
+                                for (int g4 = 0; g4 < CPN / 4; ++g4) {
+                                    const float4 v = *reinterpret_cast<const float4*>(xr + acc_row(u * CPN + 4 * g4, 0));
+                                    xcu[4 * g4] = v.x;
+                                    xcu[4 * g4 + 1] = v.y;
+                                    xcu[4 * g4 + 2] = v.z;
+                                    xcu[4 * g4 + 3] = v.w;
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int t = 0; t < UNIT; ++t)
+                            cur = __builtin_amdgcn_mfma_f32_32x32x2f32(a[pos % RING][t],
+                                                                       BQL ? bqr[pos & 1][t] : bq[u * UNIT + t],
+                                                                       t == 0 && u == 0 ? f32x16{} : cur, 0, 0, 0);
+                        // branch-free for i = 0 too: the NaN-filled accumulator admits nothing
+#pragma unroll
+                        for (int c = 0; c < CPN; ++c) {
+                            const int r = u * CPN + c;
+                            consider(prv[r], xcu[c], jb + acc_row(r, 0), std::false_type{});
+                        }
                     }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // one flush site in the loop (the FIFO holds <= QCAP-16 + 16 entries here)
+                if (live && i > 0 && __any(cnt > KQ_QCAP - 16)) {
+#ifdef DGX_KNN_LAB
+                    const long long f0 = clock64();
+                    flush();
+                    lab_flush += clock64() - f0;
+                    ++lab_nflush;
+#else
+                    flush();
+#endif
                 }
             }
         }
+        // the part's last tile: the only one that can hold padding rows (j >= N)
+        {
+            const int s = wave + KP * (ntl - 1);
+            const f32x16 last = ((ntl - 1) & 1) ? acc[1] : acc[0];
+            float xc[16];
+            tile_xc(s, xc);
+            const int jb = s * KT + 4 * hh;
+            auto tile16 = [&](auto tail) __attribute__((always_inline)) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) consider(last[r], xc[r], jb + acc_row(r, 0), tail);
+            };
+            if ((s + 1) * KT > N) tile16(std::true_type{});
+            else tile16(std::false_type{});
+        }
     }
+#ifdef DGX_KNN_LAB
+#ifdef DGX_KNN_LAB_NOSEL
+    if (lab_sink == 12345.f) DGX_KNN_LAB_BUF[0] = 1;
+#endif
+    if ((threadIdx.x & 63) == 0) {
+        DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 16 + 12] = lab_flush;
+        DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 16 + 13] = lab_nflush;
+    }
+#endif
+    KNN_MARK(3);
     flush();
+    KNN_MARK(4);
 
-    // Merge the wave's 2 lists of each query (lanes ql, ql + 32) by k rounds of a
-    // canonical arg-max over the 2 list heads; the winning lane pops its head.
-    // Rank r ends up in lane half r % 2.
-    const float last = lv[KL - 1];
-    float ov[RPL];
-    int oj[RPL];
-#pragma unroll
-    for (int t = 0; t < RPL; ++t) { ov[t] = -INFINITY; oj[t] = 0x7fffffff; }
-#pragma unroll
-    for (int r = 0; r < KB; ++r) {
-        if (r < k) {
-            float hv = lv[0];
-            int hj = li[0];
-            const float pv = __shfl_xor(hv, 32);
-            const int pj = __shfl_xor(hj, 32);
-            if (canon_better(pv, pj, hv, hj)) { hv = pv; hj = pj; }
-            const bool pop = li[0] == hj && lv[0] == hv;
-#pragma unroll
-            for (int t = 0; t < KL - 1; ++t) {
-                lv[t] = pop ? lv[t + 1] : lv[t];
-                li[t] = pop ? li[t + 1] : li[t];
-            }
-            lv[KL - 1] = pop ? -INFINITY : lv[KL - 1];
-            li[KL - 1] = pop ? 0x7fffffff : li[KL - 1];
-            if ((r & 1) == hh) { ov[r >> 1] = hv; oj[r >> 1] = hj; }
-        }
-    }
-
-    // Merge the parts: each part's sorted top-k goes to LDS; an element's final
-    // rank is its rank in its own list plus, for every other part, the number of
-    // that part's elements that are canonically better (binary search). The
-    // parts hold disjoint candidates, so the ranks 0..k-1 are taken exactly once.
+    // Merge: the query's 8 sorted lists (2 lane halves x KP parts, disjoint
+    // candidates) go to LDS; then 8 lanes per query (tid = 8 query + list) run k
+    // rounds of a canonical arg-max over their list heads — a 3-step DPP
+    // reduction inside the lane octet — and the winning lane pops its head. Rank
+    // r lands in octet lane r % 8, so the rows are written 8 ranks at a time.
+    KNN_MARK(5);
     __syncthreads();  // every wave is done with its FIFO
-    float2* lists = reinterpret_cast<float2*>(F);    // [KP][KT][KB]
-    float* kth = F + KP * KT * KB * 2;               // [KT] merged k-th value
+    KNN_MARK(6);
+    constexpr int LS = KL + 1;                        // list stride: KL entries + a (-inf, max) sentinel
+    float2* lists = reinterpret_cast<float2*>(F);    // [KT][KQ_LISTS][LS]
+    float* kth = F + KT * KQ_LISTS * LS * 2;         // [KT] merged k-th value
     int* flg = reinterpret_cast<int*>(kth + KT);     // [KT] row needs the fix-up
-#pragma unroll
-    for (int t = 0; t < RPL; ++t) {
-        const int r = 2 * t + hh;
-        if (r < k) lists[(wave * KT + ql) * KB + r] = make_float2(ov[t], __int_as_float(oj[t]));
-    }
-    if (tid < KT) {
-        kth[tid] = -INFINITY;
-        flg[tid] = 0;
-    }
-    __syncthreads();
-    int rk[RPL];
-#pragma unroll
-    for (int t = 0; t < RPL; ++t) {
-        const int r = 2 * t + hh;
-        rk[t] = k;
-        if (r < k) {
-            int tot = r;
-#pragma unroll
-            for (int w = 0; w < KP; ++w) {
-                if (w == wave) continue;
-                const float2* other = lists + (w * KT + ql) * KB;
-                int lo = 0, hi = k;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    const float2 o = other[mid];
-                    if (canon_better(o.x, __float_as_int(o.y), ov[t], oj[t])) lo = mid + 1;
-                    else hi = mid;
-                }
-                tot += lo;
-            }
-            rk[t] = tot;
-            if (tot == k - 1) kth[ql] = ov[t];
-        }
-    }
-    __syncthreads();
+    float* seedv = kth + 2 * KT;                     // [KT] admission seed of the row
     {
-        // A lane whose list was full and whose last kept value reaches the merged
-        // k-th may have dropped a member of the true top-k: mark the row for the
-        // exact fix-up pass. Fewer than k candidates reaching the seed (the merged
-        // k-th is then a -inf pad) marks it too.
-        const float kv = kth[ql];
-        if (last != -INFINITY && last >= kv) flg[ql] = 1;
-        if (!(kv >= tseed)) flg[ql] = 1;
+        float2* my = lists + (ql * KQ_LISTS + wave * 2 + hh) * LS;
+#pragma unroll
+        for (int t = 0; t < KL; ++t) my[t] = make_float2(lv[t], __int_as_float(li[t]));
+        my[KL] = make_float2(-INFINITY, __int_as_float(0x7fffffff));
+        if (wave == 0 && hh == 0) seedv[ql] = tseed;
     }
     __syncthreads();
-    if (q < N && flg[ql] == 0) {  // flagged rows are written by the fix-up below
-        const int64_t row = ((int64_t)b * N + q) * k;
+    const int qm = tid >> 3, g = tid & 7;            // merge role: query qm, list g
+    {
+        const float2* L = lists + (qm * KQ_LISTS + g) * LS;
+        float2 h0 = L[0], h1 = L[1];
+        int pos = 1;                                  // list index of h1
+        const float lastv = L[KL - 1].x;
+        constexpr int RO = (KB + KQ_LISTS - 1) / KQ_LISTS;
+        float outv[RO];
+        int outj[RO];
 #pragma unroll
-        for (int t = 0; t < RPL; ++t) {
-            const int r = rk[t];
+        for (int t = 0; t < RO; ++t) { outv[t] = -INFINITY; outj[t] = 0x7fffffff; }
+        float kv = -INFINITY;
+        auto step = [&](float& v, int& j, auto ctrl) __attribute__((always_inline)) {
+            constexpr int C = decltype(ctrl)::value;
+            const float ov = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xf, 0xf, false));
+            const int oj = __builtin_amdgcn_update_dpp(0, j, C, 0xf, 0xf, false);
+            if (canon_better(ov, oj, v, j)) { v = ov; j = oj; }
+        };
+#pragma unroll
+        for (int r = 0; r < KB; ++r) {
             if (r < k) {
-                if (idx64) idx64[row + r] = oj[t];
-                if (idx32) idx32[row + r] = oj[t];
-                if (vals) vals[row + r] = ov[t];
+                const int hj = __float_as_int(h0.y);
+                float bv = h0.x;
+                int bj = hj;
+                step(bv, bj, std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]: lane ^ 1
+                step(bv, bj, std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]: lane ^ 2
+                step(bv, bj, std::integral_constant<int, 0x141>{});   // row_half_mirror: the other quad
+                const float2 nx = L[min(pos + 1, KL)];
+                const bool pop = hj == bj;                // candidates are in exactly one list
+                h0 = pop ? h1 : h0;
+                h1 = pop ? nx : h1;
+                pos += pop ? 1 : 0;
+                if ((r & 7) == g) { outv[r >> 3] = bv; outj[r >> 3] = bj; }
+                if (r == k - 1) kv = bv;
+            }
+        }
+        // A list that was full and whose last kept value reaches the merged k-th
+        // may have dropped a member of the true top-k: the row goes to the exact
+        // fix-up pass. Fewer than k candidates reaching the seed (the merged k-th
+        // is then a -inf pad) sends it there too.
+        int bad = (lastv != -INFINITY && lastv >= kv) ? 1 : 0;
+        bad |= __builtin_amdgcn_update_dpp(0, bad, 0xB1, 0xf, 0xf, false);
+        bad |= __builtin_amdgcn_update_dpp(0, bad, 0x4E, 0xf, 0xf, false);
+        bad |= __builtin_amdgcn_update_dpp(0, bad, 0x141, 0xf, 0xf, false);
+        if (!(kv >= seedv[qm])) bad = 1;
+        if (g == 0) {
+            kth[qm] = kv;
+            flg[qm] = bad;
+        }
+        const int qr = qb * KT + qm;
+        if (qr < N && !bad) {  // flagged rows are written by the fix-up below
+            const int64_t row = ((int64_t)b * N + qr) * k;
+#pragma unroll
+            for (int t = 0; t < RO; ++t) {
+                const int r = 8 * t + g;
+                if (r < k) {
+                    if (idx64) idx64[row + r] = outj[t];
+                    if (idx32) idx32[row + r] = outj[t];
+                    if (vals) vals[row + r] = outv[t];
+                }
             }
         }
     }
+    KNN_MARK(7);
+    __syncthreads();
+    KNN_MARK(8);
     // the block's flagged rows (rare), one at a time; flg / kth are block-uniform LDS reads
-    float* fixa = F + KP * KT * KB * 2 + 2 * KT;
+    float* fixa = F + KT * KQ_LISTS * LS * 2 + 3 * KT;
+#ifdef DGX_KNN_LAB
+    int nfix = 0;
+#endif
     for (int f = 0; f < KT; ++f) {
         const int qf = qb * KT + f;
-        if (flg[f] != 0 && qf < N)
+        if (flg[f] != 0 && qf < N) {
             knn_fix_row<NS>(fixa, ib, xs, N, k, qf, xx[(int64_t)b * N + qf], kth[f], (int64_t)b * N + qf, idx64,
                             idx32, vals);
+#ifdef DGX_KNN_LAB
+            ++nfix;
+#endif
+        }
     }
+    KNN_MARK(9);
+#ifdef DGX_KNN_LAB
+    if ((threadIdx.x & 63) == 0) DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 16 + 15] = nfix;
+#endif
 }
 
 template <int NS, int KB>
@@ -600,7 +724,7 @@ int launch_knn(const float* xx, int B, int N, int k, int64_t* idx64, int32_t* id
                const float* xximg, hipStream_t st) {
     const int nqb = knn_ntile(N);
     hipLaunchKernelGGL((knn_kernel<NS, KB>), dim3(dgx_xcd_cloud_grid(B, nqb)), dim3(KQ_THREADS),
-                       knn_lds_bytes<KB>(N), st, img, xximg, xx, B, N, k, nqb, idx64, idx32, vals);
+                       (knn_lds_bytes<NS, KB>(N)), st, img, xximg, xx, B, N, k, nqb, idx64, idx32, vals);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -26,6 +26,8 @@ def main():
     posemb = mode.startswith("posemb")
     if mode == "net_syncbn_amp":
         return net_syncbn_amp(rank, world, out_dir, dev)
+    if mode == "dgcnn_syncbn_amp":
+        return dgcnn_syncbn_amp(rank, world, out_dir, dev)
     if posemb:  # PositionEmbedding (a6) as main_partseg_dist.py converts Net's modules
         model = PositionEmbedding(types.SimpleNamespace(k=10))
         with torch.no_grad():
@@ -46,6 +48,40 @@ def main():
     torch.cuda.synchronize()
     res = {"y": y.detach().cpu(),
            "grads": {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None},
+           "running": {n: b.detach().cpu() for n, b in model.named_buffers()}}
+    torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+AMP_ARGS = dict(emb_dim=512, k=40)   # DGCNN as Net's emb_nn builds it at cfg4 (main_partseg_dist.py:534)
+AMP_B, AMP_N = 2, 2048
+
+
+def amp_inputs(world):
+    from dgx import synth
+    pts = synth.cube_clouds(AMP_B * world, AMP_N, 41)
+    g = torch.from_numpy(synth.uniform(42, (AMP_B * world, AMP_ARGS["emb_dim"], AMP_N)) - 0.5).float()
+    return pts, g
+
+
+def dgcnn_syncbn_amp(rank, world, out_dir, dev):
+    """DGCNN (the engine) converted with SyncBatchNorm under DDP, forward under
+    fp16 autocast (main_partseg_dist.py:189-196, 253): bf16 GEMMs, BatchNorm
+    statistics of the global batch all-reduced from the C++ op."""
+    from models.dgcnn import DGCNN
+    torch.manual_seed(0)
+    model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(DGCNN(types.SimpleNamespace(**AMP_ARGS))).to(dev).train()
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
+    pts, g = amp_inputs(world)
+    sl = slice(rank * AMP_B, (rank + 1) * AMP_B)
+    x = torch.from_numpy(pts[sl]).to(dev).permute(0, 2, 1)
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = ddp(x)
+    (y.float() * g[sl].to(dev)).sum().backward()
+    torch.cuda.synchronize()
+    res = {"y": y.detach().float().cpu(),
+           "grads": {n: p.grad.detach().float().cpu() for n, p in model.named_parameters()},
            "running": {n: b.detach().cpu() for n, b in model.named_buffers()}}
     torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
