@@ -17,7 +17,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define KNN_MARK(i)                                                                                   \
     do {                                                                                              \
         if ((threadIdx.x & 63) == 0)                                                                  \
-            DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (i)] = \
+            DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (i)] = \
                 (long long)clock64();                                                                 \
     } while (0)
 #else
@@ -30,42 +30,6 @@ constexpr int KT = 32;                // candidates per tile = queries per block
 constexpr int KP = 4;                  // candidate parts = waves per block (part p: tiles p, p+KP, ...)
 constexpr int KQ_THREADS = 64 * KP;
 constexpr int KQ_LISTS = 2 * KP;       // top-k lists per query: 2 lane halves x KP parts
-constexpr int KQ_QCAP = 24;            // per-lane pending-candidate FIFO (a tile adds <= 16)
-
-// ------------------------------------------------------------- top-k list ----
-// Sorted (desc) list in registers, static indexing only. Candidates reach a
-// lane in ascending index order, so a strict '>' keeps earlier (smaller) indices
-// ahead of equal values: canonical tie order for free.
-template <int KMAX>
-__device__ __forceinline__ void list_insert_ordered(float (&v)[KMAX], int (&id)[KMAX], float nv, int nj) {
-    // Shift insert from the tail: slot q takes slot q-1 if the new value beats
-    // v[q-1], else the new value if it beats v[q], else keeps its own. Every
-    // compare uses the NEW value against the original list, so elements of
-    // equal value keep their relative order (a carried-element bubble would
-    // swap equal neighbours). One lane mask live per step.
-    // For a sorted list the new slot q value is median(v[q-1], v[q], nv): one
-    // v_med3_f32 per slot (ties keep the value, the ids follow the compares).
-    bool gt_cur = nv > v[KMAX - 1];
-#pragma unroll
-    for (int q = KMAX - 1; q > 0; --q) {
-        const bool gt_prev = nv > v[q - 1];
-        v[q] = __builtin_amdgcn_fmed3f(v[q - 1], v[q], nv);
-        id[q] = gt_prev ? id[q - 1] : (gt_cur ? nj : id[q]);
-        gt_cur = gt_prev;
-    }
-    v[0] = gt_cur ? nv : v[0];
-    id[0] = gt_cur ? nj : id[0];
-}
-
-// Per-lane list length for k <= KB. A query's candidates are dealt over
-// KQ_LISTS = 8 lists (2 lane halves x 4 parts, interleaved by index), so the
-// true top-k splits ~Binomial(k, 1/8) over its lists; KL is where that
-// distribution's upper tail drops to ~2e-6 per list. A lane needing more than
-// KL slots flags its row, which is recomputed exactly (knn_fix_row).
-template <int KB>
-struct KnnList {
-    static constexpr int KL = KB <= 16 ? 10 : (KB <= 20 ? 12 : (KB <= 32 ? 15 : (KB <= 40 ? 17 : 23)));
-};
 
 // ------------------------------------------------------------ operand image --
 // MFMA operands of v_mfma_f32_32x32x2_f32 for 32-candidate tiles: step t of a
@@ -233,20 +197,46 @@ struct KnnStream {
     // NS = 64: the query operand (64 VGPRs) is read from LDS one unit ahead instead
     // of held in registers, which keeps the kernel within 256 VGPRs for every k
     static constexpr bool BQL = NS == 64;
-    static_assert((TT * NU) % RING == 0 && TT % 2 == 0, "unit split");
 };
 
-// LDS after [pub KP x KT | xs ntile x KT]: the FIFO while streaming, then the
-// merge lists, k-th values, flags and the fix-up's scratch
+// Per-lane list depth KL for k <= KB. A query's candidates are dealt over
+// KQ_LISTS = 8 lists (2 lane halves x 4 parts, interleaved by index), so its
+// true top-k splits ~Binomial(k, 1/8) over them; KL is where the chance that a
+// list holds >= KL of them drops below ~5e-4 per row. Such a row (the list may
+// have dropped a member) is recomputed exactly (knn_fix_row).
 template <int KB>
+struct KnnList {
+    static constexpr int KL = KB <= 16 ? 9 : (KB <= 20 ? 10 : (KB <= 32 ? 13 : (KB <= 40 ? 15 : 20)));
+};
+// A lane's candidate log: compacted (to <= KL entries, the lane's own top-KL
+// bounding it) whenever a chunk of candidates leaves it holding more than
+// KL + KH; the KH slots of headroom make compactions rare once the lane's list
+// has settled. Chunk = one unit's candidates (16 / NU), at most 8.
+constexpr int KH = 8;
+template <int NS>
+constexpr int knn_chunk() { return 16 / KnnStream<NS>::NU > 8 ? 8 : 16 / KnnStream<NS>::NU; }
+template <int NS, int KB>
+constexpr int knn_qcap() { return KnnList<KB>::KL + KH + knn_chunk<NS>(); }
+
+// LDS after [pub KP x KT | xs ntile x KT | bqs]: the final stage's small arrays
+// (Tq, row flags, overflow flags, survivor counts, staged rows), then the candidate logs
+// while streaming and ranking, which the fix-up's scratch aliases afterwards
+// the final bound counts each list's top-(m + 2) values (8 (m + 2) > k, so the
+// k-th of their union is tighter than the lists' smallest m-th value)
+template <int KB>
+constexpr int knn_mm() { return (KB + KQ_LISTS - 1) / KQ_LISTS + 2 < KnnList<KB>::KL ? (KB + KQ_LISTS - 1) / KQ_LISTS + 2 : KnnList<KB>::KL; }
+template <int KB>
+constexpr int knn_small_floats() { return 18 * KT + 4 + KT * KB + KT * KQ_LISTS * knn_mm<KB>() + KT; }
+template <int NS, int KB>
 constexpr int knn_f_floats() {
-    constexpr int fifo = KP * KQ_QCAP * 64 * 2;
-    constexpr int fix = KT * KQ_LISTS * (KnnList<KB>::KL + 1) * 2 + 3 * KT + 2 * FX_CAP + 8 + FIX_MAXN / 32;
-    return fifo > fix ? fifo : fix;
+    constexpr int SMALL_FLOATS = knn_small_floats<KB>();
+    constexpr int logs = KP * knn_qcap<NS, KB>() * 64 * 2;
+    constexpr int fix = 2 * FX_CAP + 8 + FIX_MAXN / 32;
+    return SMALL_FLOATS + (logs > fix ? logs : fix);
 }
 template <int NS, int KB>
 inline size_t knn_lds_bytes(int N) {
-    return ((size_t)KP * KT + (size_t)knn_ntile(N) * KT + (NS == 64 ? 64 * NS : 0) + knn_f_floats<KB>()) * 4;
+    return ((size_t)KP * KT + (size_t)knn_ntile(N) * KT + (NS == 64 ? 64 * NS : 0) + knn_f_floats<NS, KB>()) * 4;
 }
 
 template <int NS, int KB>
@@ -255,10 +245,11 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                 int N, int k, int nqb, int64_t* __restrict__ idx64, int32_t* __restrict__ idx32,
                 float* __restrict__ vals) {
 #pragma clang fp contract(off)
-    constexpr int KL = KnnList<KB>::KL;
     using SP = KnnStream<NS>;
     constexpr int UNIT = SP::UNIT, NU = SP::NU, RING = SP::RING;
     constexpr bool BQL = SP::BQL;
+    constexpr int QCAP = knn_qcap<NS, KB>();
+    constexpr int KL = KnnList<KB>::KL;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int b, qb;
     if (!dgx_xcd_cloud_map(blockIdx.x, B, nqb, b, qb)) return;
@@ -268,7 +259,9 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     float* xs = smem + KP * KT;        // [ntile][KT] the cloud's |x|^2 in tile row order
     float* bqs = xs + ntile * KT;      // [NS/4][64][4] the doubled query operand (BQL only)
     float* F = bqs + (BQL ? 64 * NS : 0);
-    float2* fifo = reinterpret_cast<float2*>(F);
+    constexpr int SMALL_FLOATS = knn_small_floats<KB>();
+    float* small = F;
+    float2* logs = reinterpret_cast<float2*>(F + SMALL_FLOATS);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     // wave-uniform in a scalar register: the part's tile count and every "unit
@@ -280,7 +273,6 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     const float* __restrict__ xib = xximg + (int64_t)b * ntile * KT;
     const int q = qb * KT + ql;
     const int m = (k + KQ_LISTS - 1) / KQ_LISTS;   // every list's m-th value: 8 m >= k candidates reach their min
-    const int m2 = (k + 1) / 2;                    // the wave's two lists' m2-th: 2 m2 >= k
 
     for (int e = tid * 4; e < ntile * KT; e += KQ_THREADS * 4)
         *reinterpret_cast<float4*>(xs + e) = *reinterpret_cast<const float4*>(xib + e);
@@ -394,77 +386,92 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     }
     KNN_MARK(2);
 
-    // Each lane keeps the KL best of ITS candidates (sorted, registers, static
-    // indexing). Admission filter thr = max(own KL-th, t2, T, seed): t2 = the
-    // wave's two lists' min m2-th value (2 m2 >= k candidates reach it), T = the
-    // query's 8 lists' min m-th value (the other parts' through `pub`, a value
-    // published at their last flush: lists only improve, so a stale value is
-    // still a lower bound). '>=' keeps equal values; their order is settled
-    // canonically at the merge. Candidates that pass wait in the lane's FIFO
-    // and are inserted in batches, so an insertion round (5*KL VALU ops for the
-    // whole wave) is paid once per admitted candidate of the busiest lane.
+    // Selection state of a lane (one of the query's 8 candidate lists: 2 lane
+    // halves x KP parts). Admitted candidates are appended to the lane's LOG (LDS,
+    // index order, never sorted); `tl` holds the top KL logged VALUES (one v_med3
+    // per slot per entry, no index bookkeeping while streaming). Admission and
+    // the log's compaction use adm = max(thr, tl[KL-1]):
+    //   thr = max(seed, T), T = min over the query's 8 lists of their m-th value
+    //   (m = ceil(k/8): 8 m >= k candidates reach T, a lower bound of the row's
+    //   k-th value; read through `pub`, where a stale entry is still a bound);
+    //   tl[KL-1]: a candidate below the lane's own KL-th value is in the top-k
+    //   only if the lane holds >= KL members, and then the row is flagged at the
+    //   end and recomputed (knn_fix_row).
+    // At the end the survivors (>= the final T) of the 8 logs are ranked by
+    // counting.
 #ifdef DGX_KNN_LAB
-    long long lab_flush = 0, lab_nflush = 0;   // in-stream flush cycles / count
+    long long lab_flush = 0, lab_nflush = 0;   // in-stream fold/compact cycles / count
 #endif
     float thr = tseed;
-    float lv[KL];
-    int li[KL];
+    float tl[KL];
 #pragma unroll
-    for (int t = 0; t < KL; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
-    float2* fq = fifo + wave * (KQ_QCAP * 64) + lane;
-    int cnt = 0;
-    auto flush = [&]() __attribute__((always_inline)) {
-        // branch-free rounds: slots past a lane's count read stale entries and
-        // are replaced by -inf, so every round is the same straight-line code
-        float2 c0 = fq[0];
-        float cv = cnt > 0 ? c0.x : -INFINITY;
-        int cj = __float_as_int(c0.y);
-        // fully unrolled with an early exit: no loop-carried copies of the list
+    for (int t = 0; t < KL; ++t) tl[t] = -INFINITY;
+    float adm = thr;  // admission threshold max(thr, tl[KL-1]); NaN once the log overflowed
+    float2* fq = logs + wave * (QCAP * 64) + lane;   // this lane's log: entry e at fq[64 e]
+    int cnt = 0;      // entries in the log
+    int done = 0;     // entries folded into tl
+    bool ovf = false; // the log could not hold the lane's candidates: the row is recomputed
+    // (the round loops below stay rolled: every inlined copy of an unrolled one
+    // would cost ~QCAP x KL instructions of I-cache in the stream loop)
+    auto fold = [&]() __attribute__((always_inline)) {
+        // rounds = the busiest lane's new entries; lanes past their count fold -inf
+#pragma unroll 1
+        for (int t = 0; t < QCAP; ++t) {
+            if (!__any(done + t < cnt)) break;
+            const float v = done + t < cnt ? fq[min(done + t, QCAP - 1) * 64].x : -INFINITY;
 #pragma unroll
-        for (int t = 0; t < KQ_QCAP; ++t) {
-            if (!__any(t < cnt)) break;
-            const int nx = min(t + 1, KQ_QCAP - 1);
-            const float2 n0 = fq[nx * 64];
-            const float nv = t + 1 < cnt ? n0.x : -INFINITY;
-            const int nj = __float_as_int(n0.y);
-            list_insert_ordered<KL>(lv, li, cv >= thr ? cv : -INFINITY, cj);
-            cv = nv;
-            cj = nj;
+            for (int u = KL - 1; u > 0; --u) tl[u] = __builtin_amdgcn_fmed3f(tl[u - 1], tl[u], v);
+            tl[0] = fmaxf(tl[0], v);
         }
-        cnt = 0;
-        float tm = lv[0], t2 = lv[0];
+        done = cnt;
+        float tm = tl[0];
 #pragma unroll
-        for (int t = 1; t < KL; ++t) {
-            tm = (t == m - 1) ? lv[t] : tm;
-            t2 = (t == m2 - 1) ? lv[t] : t2;
-        }
-        if (m2 > KL) t2 = -INFINITY;   // the two lists cannot certify k candidates
+        for (int t = 1; t < KL; ++t) tm = (t == m - 1) ? tl[t] : tm;
         tm = fminf(tm, __shfl_xor(tm, 32));
-        t2 = fminf(t2, __shfl_xor(t2, 32));
         if (hh == 0) __hip_atomic_store(pub + wave * KT + ql, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         float T = tm;
 #pragma unroll
         for (int w = 0; w < KP; ++w)
             if (w != wave)
                 T = fminf(T, __hip_atomic_load(pub + w * KT + ql, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        thr = fmaxf(fmaxf(fmaxf(t2, T), lv[KL - 1]), tseed);
+        thr = fmaxf(thr, T);
+        adm = ovf ? __builtin_nanf("") : fmaxf(thr, tl[KL - 1]);   // NaN: admits nothing
+    };
+    auto compact = [&]() __attribute__((always_inline)) {
+        // keep the entries >= adm, in order (write position <= read position)
+        int w = 0;
+#pragma unroll 1
+        for (int t = 0; t < QCAP; ++t) {
+            if (!__any(t < cnt)) break;
+            const float2 e = fq[t * 64];
+            fq[w * 64] = e;
+            w += (t < cnt && e.x >= adm) ? 1 : 0;
+        }
+        cnt = w;
+        done = w;
+        if (cnt > KL + KH) {   // ties at the KL-th value fill the log: stop admitting, recompute the row
+            ovf = true;
+            adm = __builtin_nanf("");
+            cnt = 0;
+            done = 0;
+        }
     };
     // TAIL: the cloud's last tile when N % 32 != 0 (wave-uniform), the only one
     // whose rows can be padding (j >= N)
 #ifdef DGX_KNN_LAB_NOSEL
     float lab_sink = 0.f;   // lab variant: the stream alone (the sink keeps the MFMAs live)
-    auto consider = [&](float dot, float xc, int j, auto tail) __attribute__((always_inline)) {
+    auto consider = [&](float dot, float xc, int j, float th, auto tail) __attribute__((always_inline)) {
         lab_sink = fmaxf(lab_sink, dot - xc);
     };
-    auto consider_real = [&](float dot, float xc, int j, auto tail) __attribute__((always_inline)) {
+    auto consider_real = [&](float dot, float xc, int j, float th, auto tail) __attribute__((always_inline)) {
 #else
-    auto consider = [&](float dot, float xc, int j, auto tail) __attribute__((always_inline)) {
+    auto consider = [&](float dot, float xc, int j, float th, auto tail) __attribute__((always_inline)) {
 #endif
         const float tq = dot - xc;   // dot is already 2 x (query operand doubled)
         const float v = tq - xxq;
-        const bool pass = (!decltype(tail)::value || j < N) && v >= thr;
+        const bool pass = (!decltype(tail)::value || j < N) && v >= th;
         // unconditional store: a rejected candidate's slot is reused by the
-        // next one (a tile adds at most 16 entries to a FIFO holding <= QCAP-16)
+        // next one (a unit adds at most 16 / NU entries to a log holding <= KL)
         fq[cnt * 64] = make_float2(v, __int_as_float(j));
         cnt += pass ? 1 : 0;
     };
@@ -519,12 +526,15 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         };
         load_bq(0, 0);
         constexpr int CPN = 16 / NU;   // candidates of the previous tile filtered per unit
+        constexpr int CH = knn_chunk<NS>();   // ... in chunks of CH between log checks
 #pragma unroll 1
         for (int tl0 = 0; tl0 < ntl; tl0 += TT) {
 #pragma unroll
             for (int t2 = 0; t2 < TT; ++t2) {
                 const int i = tl0 + t2;
                 const bool live = i < ntl;          // wave-uniform
+                // every trip runs the same straight-line MFMA code (past the end on the
+                // clamped last tile, unused): no accumulator phi copies at unit ends
                 f32x16& cur = acc[t2 & 1];
                 f32x16& prv = acc[(t2 & 1) ^ 1];
                 const int jb = (wave + KP * (i - 1)) * KT + 4 * hh;   // previous tile's rows
@@ -534,13 +544,13 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                     load((pos + RING - 1) % RING, i * NU + u + RING - 1, (u + RING - 1) % NU);
                     load_bq((pos + 1) & 1, (u + 1) % NU);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (live) {
-                        // |x_j|^2 of this unit's CPN rows of the previous tile: rows
-                        // acc_row(r, hh) for r in [u CPN, (u+1) CPN) come in runs of 4
-                        // (2 for CPN = 2), contiguous in the tile's xs row order
-                        float xcu[CPN];
+                    // |x_j|^2 of this unit's CPN rows of the previous tile: rows
+                    // acc_row(r, hh) for r in [u CPN, (u+1) CPN) come in runs of 4
+                    // (2 for CPN = 2), contiguous in the tile's xs row order
+                    float xcu[CPN];
+                    {
                         {
-                            const float* xr = xs + (wave + KP * max(i - 1, 0)) * KT + 4 * hh;
+                            const float* xr = xs + (wave + KP * min(max(i - 1, 0), ntl - 1)) * KT + 4 * hh;
                             if constexpr (CPN == 2) {
                                 const float2 v = *reinterpret_cast<const float2*>(xr + acc_row(u * CPN, 0));
                                 xcu[0] = v.x;
@@ -561,26 +571,47 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                             cur = __builtin_amdgcn_mfma_f32_32x32x2f32(a[pos % RING][t],
                                                                        BQL ? bqr[pos & 1][t] : bq[u * UNIT + t],
                                                                        t == 0 && u == 0 ? f32x16{} : cur, 0, 0, 0);
-                        // branch-free for i = 0 too: the NaN-filled accumulator admits nothing
+                        // branch-free for i = 0 too (the NaN-filled accumulator admits
+                        // nothing) and past the part's end (a NaN bound admits nothing,
+                        // not even a +inf value)
+                        const float adm_live = live ? adm : __builtin_nanf("");
 #pragma unroll
-                        for (int c = 0; c < CPN; ++c) {
+                        for (int c = 0; c < CH; ++c) {
                             const int r = u * CPN + c;
-                            consider(prv[r], xcu[c], jb + acc_row(r, 0), std::false_type{});
+                            consider(prv[r], xcu[c], jb + acc_row(r, 0), adm_live, std::false_type{});
                         }
                     }
                     __builtin_amdgcn_sched_barrier(0);
-                }
-                // one flush site in the loop (the FIFO holds <= QCAP-16 + 16 entries here)
-                if (live && i > 0 && __any(cnt > KQ_QCAP - 16)) {
+                    // the log holds <= KL + KH + CH entries after a chunk: compact it
+                    // when it has no room for the next one
+                    auto check = [&]() __attribute__((always_inline)) {
+                        if (__any(cnt > KL + KH)) {
 #ifdef DGX_KNN_LAB
-                    const long long f0 = clock64();
-                    flush();
-                    lab_flush += clock64() - f0;
-                    ++lab_nflush;
-#else
-                    flush();
+                            const long long f0 = clock64();
 #endif
+                            fold();
+                            compact();
+#ifdef DGX_KNN_LAB
+                            lab_flush += clock64() - f0;
+                            ++lab_nflush;
+#endif
+                        }
+                    };
+                    check();
+                    // the unit's further chunks (16-candidate units: NU = 1)
+#pragma unroll
+                    for (int ch = 1; ch < CPN / CH; ++ch) {
+                        const float adm_live = live ? adm : __builtin_nanf("");
+#pragma unroll
+                        for (int c = 0; c < CH; ++c) {
+                            const int r = u * CPN + ch * CH + c;
+                            consider(prv[r], xcu[ch * CH + c], jb + acc_row(r, 0), adm_live, std::false_type{});
+                        }
+                        check();
+                    }
                 }
+                // fold the previous tile's admissions: publish the bound early
+                if (live && i > 0 && __any(cnt > done)) fold();
             }
         }
         // the part's last tile: the only one that can hold padding rows (j >= N)
@@ -591,8 +622,19 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
             tile_xc(s, xc);
             const int jb = s * KT + 4 * hh;
             auto tile16 = [&](auto tail) __attribute__((always_inline)) {
+                // in chunks of CH candidates, the log compacted between them as in the stream
 #pragma unroll
-                for (int r = 0; r < 16; ++r) consider(last[r], xc[r], jb + acc_row(r, 0), tail);
+                for (int u = 0; u < 16 / CH; ++u) {
+#pragma unroll
+                    for (int c = 0; c < CH; ++c) {
+                        const int r = u * CH + c;
+                        consider(last[r], xc[r], jb + acc_row(r, 0), adm, tail);
+                    }
+                    if (u + 1 < 16 / CH && __any(cnt > KL + KH)) {
+                        fold();
+                        compact();
+                    }
+                }
             };
             if ((s + 1) * KT > N) tile16(std::true_type{});
             else tile16(std::false_type{});
@@ -603,119 +645,233 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     if (lab_sink == 12345.f) DGX_KNN_LAB_BUF[0] = 1;
 #endif
     if ((threadIdx.x & 63) == 0) {
-        DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 16 + 12] = lab_flush;
-        DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 16 + 13] = lab_nflush;
+        DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 32 + 24] = lab_flush;
+        DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 32 + 25] = lab_nflush;
     }
 #endif
     KNN_MARK(3);
-    flush();
+    if (__any(cnt > done)) fold();
     KNN_MARK(4);
 
-    // Merge: the query's 8 sorted lists (2 lane halves x KP parts, disjoint
-    // candidates) go to LDS; then 8 lanes per query (tid = 8 query + list) run k
-    // rounds of a canonical arg-max over their list heads — a 3-step DPP
-    // reduction inside the lane octet — and the winning lane pops its head. Rank
-    // r lands in octet lane r % 8, so the rows are written 8 ranks at a time.
-    KNN_MARK(5);
-    __syncthreads();  // every wave is done with its FIFO
-    KNN_MARK(6);
-    constexpr int LS = KL + 1;                        // list stride: KL entries + a (-inf, max) sentinel
-    float2* lists = reinterpret_cast<float2*>(F);    // [KT][KQ_LISTS][LS]
-    float* kth = F + KT * KQ_LISTS * LS * 2;         // [KT] merged k-th value
-    int* flg = reinterpret_cast<int*>(kth + KT);     // [KT] row needs the fix-up
-    float* seedv = kth + 2 * KT;                     // [KT] admission seed of the row
+    // Final threshold of the row. Every list published its final m-th value, so
+    // min over the 8 lists (and the seed) bounds the row's k-th value from below;
+    // tighter: the k-th largest of the 8 lists' top-m2 values (m2 = min(m + 2, KL):
+    // 8 m2 > k distinct candidates), counted by the octet of lanes of the query
+    // (tid = 8 query + list). Tq = the larger of the two. Every top-k member of a list that is
+    // not flagged below is in its log and >= Tq. Each lane then keeps its
+    // survivors (v >= Tq) in place as 64-bit canonical keys: (order-preserving
+    // bits of v) << 32 | ~j, so "canonically better" (value desc, index asc) is
+    // one unsigned compare; the octet ranks list g's survivors against all 8
+    // lists by counting: rank r < k is row slot r, staged in LDS.
+    float* kth = small;                                        // [KT] the row's Tq
+    int* flg = reinterpret_cast<int*>(small + KT);             // [KP] per wave: flagged rows of its 8 queries
+    int* scnt = reinterpret_cast<int*>(small + 2 * KT + 4);    // [KT][8] survivors per list
+    float* klv = small + 10 * KT + 4;                          // [KT][8] each list's KL-th value
+    int* ostage = reinterpret_cast<int*>(small + 18 * KT + 4); // [KT][KB] the rows' indices by rank
+    constexpr int MM = knn_mm<KB>();
+    float* tlq = small + 18 * KT + 4 + KT * KB;                // [KT][8][MM] each list's top-MM values
+    float* t2q = tlq + KT * KQ_LISTS * MM;                     // [KT] k-th of the lists' top-m values
     {
-        float2* my = lists + (ql * KQ_LISTS + wave * 2 + hh) * LS;
+        float* d = tlq + (ql * KQ_LISTS + wave * 2 + hh) * MM;
 #pragma unroll
-        for (int t = 0; t < KL; ++t) my[t] = make_float2(lv[t], __int_as_float(li[t]));
-        my[KL] = make_float2(-INFINITY, __int_as_float(0x7fffffff));
-        if (wave == 0 && hh == 0) seedv[ql] = tseed;
+        for (int t = 0; t < MM; ++t) d[t] = tl[t];
     }
-    __syncthreads();
-    const int qm = tid >> 3, g = tid & 7;            // merge role: query qm, list g
+    KNN_MARK(5);
+    __syncthreads();   // every list's final m-th value and top-MM values are published
+    KNN_MARK(6);
+    const int qm = tid >> 3, g = tid & 7;                      // octet role: query qm, list g
     {
-        const float2* L = lists + (qm * KQ_LISTS + g) * LS;
-        float2 h0 = L[0], h1 = L[1];
-        int pos = 1;                                  // list index of h1
-        const float lastv = L[KL - 1].x;
-        constexpr int RO = (KB + KQ_LISTS - 1) / KQ_LISTS;
-        float outv[RO];
-        int outj[RO];
+        // count, for each of list g's top-m values, the values >= it over the 8
+        // lists' top-m; the largest one reaching k is a valid bound
+        const float* tq = tlq + qm * KQ_LISTS * MM;
+        const int m2 = min(m + 2, KL);
+        float mine[MM];
 #pragma unroll
-        for (int t = 0; t < RO; ++t) { outv[t] = -INFINITY; outj[t] = 0x7fffffff; }
-        float kv = -INFINITY;
-        auto step = [&](float& v, int& j, auto ctrl) __attribute__((always_inline)) {
-            constexpr int C = decltype(ctrl)::value;
-            const float ov = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xf, 0xf, false));
-            const int oj = __builtin_amdgcn_update_dpp(0, j, C, 0xf, 0xf, false);
-            if (canon_better(ov, oj, v, j)) { v = ov; j = oj; }
-        };
+        for (int t = 0; t < MM; ++t) mine[t] = tq[g * MM + t];
+        int cnt_ge[MM];
 #pragma unroll
-        for (int r = 0; r < KB; ++r) {
-            if (r < k) {
-                const int hj = __float_as_int(h0.y);
-                float bv = h0.x;
-                int bj = hj;
-                step(bv, bj, std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]: lane ^ 1
-                step(bv, bj, std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]: lane ^ 2
-                step(bv, bj, std::integral_constant<int, 0x141>{});   // row_half_mirror: the other quad
-                const float2 nx = L[min(pos + 1, KL)];
-                const bool pop = hj == bj;                // candidates are in exactly one list
-                h0 = pop ? h1 : h0;
-                h1 = pop ? nx : h1;
-                pos += pop ? 1 : 0;
-                if ((r & 7) == g) { outv[r >> 3] = bv; outj[r >> 3] = bj; }
-                if (r == k - 1) kv = bv;
+        for (int t = 0; t < MM; ++t) cnt_ge[t] = 0;
+#pragma unroll
+        for (int l = 0; l < KQ_LISTS; ++l) {
+#pragma unroll
+            for (int u = 0; u < MM; ++u) {
+                const float o = u < m2 ? tq[l * MM + u] : -INFINITY;
+#pragma unroll
+                for (int t = 0; t < MM; ++t) cnt_ge[t] += o >= mine[t] ? 1 : 0;
             }
         }
-        // A list that was full and whose last kept value reaches the merged k-th
-        // may have dropped a member of the true top-k: the row goes to the exact
-        // fix-up pass. Fewer than k candidates reaching the seed (the merged k-th
-        // is then a -inf pad) sends it there too.
-        int bad = (lastv != -INFINITY && lastv >= kv) ? 1 : 0;
-        bad |= __builtin_amdgcn_update_dpp(0, bad, 0xB1, 0xf, 0xf, false);
-        bad |= __builtin_amdgcn_update_dpp(0, bad, 0x4E, 0xf, 0xf, false);
-        bad |= __builtin_amdgcn_update_dpp(0, bad, 0x141, 0xf, 0xf, false);
-        if (!(kv >= seedv[qm])) bad = 1;
-        if (g == 0) {
-            kth[qm] = kv;
-            flg[qm] = bad;
-        }
-        const int qr = qb * KT + qm;
-        if (qr < N && !bad) {  // flagged rows are written by the fix-up below
-            const int64_t row = ((int64_t)b * N + qr) * k;
+        float best = -INFINITY;
 #pragma unroll
-            for (int t = 0; t < RO; ++t) {
-                const int r = 8 * t + g;
-                if (r < k) {
-                    if (idx64) idx64[row + r] = outj[t];
-                    if (idx32) idx32[row + r] = outj[t];
-                    if (vals) vals[row + r] = outv[t];
-                }
-            }
-        }
+        for (int t = 0; t < MM; ++t)
+            if (t < m2 && cnt_ge[t] >= k) best = fmaxf(best, mine[t]);
+        best = fmaxf(best, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(best), 0xB1, 0xf, 0xf, false)));
+        best = fmaxf(best, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(best), 0x4E, 0xf, 0xf, false)));
+        best = fmaxf(best, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(best), 0x141, 0xf, 0xf, false)));
+        if (g == 0) t2q[qm] = best;
     }
     KNN_MARK(7);
     __syncthreads();
     KNN_MARK(8);
+    {
+        float Tq = pub[ql];
+#pragma unroll
+        for (int w = 1; w < KP; ++w) Tq = fminf(Tq, pub[w * KT + ql]);
+        Tq = fmaxf(fmaxf(Tq, tseed), t2q[ql]);
+        uint64_t* fk = reinterpret_cast<uint64_t*>(fq);
+        int sc = 0;
+#pragma unroll 1
+        for (int t = 0; t < QCAP; ++t) {
+            if (!__any(t < cnt)) break;
+            const float2 e = fq[t * 64];
+            const float v = e.x + 0.0f;   // -0 -> +0: keys order like the float compare
+            const uint32_t u = __float_as_uint(v);
+            const uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+            fk[sc * 64] = ((uint64_t)ord << 32) | (uint32_t)~__float_as_uint(e.y);
+            sc += (t < cnt && e.x >= Tq) ? 1 : 0;
+        }
+        const int li = ql * KQ_LISTS + wave * 2 + hh;
+        scnt[li] = sc;
+        klv[li] = ovf ? INFINITY : tl[KL - 1];   // an overflowed list flags its row below
+        if (wave == 0 && hh == 0) kth[ql] = Tq;
+    }
+    KNN_MARK(9);
+    __syncthreads();
+    KNN_MARK(10);
+    {
+        const uint64_t* lg = reinterpret_cast<const uint64_t*>(logs);
+        auto col = [&](int l) __attribute__((always_inline)) {   // list l of query qm
+            return lg + (l >> 1) * (QCAP * 64) + (l & 1) * 32 + qm;
+        };
+        int sl[KQ_LISTS];
+        int c = 0, ns = 0;
+#pragma unroll
+        for (int l = 0; l < KQ_LISTS; ++l) {
+            sl[l] = scnt[qm * KQ_LISTS + l];
+            c += sl[l];
+            ns = l == g ? sl[l] : ns;
+        }
+        const int qr = qb * KT + qm;
+#ifdef DGX_KNN_LAB
+        {   // survivors per row (c, counted by octet leaders) and per list (ns), summed over the wave
+            int sc_ = (g == 0 && qr < N) ? c : 0, sn_ = qr < N ? ns : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                sc_ += __shfl_xor(sc_, o);
+                sn_ += __shfl_xor(sn_, o);
+            }
+            if (lane == 0) {
+                DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 32 + 26] = sc_;
+                DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 32 + 27] = sn_;
+            }
+        }
+#endif
+        // the k-th value of the row (rank k - 1), for the flag test below
+        uint64_t kkey = 0ull;
+        if (qr < N && c >= k) {
+            // EPL own survivors per sweep against every survivor of the row, two
+            // independent LDS reads per trip (padding keys 0 are never better)
+            constexpr int EPL = 4;
+            const uint64_t* mine = col(g);
+            for (int i0 = 0; i0 < ns; i0 += EPL) {
+                uint64_t key[EPL];
+                int rk[EPL];
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) {
+                    key[i] = i0 + i < ns ? mine[(i0 + i) * 64] : ~0ull;
+                    rk[i] = 0;
+                }
+#pragma unroll
+                for (int l = 0; l < KQ_LISTS; ++l) {
+                    const uint64_t* o = col(l);
+                    for (int u = 0; u < sl[l]; u += 2) {
+                        const uint64_t o0 = o[u * 64];
+                        const uint64_t o1 = u + 1 < sl[l] ? o[(u + 1) * 64] : 0ull;
+#pragma unroll
+                        for (int i = 0; i < EPL; ++i) rk[i] += (o0 > key[i] ? 1 : 0) + (o1 > key[i] ? 1 : 0);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) {
+                    if (i0 + i < ns && rk[i] < k) {
+                        ostage[qm * KB + rk[i]] = (int)~(uint32_t)key[i];
+                        if (vals) {
+                            const uint32_t ord = (uint32_t)(key[i] >> 32);
+                            vals[((int64_t)b * N + qr) * k + rk[i]] =
+                                __uint_as_float((ord & 0x80000000u) ? (ord & 0x7fffffffu) : ~ord);
+                        }
+                    }
+                    if (i0 + i < ns && rk[i] == k - 1) kkey = key[i];
+                }
+            }
+        }
+        KNN_MARK(11);
+        // octet max: every lane gets the k-th key (0 when the row has < k survivors)
+        auto omax = [&](uint64_t v, auto ctrl) __attribute__((always_inline)) {
+            constexpr int C = decltype(ctrl)::value;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, C, 0xf, 0xf, false);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), C, 0xf, 0xf, false);
+            const uint64_t o = ((uint64_t)hi << 32) | lo;
+            return o > v ? o : v;
+        };
+        kkey = omax(kkey, std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]: lane ^ 1
+        kkey = omax(kkey, std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]: lane ^ 2
+        kkey = omax(kkey, std::integral_constant<int, 0x141>{});   // row_half_mirror: the other quad
+        // A list whose KL-th value reaches the row's k-th value may have dropped a
+        // member (it admitted and kept only values >= its KL-th): the row goes to
+        // the exact fix-up, as does a row with fewer than k survivors.
+        const uint32_t kord = (uint32_t)(kkey >> 32);
+        const float kv = __uint_as_float((kord & 0x80000000u) ? (kord & 0x7fffffffu) : ~kord);
+        const float lk = klv[qm * KQ_LISTS + g];
+        const bool mine_bad = c < k || (lk != -INFINITY && lk >= kv);
+        {   // the wave's 8 row flags (octet o = lanes 8o..8o+7) as one byte
+            const uint64_t bm = __ballot(mine_bad && qr < N);
+            uint32_t m8 = 0;
+#pragma unroll
+            for (int o = 0; o < 8; ++o) m8 |= ((bm >> (8 * o)) & 0xffull) != 0 ? (1u << o) : 0u;
+            if (lane == 0) flg[wave] = (int)m8;
+        }
+    }
+    KNN_MARK(12);
+    __syncthreads();
+    KNN_MARK(13);
+    {   // the block's rows are consecutive in the output: 32 k entries, written
+        // coalesced (flagged rows are left to the fix-up)
+        uint32_t fm = 0;
+#pragma unroll
+        for (int w = 0; w < KP; ++w) fm |= (uint32_t)flg[w] << (8 * w);
+        const int nrow = min(KT, N - qb * KT);
+        const int64_t base = ((int64_t)b * N + qb * KT) * k;
+        for (int e = tid; e < nrow * k; e += KQ_THREADS) {
+            const int r = e / k, s2 = e - r * k;
+            if ((fm >> r) & 1u) continue;
+            const int j = ostage[r * KB + s2];
+            if (idx64) idx64[base + e] = j;
+            if (idx32) idx32[base + e] = j;
+        }
+    }
+    KNN_MARK(14);
     // the block's flagged rows (rare), one at a time; flg / kth are block-uniform LDS reads
-    float* fixa = F + KT * KQ_LISTS * LS * 2 + 3 * KT;
+    float* fixa = F + SMALL_FLOATS;   // aliases the logs, done with
 #ifdef DGX_KNN_LAB
     int nfix = 0;
 #endif
-    for (int f = 0; f < KT; ++f) {
+    uint32_t fmask = 0;   // block-uniform: the flagged rows of the block
+#pragma unroll
+    for (int w = 0; w < KP; ++w) fmask |= (uint32_t)flg[w] << (8 * w);
+    fmask = __builtin_amdgcn_readfirstlane(fmask);
+    while (fmask != 0u) {
+        const int f = __ffs(fmask) - 1;
+        fmask &= fmask - 1u;
         const int qf = qb * KT + f;
-        if (flg[f] != 0 && qf < N) {
-            knn_fix_row<NS>(fixa, ib, xs, N, k, qf, xx[(int64_t)b * N + qf], kth[f], (int64_t)b * N + qf, idx64,
-                            idx32, vals);
+        knn_fix_row<NS>(fixa, ib, xs, N, k, qf, xx[(int64_t)b * N + qf], kth[f], (int64_t)b * N + qf, idx64, idx32,
+                        vals);
 #ifdef DGX_KNN_LAB
-            ++nfix;
+        ++nfix;
 #endif
-        }
     }
-    KNN_MARK(9);
+    KNN_MARK(15);
 #ifdef DGX_KNN_LAB
-    if ((threadIdx.x & 63) == 0) DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 16 + 15] = nfix;
+    if ((threadIdx.x & 63) == 0) DGX_KNN_LAB_BUF[((int64_t)blockIdx.x * KP + wave) * 32 + 28] = nfix;
 #endif
 }
 

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void bwd16_dz_lt_kernel(const float* __restric
 // block: per-thread sums over its 4 points, then over the 32 lanes of its
 // channel group (one shuffle tree), one partial row per block.
 constexpr int RS_LT = 2;
-__global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __restrict__ dout,
+__global__ __launch_bounds__(256, 4) void bwd16_stats_lt_kernel(const float* __restrict__ dout,
                                                              const bf16* __restrict__ Z, int N, int C,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift,
@@ -309,20 +309,21 @@ __global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __rest
                                                              const float* __restrict__ invstd, float slope,
                                                              float* __restrict__ partials) {
     __shared__ __attribute__((aligned(16))) bf16 zt[RT_P * ZT_LD];
+    __shared__ __attribute__((aligned(16))) float4 cst[64];   // per channel {scale, shift, mean, invstd}
     const int nt = (N + RT_P * RS_LT - 1) / (RT_P * RS_LT);
     const int b = blockIdx.x / nt;
     const int nb = (blockIdx.x - b * nt) * RT_P * RS_LT;
     const int o0 = blockIdx.y * 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int pg = lane & 31, cg = 2 * w + (lane >> 5);
-    float a[8], sh[8], mu[8], is[8], s1[8], s2[8];
+    if (threadIdx.x < 64) {
+        const int oj = min(o0 + (int)threadIdx.x, C - 1);
+        cst[threadIdx.x] = make_float4(scale[oj], shift[oj], mean[oj], invstd[oj]);
+    }
+    // the channel constants come from LDS at each use (they would hold 32 VGPRs)
+    float s1[8], s2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int oj = min(o0 + 8 * cg + j, C - 1);
-        a[j] = scale[oj];
-        sh[j] = shift[oj];
-        mu[j] = mean[oj];
-        is[j] = invstd[oj];
         s1[j] = 0.f;
         s2[j] = 0.f;
     }
@@ -345,11 +346,12 @@ __global__ __launch_bounds__(256) void bwd16_stats_lt_kernel(const float* __rest
         read_z48(zt, pg, cg, z);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+            const float4 k4 = cst[8 * cg + j];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float d = g[j][i] * (fmaf(a[j], z[i][j], sh[j]) > 0.f ? 1.f : slope);
+                const float d = g[j][i] * (fmaf(k4.x, z[i][j], k4.y) > 0.f ? 1.f : slope);
                 s1[j] += d;
-                s2[j] = fmaf(d, (z[i][j] - mu[j]) * is[j], s2[j]);
+                s2[j] = fmaf(d, (z[i][j] - k4.z) * k4.w, s2[j]);
             }
         }
     }

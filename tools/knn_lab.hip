@@ -19,7 +19,9 @@ using namespace dgx_knn;
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-static const char* kPhase[9] = {"xs+seed", "prepass", "stream", "flush", "2-merge", "barrier", "rank", "write", "fixup"};
+constexpr int NPH = 15;
+static const char* kPhase[NPH] = {"xs+seed", "prepass", "stream", "final-fold", "tl-publish", "bar1", "T2", "bar2",
+                                 "keys", "bar3", "rank", "flags", "bar4", "copy", "fixup"};
 
 template <int NS, int KB>
 void run_case(const char* name, int B, int N, int C, int k, bool cube, int reps) {
@@ -47,7 +49,7 @@ void run_case(const char* name, int B, int N, int C, int k, bool cube, int reps)
     int32_t* didx;
     long long* dlab;
     const int grid = dgx_xcd_cloud_grid(B, ntile);
-    const size_t nlab = (size_t)grid * KP * 16;
+    const size_t nlab = (size_t)grid * KP * 32;
     CHECK(hipMalloc(&dimg, img.size() * 4));
     CHECK(hipMalloc(&dxximg, xximg.size() * 4));
     CHECK(hipMalloc(&dxx, xx.size() * 4));
@@ -74,26 +76,51 @@ void run_case(const char* name, int B, int N, int C, int k, bool cube, int reps)
     CHECK(hipEventSynchronize(e1));
     float ms;
     CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipMemset(dlab, 0, nlab * 8));   // one instrumented launch: marks and counters of a single call
+    launch();
+    CHECK(hipDeviceSynchronize());
     std::vector<long long> lab(nlab);
     CHECK(hipMemcpy(lab.data(), dlab, nlab * 8, hipMemcpyDeviceToHost));
     std::vector<int32_t> idx((size_t)B * N * k);
     CHECK(hipMemcpy(idx.data(), didx, idx.size() * 4, hipMemcpyDeviceToHost));
     uint64_t h = 1469598103934665603ull;
     for (int32_t v : idx) h = (h ^ (uint32_t)v) * 1099511628211ull;
-    double ph[9] = {0};
-    double tot = 0, fl = 0, nfl = 0;
+    // structural check: every row holds k distinct indices in [0, N)
+    int badrows = 0;
+    for (int row = 0; row < B * N; ++row) {
+        std::vector<char> seen(N, 0);
+        bool ok = true;
+        for (int t = 0; t < k; ++t) {
+            const int j = idx[(size_t)row * k + t];
+            if (j < 0 || j >= N || seen[j]) { ok = false; break; }
+            seen[j] = 1;
+        }
+        if (!ok) {
+            if (badrows < 3) {
+                printf("   bad row b=%d q=%d (block qb=%d):", row / N, row % N, (row % N) / KT);
+                for (int t = 0; t < std::min(k, 10); ++t) printf(" %d", idx[(size_t)row * k + t]);
+                printf("\n");
+            }
+            ++badrows;
+        }
+    }
+    if (badrows) printf("   %d structurally bad rows\n", badrows);
+    double ph[NPH] = {0};
+    double tot = 0, fl = 0, nfl = 0, sc = 0, sns = 0;
     long long fix = 0;
     int nw = 0;
     for (int blk = 0; blk < grid; ++blk) {
-        const long long* m0 = &lab[(size_t)blk * KP * 16];
+        const long long* m0 = &lab[(size_t)blk * KP * 32];
         if (m0[0] == 0) continue;   // padding block
-        fix += m0[15];
+        fix += m0[28];
         for (int w = 0; w < KP; ++w) {
-            const long long* m = m0 + w * 16;
-            for (int i = 0; i < 9; ++i) ph[i] += (double)(m[i + 1] - m[i]);
-            tot += (double)(m[9] - m[0]);
-            fl += (double)m[12];
-            nfl += (double)m[13];
+            const long long* m = m0 + w * 32;
+            for (int i = 0; i < NPH; ++i) ph[i] += (double)(m[i + 1] - m[i]);
+            tot += (double)(m[NPH] - m[0]);
+            fl += (double)m[24];
+            sc += (double)m[26];
+            sns += (double)m[27];
+            nfl += (double)m[25];
             ++nw;
         }
     }
@@ -101,8 +128,9 @@ void run_case(const char* name, int B, int N, int C, int k, bool cube, int reps)
     printf("%-16s NS=%2d KB=%2d  %8.2f us  %6.1f TF/s  fixrows=%lld  hash=%016llx\n", name, NS, KB, ms / reps * 1e3,
            flops / (ms / reps * 1e-3) / 1e12, fix, (unsigned long long)h);
     printf("   cycles/wave: total %.0f |", tot / nw);
-    for (int i = 0; i < 9; ++i) printf(" %s %.0f", kPhase[i], ph[i] / nw);
-    printf(" | in-stream flushes %.2f taking %.0f\n", nfl / nw, fl / nw);
+    for (int i = 0; i < NPH; ++i) printf(" %s %.0f", kPhase[i], ph[i] / nw);
+    printf(" | in-stream compactions %.2f taking %.0f | survivors/row %.1f /list %.2f\n", nfl / nw, fl / nw,
+           sc / (B * N), sns / (B * N * 8.0));
     CHECK(hipFree(dimg));
     CHECK(hipFree(dxximg));
     CHECK(hipFree(dxx));
@@ -112,6 +140,14 @@ void run_case(const char* name, int B, int N, int C, int k, bool cube, int reps)
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    if (argc > 2) {   // small ragged shapes, repeated: structural checks only
+        for (int r = 0; r < 5; ++r) {
+            run_case<8, 64>("C12 N100 k50", 2, 100, 12, 50, false, 3);
+            run_case<32, 40>("C33 N777 k33", 2, 777, 33, 33, false, 3);
+            run_case<2, 16>("C3 N77 k1", 2, 77, 3, 1, true, 3);
+        }
+        return 0;
+    }
     run_case<2, 20>("C3 N1024 k20", 32, 1024, 3, 20, true, reps);
     run_case<32, 20>("C64 N1024 k20", 32, 1024, 64, 20, false, reps);
     run_case<64, 20>("C128 N1024 k20", 32, 1024, 128, 20, false, reps);
