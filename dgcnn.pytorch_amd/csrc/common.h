@@ -16,16 +16,30 @@ static inline hipStream_t dgx_stream(void* s) { return reinterpret_cast<hipStrea
 
 // XCD-aware block -> work-item map (MI355X_MICROARCH.md: blocks b and b+8 share
 // an XCD). Items are (cloud, tile) pairs; all tiles of one cloud get the same
-// block residue mod 8 so the cloud's rows are served from one XCD's L2.
-// grid = 8 * ceil(B/8) * tiles; returns false for padding blocks.
+// block residue mod 8 so the cloud's rows are served from one XCD's L2:
+// grid = 8 * ceil(B/8) * tiles. A batch of fewer than 8 clouds (a strong-scaling
+// shard) would leave 8 - B XCDs with padding blocks only, so there each cloud
+// takes rep = 8 / B XCDs, each a contiguous range of ceil(tiles / rep) of its
+// tiles: grid = 8 * ceil(tiles / rep). Returns false for padding blocks.
+__host__ __device__ __forceinline__ int dgx_xcd_rep(int B) { return B >= 8 ? 1 : 8 / B; }
 __device__ __forceinline__ bool dgx_xcd_cloud_map(int block, int B, int tiles, int& b, int& tile) {
-    int xcd = block & 7, r = block >> 3;
-    int bl = r / tiles;
-    tile = r - bl * tiles;
-    b = bl * 8 + xcd;
-    return b < B;
+    const int xcd = block & 7, r = block >> 3;
+    const int rep = dgx_xcd_rep(B);
+    if (rep == 1) {
+        const int bl = r / tiles;
+        tile = r - bl * tiles;
+        b = bl * 8 + xcd;
+        return b < B;
+    }
+    const int per = (tiles + rep - 1) / rep;
+    b = xcd / rep;
+    tile = (xcd - b * rep) * per + r;
+    return b < B && r < per && tile < tiles;
 }
-static inline int dgx_xcd_cloud_grid(int B, int tiles) { return 8 * ((B + 7) / 8) * tiles; }
+static inline int dgx_xcd_cloud_grid(int B, int tiles) {
+    const int rep = dgx_xcd_rep(B);
+    return rep == 1 ? 8 * ((B + 7) / 8) * tiles : 8 * ((tiles + rep - 1) / rep);
+}
 
 // (cloud, point part, channel slice) work items of the EdgeConv gather/scatter
 // kernels: every block of one cloud gets the same residue mod 8 (one XCD) and

@@ -38,7 +38,9 @@ def test_version_and_errors():
     # |x|^2 (B*N floats) + operand image per cloud: 32-point tiles x 64 lanes x NS = ceil(C/2) (rounded
     # to 2, 4, 8, ...) MFMA steps + 32 norms per tile (C=64: 32 tiles x 64 x 32 + 32 x 32)
     assert L.dgx_knn_workspace_bytes(2, 64, 1024) == 2 * 1024 * 4 + 2 * (32 * 64 * 32 + 32 * 32) * 4
-    assert L.dgx_knn_image_bytes(2, 3, 1000) == 2 * (32 * 64 * 2 + 32 * 32) * 4
+    # |x|^2 (B*N floats) + operand image (64 tiles x 64 lanes x 16 floats + 64 x 16 norms per cloud at C=64)
+    assert L.dgx_knn_workspace_bytes(2, 64, 1024) == 2 * 1024 * 4 + 2 * (64 * 64 * 16 + 64 * 16) * 4
+    assert L.dgx_knn_image_bytes(2, 3, 1000) == 2 * (63 * 64 * 1 + 63 * 16) * 4
 
 
 def test_host_tensors_take_the_cpu_path_without_libdgx(monkeypatch):

@@ -257,8 +257,10 @@ def test_net_cfg4_routed(cuda, amp, monkeypatch):
         E.set_debug_capture(None)
         for h in hooks:
             h.remove()
-    # decisions: DGCNN blocks, edge stage, max over points, HOG
-    dec = validate_dgcnn_decisions(cap, src, k, init_emb)
+    # decisions: DGCNN blocks, edge stage, max over points, HOG. Under autocast
+    # the engine's DGCNN GEMMs run in bf16 (dgx.precision.effective): its
+    # decisions are checked against the bf16-operand recomputation
+    dec = validate_dgcnn_decisions(cap, src, k, init_emb, bf16=amp)
     dgcnn_dec = [(i.long(), a, z) for (i, a, z) in (cap[("fwd", l)] for l in range(4))]
     zpos1, arg2, zpos2, edec = edge_mlp_decisions(cap, B, N, k, net.pos_mlp[0].conv2[0].weight)
     eidx = cap["emlp"]["idx"].view(B, N, k).long()
