@@ -281,7 +281,10 @@ def test_net_cfg4_routed(cuda, amp, monkeypatch):
     t3 = runs["f64"][2]
     gap_n = float((t3.max(dim=-1)[0] - torch.gather(t3, 2, argmax_n.unsqueeze(-1)).squeeze(-1)).max()
                   / t3.abs().max())
-    assert gap_n <= (2e-3 if amp else 1e-5), ("max over points", gap_n)
+    # under autocast the engine's DGCNN and edge-MLP GEMMs run in bf16 (8 significant
+    # bits, unit roundoff 2^-9): a near-tied max over points may pick a point whose
+    # fp64 value trails the maximum by a few bf16 ulps of the scale
+    assert gap_n <= (1e-2 if amp else 1e-5), ("max over points", gap_n)
     ref = runs["f64"][0].cpu()
     e_out = rel_err(out.detach().float().cpu(), ref)
     assert e_out < (AMP_TOL if amp else TOL), ("out", e_out)
