@@ -66,6 +66,7 @@ struct Opts {
   bool fuse_edge_dz = true;  // bf16: block l-1's dz from block l's dX GEMM epilogue
   int64_t slab_cap_mb = 8;   // split-K slab cap of small weight gradients (0 = off)
   bool split32 = true;       // fp32 mode: conv5 GEMMs as 3-pass split bf16 (hi.hi + hi.lo + lo.hi)
+  bool push = false;         // backward scatter: selected-edge dz pushed from the sources (fixed-point LDS sums)
 };
 Opts decode(int64_t o) {
   Opts r;
@@ -75,6 +76,7 @@ Opts decode(int64_t o) {
   r.fuse_edge_dz = o & 8;
   r.slab_cap_mb = (o >> 8) & 0xff;
   r.split32 = o & 16;
+  r.push = o & 32;
   return r;
 }
 
@@ -884,7 +886,18 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
     Tensor dPQ = at::empty({M, 2 * co}, bf16 ? d.bf16 : d.f32);
     Tensor dgamma, dbeta, c0, c1;
     const bool fold = st.group.empty() && o.fold_bwd;
-    if (fold) {   // BN backward finalize in the scatter's prologue (one launch)
+    if (fold && o.push) {   // BN backward finalize in the push scatter's prologue (one launch)
+      dgamma = at::empty({co}, d.f32);
+      dbeta = at::empty({co}, d.f32);
+      c0 = at::empty({co}, d.f32);
+      c1 = at::empty({co}, d.f32);
+      check(dgx_edge_bwd_scatter_push_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(s[0]), P<int32_t>(rowptr[li]),
+                                          P<int32_t>(edges[li]), P(dz), packed ? nullptr : P<uint8_t>(arg), P(sumP),
+                                          B, N, k, co, P(partials), nblk, count, P(st.scale), P(st.mean),
+                                          P(st.invstd), (int)st.eval, P(dgamma), P(dbeta), P(c0), P(c1),
+                                          dPQ.data_ptr(), (int)bf16, (int)packed, d.stream),
+            "edge bwd scatter");
+    } else if (fold) {   // BN backward finalize in the scatter's prologue (one launch)
       dgamma = at::empty({co}, d.f32);
       dbeta = at::empty({co}, d.f32);
       c0 = at::empty({co}, d.f32);
@@ -900,7 +913,13 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
       dbeta = r[1];
       c0 = r[2];
       c1 = r[3];
-      if (packed)
+      if (o.push)
+        check(dgx_edge_bwd_scatter_push_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(s[0]), P<int32_t>(rowptr[li]),
+                                            P<int32_t>(edges[li]), P(dz), packed ? nullptr : P<uint8_t>(arg), P(sumP),
+                                            B, N, k, co, nullptr, 0, 0.0, P(st.scale), nullptr, nullptr, 0, nullptr,
+                                            nullptr, P(c0), P(c1), dPQ.data_ptr(), (int)bf16, (int)packed, d.stream),
+              "edge bwd scatter");
+      else if (packed)
         check(dgx_edge_bwd_scatter_packed_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(rowptr[li]), P<int32_t>(edges[li]),
                                               P(dz), P(sumP), B, N, k, co, P(st.scale), P(c0), P(c1), dPQ.data_ptr(),
                                               (int)bf16, d.stream),
@@ -1052,10 +1071,32 @@ std::array<Tensor, 4> pointconv_backward_impl(const Dev& d, Tensor dout, const P
   const int B = s.B, N = s.N;
   dout = dout.to(at::kFloat).contiguous();
   const bool z16 = is16(s.Z);
+  const Stats& st = s.st;
+  const int64_t K = s.Xop.size(1);
+  if (!s.bf16 && s.xhi.defined() && s.Z.is_contiguous() && Co % 4 == 0) {
+    // fp32 mode, split GEMMs: two passes over (dout, Z) — BN-backward reductions,
+    // then dZ straight into its split-bf16 planes (no fp32 dz / dZ round trip)
+    const int rows = dgx_pointconv_bf16_rows(B, N);
+    Tensor partials = at::empty({rows, 2, Co}, d.f32);
+    check(dgx_pointconv_bwd_split_f32(P(dout), P(s.Z), B, N, Co, P(st.scale), P(st.shift), P(st.mean), P(st.invstd),
+                                      (float)s.slope, nullptr, nullptr, P(partials), nullptr, nullptr, 0, d.stream),
+          "pointconv bwd stats f32");
+    auto cs = backward_consts(d, partials, rows, (double)M, st);
+    Tensor zhi = at::empty({M, Co}, d.bf16), zlo = at::empty({M, Co}, d.bf16);
+    check(dgx_pointconv_bwd_split_f32(P(dout), P(s.Z), B, N, Co, P(st.scale), P(st.shift), nullptr, nullptr,
+                                      (float)s.slope, P(cs[2]), P(cs[3]), nullptr, zhi.data_ptr(), zlo.data_ptr(), 1,
+                                      d.stream),
+          "pointconv bwd dZ split");
+    Tensor dW = at::empty({Co, K}, d.f32);
+    lds_atb_sum(d, {{zhi, s.xhi}, {zhi, s.xlo}, {zlo, s.xhi}}, dW, slabs);
+    Tensor dX = lds_xwt(d, zhi, s.tn, nullptr, false);                       // dZ_hi (W_hi + W_lo)
+    Tensor wt_hi = s.tn.narrow(1, 0, Co);
+    lds_xwt(d, zlo, wt_hi, nullptr, false, &dX, &dX);                        // + dZ_lo W_hi
+    return {dX, dW, cs[0], cs[1]};
+  }
   const int rows = z16 ? dgx_pointconv_bf16_rows(B, N) : dgx_pointconv_bwd_rows(B, N);
   Tensor partials = at::empty({rows, 2, Co}, d.f32);
   Tensor dZ = at::empty({M, Co}, s.bf16 ? d.bf16 : d.f32);
-  const Stats& st = s.st;
   Tensor dz;
   if (z16) {   // two passes over (dout, Z): BN-backward reductions, then dZ directly
     check(dgx_pointconv_bwd_bf16(P(dout), s.Z.data_ptr(), B, N, Co, P(st.scale), P(st.shift), P(st.mean),
@@ -1076,7 +1117,6 @@ std::array<Tensor, 4> pointconv_backward_impl(const Dev& d, Tensor dout, const P
     check(dgx_pointconv_input_grad(P(dz), P(s.Z), Co, M, Co, P(st.scale), P(cs[2]), P(cs[3]), dZ.data_ptr(),
                                    (int)s.bf16, d.stream),
           "pointconv dZ");
-  const int64_t K = s.Xop.size(1);
   Tensor dW = at::empty({Co, K}, d.f32), dX;
   if (s.bf16) {   // bf16 MFMA: dW = dZ^T X (split-K, deterministic), dX = dZ W
     if (s.nt.defined()) {

@@ -24,6 +24,7 @@
 // every neighbour access is an LDS read: HBM/L2 traffic per block is the
 // compulsory M*Co*(bytes) instead of M*k*Co*(bytes).
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -793,6 +794,99 @@ struct BnBwdFin {
 };
 constexpr int BW_FIN_LDS = 16 * 2 * 8 * sizeof(double) + 2 * 8 * sizeof(float);   // per-wave sums | c0 c1
 
+// The scatter's per-channel constants a (BN scale), k0 = c0, k1 = c1 for the
+// workgroup's CS channels: read, or (fin.partials) finalized from the dz
+// pass's partial rows. scratch: BW_FIN_LDS bytes of LDS, 8-byte aligned.
+template <int CS>
+__device__ __forceinline__ void scatter_consts(const BnBwdFin& fin, int b, int part, int o0, int Co,
+                                               const float* __restrict__ scale, const float* __restrict__ c0,
+                                               const float* __restrict__ c1, void* scratch, float (&a)[CS],
+                                               float (&k0)[CS], float (&k1)[CS]) {
+    const int t = threadIdx.x;
+    if (fin.partials) {
+        // thread t sums rows g, g + G, ... of channel o0 + t % CS (fp64), lanes of a
+        // wave with the same channel combine by xor shuffles, then the waves in order
+        static_assert(CS <= 8 && EC_THREADS / 64 <= 16, "finalize scratch");
+        double* wsum = reinterpret_cast<double*>(scratch);   // [wave][2][CS]
+        float* kc = reinterpret_cast<float*>(wsum + 16 * 2 * 8);        // [2][CS]
+        const int c = t % CS, g = t / CS;
+        constexpr int G = EC_THREADS / CS;
+        const int o = o0 + c;
+        double s1 = 0.0, s2 = 0.0;
+        if (o < Co) {
+            const float* __restrict__ pp = fin.partials + o;
+            int r = g;
+            for (; r + 3 * G < fin.nrows; r += 4 * G) {   // 8 independent loads in flight
+                float v1[4], v2[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v1[u] = pp[(int64_t)(r + u * G) * 2 * Co];
+                    v2[u] = pp[(int64_t)(r + u * G) * 2 * Co + Co];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    s1 += (double)v1[u];
+                    s2 += (double)v2[u];
+                }
+            }
+            for (; r < fin.nrows; r += G) {
+                s1 += (double)pp[(int64_t)r * 2 * Co];
+                s2 += (double)pp[(int64_t)r * 2 * Co + Co];
+            }
+        }
+#pragma unroll
+        for (int m = CS; m < 64; m <<= 1) {
+            s1 += __shfl_xor(s1, m);
+            s2 += __shfl_xor(s2, m);
+        }
+        const int lane = t & 63, wv = t >> 6;
+        if (lane < CS) {
+            wsum[(wv * 2) * CS + lane] = s1;
+            wsum[(wv * 2 + 1) * CS + lane] = s2;
+        }
+        __syncthreads();
+        if (t < CS) {
+            double r1 = 0.0, r2 = 0.0;
+            for (int w = 0; w < EC_THREADS / 64; ++w) {
+                r1 += wsum[(w * 2) * CS + t];
+                r2 += wsum[(w * 2 + 1) * CS + t];
+            }
+            float v0 = 0.f, v1 = 0.f;
+            if (o0 + t < Co) {
+                const double av = scale[o0 + t], mu = fin.mean[o0 + t], is = fin.invstd[o0 + t];
+                const double g1 = r1 / fin.count, g2 = r2 / fin.count;
+                if (!fin.eval) {
+                    v0 = (float)(av * (-g1 + g2 * mu * is));
+                    v1 = (float)(-av * g2 * is);
+                }
+                if (b == 0 && part == 0) {
+                    if (fin.dbeta) fin.dbeta[o0 + t] = (float)r1;
+                    if (fin.dgamma) fin.dgamma[o0 + t] = (float)r2;
+                    fin.c0[o0 + t] = v0;
+                    fin.c1[o0 + t] = v1;
+                }
+            }
+            kc[t] = v0;
+            kc[CS + t] = v1;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            a[u] = scale[min(o0 + u, Co - 1)];
+            k0[u] = kc[u];
+            k1[u] = kc[CS + u];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            const int o = min(o0 + u, Co - 1);
+            a[u] = scale[o];
+            k0[u] = c0[o];
+            k1[u] = c1[o];
+        }
+    }
+}
+
 template <int CS, bool OUT16, bool PACKED>
 __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
@@ -888,88 +982,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
         order[atomicAdd(&bucket[BW_BUCKETS - 1 - min(deg, BW_BUCKETS - 1)], 1)] = (uint16_t)r;
     }
     float a[CS], k0[CS], k1[CS];
-    if (fin.partials) {
-        // thread t sums rows g, g + G, ... of channel o0 + t % CS (fp64), lanes of a
-        // wave with the same channel combine by xor shuffles, then the waves in order
-        static_assert(CS <= 8 && EC_THREADS / 64 <= 16, "finalize scratch");
-        double* wsum = reinterpret_cast<double*>(bucket + BW_BUCKETS);   // [wave][2][CS]
-        float* kc = reinterpret_cast<float*>(wsum + 16 * 2 * 8);        // [2][CS]
-        const int c = t % CS, g = t / CS;
-        constexpr int G = EC_THREADS / CS;
-        const int o = o0 + c;
-        double s1 = 0.0, s2 = 0.0;
-        if (o < Co) {
-            const float* __restrict__ pp = fin.partials + o;
-            int r = g;
-            for (; r + 3 * G < fin.nrows; r += 4 * G) {   // 8 independent loads in flight
-                float v1[4], v2[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    v1[u] = pp[(int64_t)(r + u * G) * 2 * Co];
-                    v2[u] = pp[(int64_t)(r + u * G) * 2 * Co + Co];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    s1 += (double)v1[u];
-                    s2 += (double)v2[u];
-                }
-            }
-            for (; r < fin.nrows; r += G) {
-                s1 += (double)pp[(int64_t)r * 2 * Co];
-                s2 += (double)pp[(int64_t)r * 2 * Co + Co];
-            }
-        }
-#pragma unroll
-        for (int m = CS; m < 64; m <<= 1) {
-            s1 += __shfl_xor(s1, m);
-            s2 += __shfl_xor(s2, m);
-        }
-        const int lane = t & 63, wv = t >> 6;
-        if (lane < CS) {
-            wsum[(wv * 2) * CS + lane] = s1;
-            wsum[(wv * 2 + 1) * CS + lane] = s2;
-        }
-        __syncthreads();
-        if (t < CS) {
-            double r1 = 0.0, r2 = 0.0;
-            for (int w = 0; w < EC_THREADS / 64; ++w) {
-                r1 += wsum[(w * 2) * CS + t];
-                r2 += wsum[(w * 2 + 1) * CS + t];
-            }
-            float v0 = 0.f, v1 = 0.f;
-            if (o0 + t < Co) {
-                const double av = scale[o0 + t], mu = fin.mean[o0 + t], is = fin.invstd[o0 + t];
-                const double g1 = r1 / fin.count, g2 = r2 / fin.count;
-                if (!fin.eval) {
-                    v0 = (float)(av * (-g1 + g2 * mu * is));
-                    v1 = (float)(-av * g2 * is);
-                }
-                if (b == 0 && part == 0) {
-                    if (fin.dbeta) fin.dbeta[o0 + t] = (float)r1;
-                    if (fin.dgamma) fin.dgamma[o0 + t] = (float)r2;
-                    fin.c0[o0 + t] = v0;
-                    fin.c1[o0 + t] = v1;
-                }
-            }
-            kc[t] = v0;
-            kc[CS + t] = v1;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < CS; ++u) {
-            a[u] = scale[min(o0 + u, Co - 1)];
-            k0[u] = kc[u];
-            k1[u] = kc[CS + u];
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < CS; ++u) {
-            const int o = min(o0 + u, Co - 1);
-            a[u] = scale[o];
-            k0[u] = c0[o];
-            k1[u] = c1[o];
-        }
-    }
+    scatter_consts<CS>(fin, b, part, o0, Co, scale, c0, c1, bucket + BW_BUCKETS, a, k0, k1);
     const bool vec = full && (CS % 4) == 0 && (Co % 4) == 0 && (ldpq % 4) == 0;
     const float kf = (float)k;
     const int32_t ibase = (int32_t)base;
@@ -1063,6 +1076,267 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             }
         }
     }
+}
+
+// ---- push form of the scatter (dgx_edge_bwd_scatter_push_f32) ------------
+// The a * sum_{selected edges -> j} dz term is pushed from the sources instead
+// of pulled over the in-edges: each (point i, channel c) of the cloud adds its
+// dz_i[c] to the accumulator of j = idx[i][arg_i[c]] (exactly one target per
+// source and channel), so the in-edge loop reads only the Q row (no dz row, no
+// slot compare per channel). The accumulators are 64-bit fixed point in units
+// of 2^(emax - 172), emax the channel's largest biased exponent over the cloud:
+// every term is an integer below 2^46 and the sum of N <= 65535 of them stays
+// below 2^62, so the LDS atomics add exactly and the sum does not depend on the
+// order they land in (deterministic; the exact sum rounded once to fp32). A
+// channel holding an inf / NaN dz makes its sums NaN.
+__device__ __forceinline__ unsigned long long fx_term(uint32_t bits, int emax) {
+    const int E = (bits >> 23) & 0xff;
+    const uint32_t m = (bits & 0x7fffffu) | (E ? 0x800000u : 0u);
+    const int sh = max(E, 1) - emax + 22;  // <= 22
+    const unsigned long long mag =
+        sh >= 0 ? (unsigned long long)m << sh : (sh > -32 ? (unsigned long long)(m >> -sh) : 0ull);
+    return (bits >> 31) ? 0ull - mag : mag;
+}
+__device__ __forceinline__ float fx_value(unsigned long long s, int emax) {
+    return ldexpf((float)(long long)s, emax - 172);
+}
+
+constexpr int BP_U = 16;  // source (point, channel) pairs per thread per batch of the push
+
+template <int CS, bool OUT16, bool PACKED>
+__global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_push_kernel(
+    const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ idx, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ edges, const float* __restrict__ dz, const uint8_t* __restrict__ arg,
+    const float* __restrict__ sumP, int B, int N, int k, int Co, int nparts, const float* __restrict__ scale,
+    const float* __restrict__ c0, const float* __restrict__ c1, void* __restrict__ dPQv, BnBwdFin fin,
+    uint32_t skip) {   // skip: phase-timing probe (tools/push_lab.py), 0 in production
+    static_assert(CS == 1 || CS == 2 || CS == 4 || CS == 8, "slice width");
+    static_assert(EC_THREADS % CS == 0, "a thread keeps one channel");
+    float* __restrict__ dPQ = static_cast<float*>(dPQv);
+    __bf16* __restrict__ dPQh = static_cast<__bf16*>(dPQv);
+    int b, part, slice;
+    if (!dgx_xcd_slice_map(blockIdx.x, B, nparts, (Co + CS - 1) / CS, b, part, slice)) return;
+    const int o0 = slice * CS;
+    const int t = threadIdx.x, lane = t & 63;
+    const int64_t base = (int64_t)b * N;
+    const int per = (N + nparts - 1) / nparts;
+    const int per8 = (per + 7) & ~7;
+    const int n_beg = part * per, n_end = min(N, n_beg + per);
+    const int np = max(0, n_end - n_beg);
+    // [N][CS] Q | [per8][CS] u64 accumulators | [per8] u16 order | buckets | emax, bad | finalize scratch
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* qs = lds;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(lds + ((N * CS + 3) & ~3));
+    uint16_t* order = reinterpret_cast<uint16_t*>(acc + per8 * CS);
+    int* bucket = reinterpret_cast<int*>(order + per8);
+    int* emx = bucket + BW_BUCKETS;
+    int* badc = emx + 8;
+    void* scratch = badc + 8;
+    const bool full = o0 + CS <= Co;
+    constexpr bool SWZ = CS == 8;
+    for (int e = t; e < per8 * CS / 2; e += EC_THREADS) reinterpret_cast<uint4*>(acc)[e] = make_uint4(0, 0, 0, 0);
+    if (t < BW_BUCKETS) bucket[t] = 0;
+    if (t < 8) {
+        emx[t] = 1;
+        badc[t] = 0;
+    }
+    auto lds_row = [&](const float* __restrict__ arr, int n, float (&r)[CS]) {
+        if constexpr (SWZ) {
+            const int sw = ((n >> 2) & 1) << 2;
+            const float4 x = *reinterpret_cast<const float4*>(arr + n * CS + sw);
+            const float4 y = *reinterpret_cast<const float4*>(arr + n * CS + (4 ^ sw));
+            r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+            r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
+        } else {
+            lds_vec<CS>(arr + n * CS, r);
+        }
+    };
+    // the thread's channel is the same on every trip of the (point, channel) loops
+    const int cc = t % CS;
+    const bool cvalid = o0 + cc < Co;
+    const uint32_t* __restrict__ dzw = reinterpret_cast<const uint32_t*>(dz) + base * Co + o0 + cc;
+    const int total = N * CS;
+    constexpr int CHUNK = BP_U * EC_THREADS;
+    uint32_t w[BP_U];
+    auto load_w = [&](int p0) {
+#pragma unroll
+        for (int u = 0; u < BP_U; ++u) {
+            const int p = p0 + u * EC_THREADS;
+            w[u] = cvalid && p < total ? dzw[(uint32_t)((p / CS) * Co)] : 0u;   // 32-bit offsets: saddr loads
+        }
+    };
+    // the first chunk of dz words and in-degrees are loaded before the Q slice
+    // is staged, so their latency hides behind the staging
+    load_w(t);
+    const int deg0 = t < np ? rowptr[base + n_beg + t + 1] - rowptr[base + n_beg + t] : 0;
+    if (!(skip & 8))
+        stage_slice<CS, EC_THREADS, SWZ>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co,
+                                         (ldpq % 4) == 0 && (Co % 4) == 0);
+    // pass 1: the channel's largest exponent and whether it holds a non-finite dz
+    int em = 1, bad = 0;
+    for (int p0 = t; !(skip & 1);) {
+#pragma unroll
+        for (int u = 0; u < BP_U; ++u) {
+            const int E = (w[u] >> 23) & 0xff;
+            bad |= E == 0xff;
+            em = max(em, E == 0xff ? 1 : E);
+        }
+        p0 += CHUNK;
+        if (p0 >= total) break;
+        load_w(p0);
+    }
+#pragma unroll
+    for (int m = CS; m < 64; m <<= 1) {
+        em = max(em, __shfl_xor(em, m));
+        bad |= __shfl_xor(bad, m);
+    }
+    __syncthreads();  // accumulators, buckets, emx zeroed
+    if (lane < CS) {
+        atomicMax(&emx[lane], em);
+        if (bad) atomicOr(&badc[lane], 1);
+    }
+    // in-block order: counting sort of the block's points by in-degree, descending
+    for (int r = t; r < np; r += EC_THREADS) {
+        const int64_t j = base + n_beg + r;
+        const int deg = r == t ? deg0 : rowptr[j + 1] - rowptr[j];
+        atomicAdd(&bucket[BW_BUCKETS - 1 - min(deg, BW_BUCKETS - 1)], 1);
+    }
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the 64 bucket counts (one wave)
+        const int c = bucket[t];
+        int inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o);
+            if (t >= o) inc += v;
+        }
+        bucket[t] = inc - c;
+    }
+    // pass 2: push every source's selected dz into its target's accumulator
+    // (a single chunk is still in registers from pass 1)
+    if (cvalid && !(skip & 2)) {
+        const int ec = emx[cc];
+        const int32_t* __restrict__ ib = idx + base * k;
+        const uint8_t* __restrict__ ab = PACKED ? nullptr : arg + base * Co + o0 + cc;
+        for (int p0 = t; p0 < total; p0 += CHUNK) {
+            if (total > CHUNK) load_w(p0);
+            int j[BP_U];   // the slot, then the target
+#pragma unroll
+            for (int u = 0; u < BP_U; ++u) {
+                const int p = p0 + u * EC_THREADS;
+                if constexpr (PACKED) j[u] = (int)(w[u] & 63u);
+                else j[u] = p < total ? ab[(uint32_t)((p / CS) * Co)] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < BP_U; ++u) {
+                const int p = p0 + u * EC_THREADS;
+                j[u] = p < total ? ib[(uint32_t)((p / CS) * k + j[u])] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < BP_U; ++u) {
+                const uint32_t v = PACKED ? (w[u] & ~63u) : w[u];
+                if (j[u] >= n_beg && j[u] < n_end && ((v >> 23) & 0xff) != 0xff && !(skip & 16))
+                    atomicAdd(&acc[(j[u] - n_beg) * CS + cc], fx_term(v, ec));
+            }
+        }
+    }
+    __syncthreads();  // bucket offsets
+    for (int r = t; r < np; r += EC_THREADS) {
+        const int64_t j = base + n_beg + r;
+        const int deg = rowptr[j + 1] - rowptr[j];
+        order[atomicAdd(&bucket[BW_BUCKETS - 1 - min(deg, BW_BUCKETS - 1)], 1)] = (uint16_t)r;
+    }
+    float a[CS], k0[CS], k1[CS];
+    scatter_consts<CS>(fin, b, part, o0, Co, scale, c0, c1, scratch, a, k0, k1);
+    const bool vec = full && (CS % 4) == 0 && (Co % 4) == 0 && (ldpq % 4) == 0;
+    const float kf = (float)k;
+    const int32_t ibase = (int32_t)base;
+    __syncthreads();  // order, accumulators, emx / bad complete
+    int ex[CS];
+    bool nan_c[CS];
+#pragma unroll
+    for (int u = 0; u < CS; ++u) {
+        ex[u] = emx[u];
+        nan_c[u] = badc[u] != 0;
+    }
+    // boustrophedon deal of the degree-sorted points (as edge_bwd_scatter_kernel)
+    for (int it = 0; it * EC_THREADS < np; ++it) {
+        const int r = it * EC_THREADS + ((it & 1) ? EC_THREADS - 1 - t : t);
+        if (r >= np) continue;
+        const int rl = order[r];
+        const int n = n_beg + rl;
+        const int64_t j = base + n;
+        const int32_t beg = rowptr[j], end = rowptr[j + 1];
+        float pjv[CS], spv[CS], dn[CS];  // HBM reads issued before the edge loop hides their latency
+        if (vec) {
+            gld_vec<CS>(PQ + j * ldpq + o0, pjv);
+            gld_vec<CS>(sumP + j * Co + o0, spv);
+            gld_vec<CS>(dz + j * Co + o0, dn);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CS; ++u) {
+                pjv[u] = o0 + u < Co ? PQ[j * ldpq + o0 + u] : 0.f;
+                spv[u] = o0 + u < Co ? sumP[j * Co + o0 + u] : 0.f;
+                dn[u] = o0 + u < Co ? dz[j * Co + o0 + u] : 0.f;
+            }
+        }
+        float sq[CS];
+#pragma unroll
+        for (int u = 0; u < CS; ++u) sq[u] = 0.f;
+        for (int32_t u0 = beg; u0 < ((skip & 4) ? beg : end); u0 += BW_EB) {
+            int32_t ids[BW_EB];
+#pragma unroll
+            for (int v = 0; v < BW_EB; ++v) ids[v] = u0 + v < end ? edges[u0 + v] : 0;
+#pragma unroll
+            for (int v = 0; v < BW_EB; ++v)
+                if (u0 + v < end) {
+                    float q[CS];
+                    lds_row(qs, (ids[v] >> 6) - ibase, q);
+#pragma unroll
+                    for (int u = 0; u < CS; ++u) sq[u] += q[u];
+                }
+        }
+        const float deg = (float)(end - beg);
+        float qn[CS], sd[CS];
+        lds_row(qs, n, qn);
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            sd[u] = nan_c[u] ? __builtin_nanf("") : fx_value(acc[rl * CS + u], ex[u]);
+            if constexpr (PACKED) dn[u] = __uint_as_float(__float_as_uint(dn[u]) & ~63u);
+        }
+        float dp[CS], dq[CS];
+#pragma unroll
+        for (int u = 0; u < CS; ++u) {
+            dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
+            dq[u] = fmaf(a[u], dn[u], fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
+        }
+        if (OUT16 && vec) {
+            gst_bf16<CS>(dPQh + j * 2 * Co + o0, dp);
+            gst_bf16<CS>(dPQh + j * 2 * Co + Co + o0, dq);
+        } else if (vec) {
+            gst_vec<CS>(dPQ + j * 2 * Co + o0, dp);
+            gst_vec<CS>(dPQ + j * 2 * Co + Co + o0, dq);
+        } else {
+#pragma unroll
+            for (int u = 0; u < CS; ++u) {
+                if (o0 + u >= Co) continue;
+                if (OUT16) {
+                    dPQh[j * 2 * Co + o0 + u] = (__bf16)dp[u];
+                    dPQh[j * 2 * Co + Co + o0 + u] = (__bf16)dq[u];
+                } else {
+                    dPQ[j * 2 * Co + o0 + u] = dp[u];
+                    dPQ[j * 2 * Co + Co + o0 + u] = dq[u];
+                }
+            }
+        }
+    }
+}
+
+// push-scatter LDS bytes: Q slice | accumulators | order | buckets | emax, bad | finalize scratch
+inline size_t push_lds_bytes(int N, int cs, int parts) {
+    const size_t per8 = (size_t)(((N + parts - 1) / parts + 7) & ~7);
+    return (((size_t)N * cs + 3) & ~(size_t)3) * sizeof(float) + per8 * cs * 8 + per8 * sizeof(uint16_t) +
+           BW_BUCKETS * sizeof(int) + 16 * sizeof(int) + BW_FIN_LDS;
 }
 
 // scatter LDS bytes for N points at CS channels (Q | dz | slot | order | buckets;
@@ -1384,6 +1658,73 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
 #undef DGX_SCATTER_LAUNCH
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
+
+// slice width and point parts of the push scatter: the fewest re-staged Q
+// slices (parts / cs) whose LDS fits two workgroups per CU (80 KiB), else one
+// (160 KiB); parts also brings the grid to ~2 workgroups per CU (point_parts)
+bool push_geometry(int B, int N, int Co, int& cs_out, int& parts_out) {
+    for (const size_t budget : {(size_t)80 * 1024, (size_t)160 * 1024}) {
+        int best_cs = 0, best_parts = 0;
+        for (int cs = 8; cs >= 1; cs >>= 1) {
+            const int slices = (Co + cs - 1) / cs;
+            int parts = point_parts(B, slices, N);
+            while (push_lds_bytes(N, cs, parts) > budget && parts * 64 < N) parts *= 2;
+            if (push_lds_bytes(N, cs, parts) > budget) continue;
+            if (!best_cs || (int64_t)parts * best_cs < (int64_t)best_parts * cs) {
+                best_cs = cs;
+                best_parts = parts;
+            }
+        }
+        if (best_cs) {
+            cs_out = best_cs;
+            parts_out = best_parts;
+            return true;
+        }
+    }
+    return false;
+}
+
+int launch_push(const float* PQ, int ldpq, const int32_t* idx, const int32_t* rowptr, const int32_t* edges,
+                const float* dz, const uint8_t* arg, const float* sumP, int B, int N, int k, int Co,
+                const float* scale, const float* c0, const float* c1, void* dPQ, int out_bf16, bool packed,
+                void* stream, const BnBwdFin& fin) {
+    if (!PQ || !idx || !rowptr || !edges || !dz || (!packed && !arg) || !sumP || !scale || !c0 || !c1 || !dPQ)
+        return DGX_EINVAL;
+    if (fin.partials && (fin.nrows < 1 || fin.count <= 0.0 || !fin.mean || !fin.invstd)) return DGX_EINVAL;
+    if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
+    if (N > 65535) return DGX_EUNSUPPORTED;
+    int cs = 0, parts = 0;
+    if (!push_geometry(B, N, Co, cs, parts)) return DGX_EUNSUPPORTED;
+    const char* probe = getenv("DGX_PUSH_SKIP");   // phase-timing probe of tools/push_lab.py (unset: 0)
+    const uint32_t skip = probe ? (uint32_t)strtoul(probe, nullptr, 0) : 0u;
+    const int slices = (Co + cs - 1) / cs;
+    const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
+    const size_t lds = push_lds_bytes(N, cs, parts);
+    hipStream_t st = dgx_stream(stream);
+#define DGX_PUSH_LAUNCH(CSV, O16, PK)                                                                              \
+    hipLaunchKernelGGL((edge_bwd_push_kernel<CSV, O16, PK>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, idx, rowptr, \
+                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, skip)
+#define DGX_PUSH_CASE(CSV)                                      \
+    case CSV:                                                   \
+        if (packed) {                                           \
+            if (out_bf16) DGX_PUSH_LAUNCH(CSV, true, true);     \
+            else DGX_PUSH_LAUNCH(CSV, false, true);             \
+        } else {                                                \
+            if (out_bf16) DGX_PUSH_LAUNCH(CSV, true, false);    \
+            else DGX_PUSH_LAUNCH(CSV, false, false);            \
+        }                                                       \
+        break;
+    switch (cs) {
+        DGX_PUSH_CASE(8)
+        DGX_PUSH_CASE(4)
+        DGX_PUSH_CASE(2)
+        DGX_PUSH_CASE(1)
+        default: return DGX_EUNSUPPORTED;
+    }
+#undef DGX_PUSH_CASE
+#undef DGX_PUSH_LAUNCH
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
 }  // namespace
 
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr, const int32_t* edges,
@@ -1411,6 +1752,17 @@ int dgx_edge_bwd_scatter_packed_f32(const float* PQ, int ldpq, const int32_t* ro
                                     void* stream) {
     return launch_scatter(PQ, ldpq, rowptr, edges, dz_packed, nullptr, sumP, B, N, k, Co, scale, c0, c1, dPQ,
                           out_bf16, true, stream);
+}
+
+int dgx_edge_bwd_scatter_push_f32(const float* PQ, int ldpq, const int32_t* idx, const int32_t* rowptr,
+                                  const int32_t* edges, const float* dz, const uint8_t* arg, const float* sumP, int B,
+                                  int N, int k, int Co, const float* partials, int nrows, double count,
+                                  const float* scale, const float* mean, const float* invstd, int eval, float* dgamma,
+                                  float* dbeta, float* c0, float* c1, void* dPQ, int out_bf16, int packed,
+                                  void* stream) {
+    const BnBwdFin fin{partials, nrows, count, mean, invstd, eval, dgamma, dbeta, c0, c1};
+    return launch_push(PQ, ldpq, idx, rowptr, edges, dz, packed ? nullptr : arg, sumP, B, N, k, Co, scale, c0, c1,
+                       dPQ, out_bf16, packed != 0, stream, fin);
 }
 
 }  // extern "C"

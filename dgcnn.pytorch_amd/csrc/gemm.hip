@@ -166,7 +166,17 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_bf16_kernel(
     const int wm = wave / WN, wn = wave % WN;
     const int nJ = (N + BN - 1) / BN;
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int ti = L / nJ, tj = L - ti * nJ;
+    // tile order in groups of two row tiles: the 4 consecutive tiles an XCD
+    // takes (xcd_remap) form a 2 x 2 square, so each A row panel and each B
+    // column panel of a K-chunk is fetched by half as many XCDs as in row-major
+    // order (which shares A panels but sends every B panel to all eight)
+    const int nI = (M + BM - 1) / BM;
+    int ti, tj;
+    {
+        const int gsz = 2 * nJ, grp = L / gsz, first = grp * 2, gm = min(nI - first, 2), r = L - grp * gsz;
+        ti = first + r % gm;
+        tj = r / gm;
+    }
     const int i0 = ti * BM, j0 = tj * BN;
     const int kbeg = blockIdx.y * kchunk;
     const int kend = min(K, kbeg + kchunk);
@@ -455,7 +465,17 @@ __global__ __launch_bounds__(GB_THREADS, 2) void gemm_lds_kernel(
     const int wm = wave / WN, wn = wave % WN;
     const int nJ = (N + BN - 1) / BN;
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int ti = L / nJ, tj = L - ti * nJ;
+    // tile order in groups of two row tiles: the 4 consecutive tiles an XCD
+    // takes (xcd_remap) form a 2 x 2 square, so each A row panel and each B
+    // column panel of a K-chunk is fetched by half as many XCDs as in row-major
+    // order (which shares A panels but sends every B panel to all eight)
+    const int nI = (M + BM - 1) / BM;
+    int ti, tj;
+    {
+        const int gsz = 2 * nJ, grp = L / gsz, first = grp * 2, gm = min(nI - first, 2), r = L - grp * gsz;
+        ti = first + r % gm;
+        tj = r / gm;
+    }
     const int i0 = ti * BM, j0 = tj * BN;
     const int kbeg = blockIdx.y * kchunk;
     const int kend = min(K, kbeg + kchunk);

@@ -375,6 +375,206 @@ __global__ __launch_bounds__(256, 4) void bwd16_stats_lt_kernel(const float* __r
     }
 }
 
+// ---- fp32 Z (precision "fp32"): the same LDS-transposed tiles, 128 points x
+// 64 channels x 4 B; a row is 16 chunks of 16 B, chunk c of row r stored at
+// c ^ ((r >> 2) & 7), so the per-thread 16-B reads of rows 4pg+i (and the
+// staging writes of one row) fall in distinct bank groups. ------------------
+__device__ __forceinline__ int zt32_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 7)) << 2); }
+
+__device__ __forceinline__ void stage_ztile32(const float* __restrict__ Z, int b, int n0, int o0, int N, int C,
+                                              float* zt) {
+    for (int e = threadIdx.x; e < RT_P * 16; e += 256) {
+        const int row = e >> 4, ch = e & 15;
+        const int n = n0 + row, o = o0 + 4 * ch;
+        float4 v;
+        if (n < N && o + 4 <= C && (C % 4) == 0) {
+            v = *reinterpret_cast<const float4*>(Z + ((int64_t)b * N + n) * C + o);
+        } else {
+            float t[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[j] = (n < N && o + j < C) ? Z[((int64_t)b * N + n) * C + o + j] : 0.f;
+            v = make_float4(t[0], t[1], t[2], t[3]);
+        }
+        *reinterpret_cast<float4*>(zt + zt32_off(row, ch)) = v;
+    }
+}
+
+__device__ __forceinline__ void read_z48_32(const float* zt, int pg, int cg, float (&z)[4][8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float4 v = *reinterpret_cast<const float4*>(zt + zt32_off(4 * pg + i, 2 * cg + h));
+            z[i][4 * h] = v.x; z[i][4 * h + 1] = v.y; z[i][4 * h + 2] = v.z; z[i][4 * h + 3] = v.w;
+        }
+}
+
+// out(b, o, n) = LeakyReLU(a_o z + b_o), fp32 Z
+__global__ __launch_bounds__(256) void apply32_lt_kernel(const float* __restrict__ Z, int N, int C,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, float slope,
+                                                         float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float zt[RT_P * 64];
+    const ZTile T(N);
+    stage_ztile32(Z, T.b, T.n0, T.o0, N, C, zt);
+    __syncthreads();
+    float z[4][8];
+    read_z48_32(zt, T.pg, T.cg, z);
+    const int n = T.n0 + 4 * T.pg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int oo = T.o0 + 8 * T.cg + j;
+        if (oo >= C) break;
+        const float a = scale[oo], sh = shift[oo];
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(a, z[i][j], sh), slope);
+        store_row4(out, ((int64_t)T.b * C + oo) * N, n, N, v);
+    }
+}
+
+// PASS 0 (fp32 Z): as bwd16_stats_lt_kernel
+__global__ __launch_bounds__(256, 4) void bwd32_stats_lt_kernel(const float* __restrict__ dout,
+                                                             const float* __restrict__ Z, int N, int C,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, float slope,
+                                                             float* __restrict__ partials) {
+    __shared__ __attribute__((aligned(16))) float zt[RT_P * 64];
+    __shared__ __attribute__((aligned(16))) float4 cst[64];   // per channel {scale, shift, mean, invstd}
+    const int nt = (N + RT_P * RS_LT - 1) / (RT_P * RS_LT);
+    const int b = blockIdx.x / nt;
+    const int nb = (blockIdx.x - b * nt) * RT_P * RS_LT;
+    const int o0 = blockIdx.y * 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int pg = lane & 31, cg = 2 * w + (lane >> 5);
+    if (threadIdx.x < 64) {
+        const int oj = min(o0 + (int)threadIdx.x, C - 1);
+        cst[threadIdx.x] = make_float4(scale[oj], shift[oj], mean[oj], invstd[oj]);
+    }
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        s1[j] = 0.f;
+        s2[j] = 0.f;
+    }
+#pragma unroll 1
+    for (int it = 0; it < RS_LT; ++it) {
+        const int n0 = nb + it * RT_P;
+        if (n0 >= N) break;
+        const int n = n0 + 4 * pg;
+        float g[8][4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int oo = o0 + 8 * cg + j;
+            const float4 v = load_row4(dout, ((int64_t)b * C + oo) * N, n, N, oo < C);
+            g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
+        }
+        if (it > 0) __syncthreads();
+        stage_ztile32(Z, b, n0, o0, N, C, zt);
+        __syncthreads();
+        float z[4][8];
+        read_z48_32(zt, pg, cg, z);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float4 k4 = cst[8 * cg + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float d = g[j][i] * (fmaf(k4.x, z[i][j], k4.y) > 0.f ? 1.f : slope);
+                s1[j] += d;
+                s2[j] = fmaf(d, (z[i][j] - k4.z) * k4.w, s2[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int m = 1; m < 32; m <<= 1) {
+            s1[j] += __shfl_xor(s1[j], m);
+            s2[j] += __shfl_xor(s2[j], m);
+        }
+    }
+    if (pg == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int oo = o0 + 8 * cg + j;
+            if (oo < C) {
+                partials[(int64_t)blockIdx.x * 2 * C + oo] = s1[j];
+                partials[(int64_t)blockIdx.x * 2 * C + C + oo] = s2[j];
+            }
+        }
+    }
+}
+
+// PASS 1 (fp32 Z) straight into the split-bf16 operand planes of the 3-pass
+// GEMMs: v = a d + c0 + c1 z (the fp32 dZ of bwd_dZ_kernel), hi = bf16(v),
+// lo = bf16(v - hi) (dgx_split_bf16), written point-major through the tile.
+__global__ __launch_bounds__(256) void bwd32_split_lt_kernel(const float* __restrict__ dout,
+                                                             const float* __restrict__ Z, int N, int C,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, float slope,
+                                                             const float* __restrict__ c0,
+                                                             const float* __restrict__ c1, bf16* __restrict__ hi,
+                                                             bf16* __restrict__ lo) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) float zt[RT_P * 64];
+    const ZTile T(N);
+    const int n = T.n0 + 4 * T.pg;
+    float g[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int oo = T.o0 + 8 * T.cg + j;
+        const float4 v = load_row4(dout, ((int64_t)T.b * C + oo) * N, n, N, oo < C);
+        g[j][0] = v.x; g[j][1] = v.y; g[j][2] = v.z; g[j][3] = v.w;
+    }
+    stage_ztile32(Z, T.b, T.n0, T.o0, N, C, zt);
+    __syncthreads();
+    float z[4][8];
+    read_z48_32(zt, T.pg, T.cg, z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int oo = min(T.o0 + 8 * T.cg + j, C - 1);
+        const float a = scale[oo], sh = shift[oo], k0 = c0[oo], k1 = c1[oo];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float d = g[j][i] * (fmaf(a, z[i][j], sh) > 0.f ? 1.f : slope);
+            z[i][j] = fmaf(a, d, fmaf(k1, z[i][j], k0));
+        }
+    }
+    __syncthreads();  // every thread has read its Z values
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            *reinterpret_cast<float4*>(zt + zt32_off(4 * T.pg + i, 2 * T.cg + h)) =
+                make_float4(z[i][4 * h], z[i][4 * h + 1], z[i][4 * h + 2], z[i][4 * h + 3]);
+    __syncthreads();
+    for (int e = threadIdx.x; e < RT_P * 16; e += 256) {
+        const int row = e >> 4, ch = e & 15;
+        const int nn = T.n0 + row, o = T.o0 + 4 * ch;
+        if (nn >= N) continue;
+        const float4 v = *reinterpret_cast<const float4*>(zt + zt32_off(row, ch));
+        const float f[4] = {v.x, v.y, v.z, v.w};
+        bf16x4 h, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            h[j] = (bf16)f[j];
+            l[j] = (bf16)(f[j] - (float)h[j]);
+        }
+        const int64_t off = ((int64_t)T.b * N + nn) * C + o;
+        if (o + 4 <= C && (C % 4) == 0) {
+            *reinterpret_cast<bf16x4*>(hi + off) = h;
+            *reinterpret_cast<bf16x4*>(lo + off) = l;
+        } else {
+            for (int j = 0; j < 4 && o + j < C; ++j) {
+                hi[off + j] = h[j];
+                lo[off + j] = l[j];
+            }
+        }
+    }
+}
+
 inline int grid_for(int64_t total, int block) {
     int64_t g = (total + block - 1) / block;
     return (int)(g < 16384 ? (g < 1 ? 1 : g) : 16384);
@@ -399,6 +599,11 @@ int dgx_colstats_f32(const float* Z, int ldz, int64_t M, int C, float* partials,
 int dgx_pointconv_apply_f32(const float* Z, int ldz, int B, int N, int C, const float* scale, const float* shift,
                               float slope, float* out, void* stream) {
     if (!Z || !scale || !shift || !out || B < 1 || N < 1 || C < 1 || ldz < C) return DGX_EINVAL;
+    if (ldz == C && C % 4 == 0 && (reinterpret_cast<uintptr_t>(Z) & 15) == 0) {   // dense rows: 128-point LDS tiles
+        hipLaunchKernelGGL(apply32_lt_kernel, dim3(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64), dim3(256), 0,
+                           dgx_stream(stream), Z, N, C, scale, shift, slope, out);
+        return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+    }
     dim3 grid(B * ((N + PT - 1) / PT), (C + PT - 1) / PT);
     hipLaunchKernelGGL(apply_T_kernel, grid, dim3(256), 0, dgx_stream(stream), Z, ldz, N, C, scale, shift, slope, out);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
@@ -461,6 +666,24 @@ int dgx_pointconv_bwd_bf16(const float* dout, const void* Z, int B, int N, int C
     else
         hipLaunchKernelGGL(bwd16_dz_lt_kernel, grid, dim3(256), 0, dgx_stream(stream), dout, z, N, C, scale, shift,
                            slope, c0, c1, static_cast<bf16*>(dZ));
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_pointconv_bwd_split_f32(const float* dout, const float* Z, int B, int N, int C, const float* scale,
+                                const float* shift, const float* mean, const float* invstd, float slope,
+                                const float* c0, const float* c1, float* partials, void* dZ_hi, void* dZ_lo, int pass,
+                                void* stream) {
+    if (!dout || !Z || !scale || !shift || B < 1 || N < 1 || C < 1) return DGX_EINVAL;
+    if (pass == 0 ? (!mean || !invstd || !partials) : (!c0 || !c1 || !dZ_hi || !dZ_lo)) return DGX_EINVAL;
+    if (C % 4 || (reinterpret_cast<uintptr_t>(Z) & 15)) return DGX_EUNSUPPORTED;
+    if (pass == 0)
+        hipLaunchKernelGGL(bwd32_stats_lt_kernel, dim3(B * ((N + RT_P * RS_LT - 1) / (RT_P * RS_LT)), (C + 63) / 64),
+                           dim3(256), 0, dgx_stream(stream), dout, Z, N, C, scale, shift, mean, invstd, slope,
+                           partials);
+    else
+        hipLaunchKernelGGL(bwd32_split_lt_kernel, dim3(B * ((N + RT_P - 1) / RT_P), (C + 63) / 64), dim3(256), 0,
+                           dgx_stream(stream), dout, Z, N, C, scale, shift, slope, c0, c1,
+                           static_cast<bf16*>(dZ_hi), static_cast<bf16*>(dZ_lo));
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -64,6 +64,8 @@ _SIGS = {
                                      _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp],
     "dgx_edge_bwd_scatter_packed_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
                                         _i32, _vp],
+    "dgx_edge_bwd_scatter_push_f32": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _i32,
+                                      _f64, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp],
     "dgx_colstats_rows": [_i64],
     "dgx_colstats_f32": [_vp, _i32, _i64, _i32, _vp, _i32, _vp],
     "dgx_pointconv_apply_f32": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],
@@ -92,6 +94,8 @@ _SIGS = {
     "dgx_pointconv_bf16_rows": [_i32, _i32],
     "dgx_pointconv_apply_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],
     "dgx_pointconv_bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _vp],
+    "dgx_pointconv_bwd_split_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
+                                    _i32, _vp],
     "dgx_edge_mlp_h1_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],
     "dgx_edge_mlp_max_f32": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
     "dgx_edge_mlp_dz_f32": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp],

@@ -262,6 +262,21 @@ int dgx_edge_bwd_scatter_packed_f32(const float* PQ, int ldpq, const int32_t* ro
                                     const float* sumP, int B, int N, int k, int Co,
                                     const float* scale, const float* c0, const float* c1,
                                     void* dPQ, int out_bf16, void* stream);
+/* The same dPQ with the selected-edge term pushed from the sources: each
+ * (point i, channel c) adds dz_i[c] to j = idx[i][slot] (idx: the forward's
+ * B x N x k kNN graph), summed exactly in 64-bit fixed point (LDS atomics,
+ * order-independent, rounded once to fp32), so the in-edge loop reads Q rows
+ * only. All modes in one entry: partials != NULL finalizes the BN backward as
+ * dgx_edge_bwd_scatter_fin_f32 (else c0 / c1 are inputs, eval ignored);
+ * packed != 0 reads dgx_edge_bwd_dz_packed_f32 words (arg unused). A channel
+ * whose dz holds inf / NaN gets NaN in every dP of the channel. */
+int dgx_edge_bwd_scatter_push_f32(const float* PQ, int ldpq, const int32_t* idx,
+                                  const int32_t* rowptr, const int32_t* edges, const float* dz,
+                                  const uint8_t* arg, const float* sumP, int B, int N, int k,
+                                  int Co, const float* partials, int nrows, double count,
+                                  const float* scale, const float* mean, const float* invstd,
+                                  int eval, float* dgamma, float* dbeta, float* c0, float* c1,
+                                  void* dPQ, int out_bf16, int packed, void* stream);
 
 /* ---- a4: pointwise Conv1x1 + BatchNorm + LeakyReLU, replaces conv5 of
  * models/dgcnn.py:74-78, 100-102 (cat(x1..x4) -> Conv2d(512,emb,1) -> BN ->
@@ -310,6 +325,17 @@ int dgx_pointconv_bwd_bf16(const float* dout, const void* Z, int B, int N, int C
                            const float* invstd, float slope, const float* c0,
                            const float* c1, float* partials, void* dZ, int pass,
                            void* stream);
+/* The same two passes for an fp32 Z (dense M x C, C % 4 == 0; fp32 mode with
+ * the 3-pass split-bf16 conv5 GEMMs): pass 0 partials as dgx_pointconv_bwd_bf16
+ * (dgx_pointconv_bf16_rows rows); pass 1 writes dZ = scale*d + c0 + c1*z (fp32
+ * arithmetic, the value dgx_pointconv_input_grad computes) as its split-bf16
+ * planes dZ_hi = bf16(dZ), dZ_lo = bf16(dZ - dZ_hi) (dgx_split_bf16), the
+ * operands of the split GEMMs — no fp32 dz or dZ round trip. */
+int dgx_pointconv_bwd_split_f32(const float* dout, const float* Z, int B, int N, int C,
+                                const float* scale, const float* shift, const float* mean,
+                                const float* invstd, float slope, const float* c0,
+                                const float* c1, float* partials, void* dZ_hi, void* dZ_lo,
+                                int pass, void* stream);
 
 /* ---- a3/a4/a8: the Conv2d(1x1) GEMMs of the chain, bf16 MFMA ----------------
  * Replace the reference's per-edge conv GEMMs (models/dgcnn.py:55-73, K11) and

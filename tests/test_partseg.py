@@ -210,17 +210,33 @@ def test_hog_restatement_matches_reference_cpu(golden):
 # constant) are measured against the model-wide gradient scale.
 AMP_TOL = 2e-2
 RATIO = 1.5
+# fp32 mode with conv5's GEMMs as 3-pass split bf16 (dgx.edgeconv.SPLIT32, the
+# default): ~2^-16 relative per product instead of fp32's 2^-24, which the
+# ill-conditioned gradients above amplify to ~2x stock fp32's error on a few
+# EdgeConv weights (r06u: conv4.0.weight 9.6e-3 vs stock 4.8e-3; 6.0e-3 vs
+# 6.0e-3 worst with exact products). Exact products are held to RATIO.
+RATIO_SPLIT = 3.0
+# amp: the engine's GEMMs run bf16 under autocast (unit roundoff 2^-9), the
+# stock layers fp16 (2^-11), so the engine's share of the error is up to ~4x
+# the stock step's: held to 4 x RATIO (r06v: worst pos_mlp.0.transform.weight
+# 1.55 vs stock 0.36 of an fp64 gradient that fp16 itself misses by 36 %)
+RATIO_AMP = 6.0
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("amp", [False, True])
-def test_net_cfg4_routed(cuda, amp, monkeypatch):
+@pytest.mark.parametrize("mode", ["fp32", "fp32_split", "amp"])
+def test_net_cfg4_routed(cuda, mode, monkeypatch):
     """Net train step at cfg4 geometry against the reference's forward over
     stock fp64 modules (oracle.partseg.net_routed) on the same neighbours:
     every EdgeConv kNN / max slot / sign, the edge stage's kNN / conv2 slot /
     sign, PositionEmbedding's max over points and the HOG are validated, then
-    the output and EVERY parameter gradient are compared."""
+    the output and EVERY parameter gradient are compared. fp32: exact fp32
+    GEMM products (DGX_SPLIT32=0); fp32_split: the fp32 mode's default conv5
+    GEMMs; amp: fp16 autocast as main_partseg_dist.py:253 trains."""
     import dgx.edgeconv as E
+    amp = mode == "amp"
+    monkeypatch.setattr(E, "SPLIT32", mode == "fp32_split")
+    ratio = {"fp32": RATIO, "fp32_split": RATIO_SPLIT, "amp": RATIO_AMP}[mode]
     import oracle
     from conftest import edge_mlp_decisions, validate_dgcnn_decisions
     from dgx import synth
@@ -299,11 +315,11 @@ def test_net_cfg4_routed(cuda, amp, monkeypatch):
     rows = []
     for n, p in net.named_parameters():
         rows.append((n, err(p.grad, g64[n].grad), err(runs["stock"][1][n].grad, g64[n].grad)))
-    rows.sort(key=lambda r: -r[1] / max(floor, RATIO * r[2]))
-    print(f"Net cfg4 amp={amp}: decisions {dec} edge {edec} maxN gap {gap_n:.1e}; out {e_out:.1e}; "
+    rows.sort(key=lambda r: -r[1] / max(floor, ratio * r[2]))
+    print(f"Net cfg4 {mode}: decisions {dec} edge {edec} maxN gap {gap_n:.1e}; out {e_out:.1e}; "
           "worst (engine, stock):", [(n, f"{e:.1e}", f"{e2:.1e}") for n, e, e2 in rows[:6]])
     for n, e, e2 in rows:
-        assert e <= max(floor, RATIO * e2), (n, e, e2)
+        assert e <= max(floor, ratio * e2), (n, e, e2)
 
 
 @pytest.mark.gpu
