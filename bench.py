@@ -23,6 +23,7 @@ Prints ONE JSON line on rank 0: whole-job clouds/s, plus
                 golden-pinned) for the same B-cloud batch on the host cores
                 this job is given, rank 0, N=1 only;
   edgeconv_fwd_bwd_ms  the 4-block EdgeConv chain alone (fwd+bwd), and per block;
+                       chain_fp32_mode: the same chain in the fp32 parity mode;
   torch_eager_gpu      the reference op sequence in stock PyTorch-ROCm eager on
                        the same GPU, fp32 and under bf16 autocast (like for like).
 """
@@ -77,6 +78,8 @@ def parse(argv=None):
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse several ranks "
                         "on one GPU)")
+    p.add_argument("--sgd", choices=["fused", "foreach"], default="fused",
+                   help="torch.optim.SGD implementation (both stock PyTorch; the same update)")
     p.add_argument("--sync-bn", action="store_true",
                    help="N>1: SyncBatchNorm (global-batch BN statistics, main_partseg_dist.py:189) instead of "
                         "per-replica BN (main_cls.py:62 DataParallel semantics)")
@@ -192,7 +195,7 @@ def _ms_graph(fn, reps, warm=2):
     return _ms(graph.replay, reps, warm=1)
 
 
-def edgeconv_legs(model, x, reps=10):
+def edgeconv_legs(model, x, reps=10, chain_only=False):
     """The metric's second number: the 4-block EdgeConv chain alone, fwd+bwd
     (train-mode BN, grads w.r.t. W, gamma, beta), and each block on its own
     with synthetic features of its input width."""
@@ -209,6 +212,8 @@ def edgeconv_legs(model, x, reps=10):
         out.backward(g[key])
     res = {"timing": "HIP-graph replay of each leg (fwd+bwd)",
            "chain": round(_ms_graph(lambda: run(x, blocks), reps), 3)}
+    if chain_only:
+        return res
     B, _, N = x.shape
     # block i runs on the features block i-1 produces from the same input (the
     # chain's own kNN graphs; random high-dimensional features would time the
@@ -537,10 +542,14 @@ def main():
                     dist.broadcast(t, 0)
         else:
             net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
-    try:  # one fused kernel for the whole parameter list (same math as the foreach form)
-        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
-    except (RuntimeError, TypeError, ValueError):
-        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt = None
+    if args.sgd == "fused":
+        try:  # one fused kernel for the whole parameter list (same math as the foreach form)
+            opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
+        except (RuntimeError, TypeError, ValueError):
+            opt = None
+    if opt is None:
+        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, foreach=True)
     pts = torch.from_numpy(make_input(args, per_gpu, seed=rank)).to(dev)
     x = pts.permute(0, 2, 1)  # (B,C,N) view, as main_cls.py:91 feeds the model
 
@@ -704,6 +713,10 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_edgeconv_leg:
             legs = edgeconv_legs(model, x)
+            if args.precision != "fp32":   # the parity mode's chain beside stock fp32 eager
+                dgx_prec.set("fp32")
+                legs["chain_fp32_mode"] = edgeconv_legs(model, x, chain_only=True)["chain"]
+                dgx_prec.set(args.precision)
             if not args.no_eager_baseline:
                 # the same 4-block chain in stock PyTorch-ROCm eager (the metric's EdgeConv ratio)
                 for name, dt in (("fp32", None), ("bf16_autocast", torch.bfloat16)):
@@ -715,6 +728,8 @@ def main():
                 ref = legs.get(f"torch_eager_{'fp32' if args.precision == 'fp32' else 'bf16_autocast'}")
                 if isinstance(ref, float):
                     legs["engine_speedup_vs_eager"] = round(ref / legs["chain"], 2)
+                if isinstance(legs.get("torch_eager_fp32"), float) and "chain_fp32_mode" in legs:
+                    legs["fp32_mode_speedup_vs_eager_fp32"] = round(legs["torch_eager_fp32"] / legs["chain_fp32_mode"], 2)
             result["edgeconv_fwd_bwd_ms"] = legs
         if not args.no_posemb_leg:
             result["posemb_edge_mlp"] = posemb_edge_leg(dev)

@@ -80,6 +80,46 @@ __global__ void graph_feature_bwd_kernel(const float* __restrict__ dout, int B, 
     }
 }
 
+// The same gradient without atomics: one thread per (b, c, j) sums j's
+// in-edges from the reverse kNN graph (dgx_graph_reverse: CSR rows of edge ids
+// (i << 6) | slot, ascending) in that fixed order, then the centre terms of
+// j's own row — every dx element has one writer and a fixed summation order.
+__global__ void graph_feature_bwd_csr_kernel(const float* __restrict__ dout, int B, int C, int N, int k, int mode,
+                                             const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
+                                             float* __restrict__ dx) {
+    const int64_t total = (int64_t)B * C * N;
+    const bool two = mode == DGX_GF_CAT || mode == DGX_GF_DIFFCAT;
+    const int Cp = two ? 2 * C : C;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int n = (int)(t % N);
+        const int64_t bc = t / N;
+        const int c = (int)(bc % C);
+        const int b = (int)(bc / C);
+        const int64_t j = (int64_t)b * N + n;
+        const int32_t beg = rowptr[j], end = rowptr[j + 1];
+        float acc = 0.f;
+        for (int32_t e = beg; e < end; ++e) {
+            const int32_t id = edges[e];
+            const int64_t i = id >> 6;   // global point of the edge's source
+            const int s = id & 63;
+            if (mode == DGX_GF_KNN_ONLY) acc += dout[(i * k + s) * C + c];
+            else acc += dout[(((int64_t)b * Cp + c) * N + (i - (int64_t)b * N)) * k + s];
+        }
+        float centre = 0.f;
+        if (mode != DGX_GF_KNN_ONLY) {
+            const float* d = dout + (((int64_t)b * Cp + c) * N + n) * k;
+            if (mode == DGX_GF_DISP || mode == DGX_GF_DIFFCAT)
+                for (int kk = 0; kk < k; ++kk) centre -= d[kk];
+            if (two) {
+                const float* dc = dout + (((int64_t)b * Cp + C + c) * N + n) * k;
+                for (int kk = 0; kk < k; ++kk) centre += dc[kk];
+            }
+        }
+        dx[(int64_t)b * C * N + (int64_t)c * N + n] += acc + centre;
+    }
+}
+
 inline int grid_for(int64_t total, int block) {
     int64_t g = (total + block - 1) / block;
     return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
@@ -108,6 +148,17 @@ int dgx_graph_feature_f32(const float* x, int64_t sB, int64_t sC, int64_t sN, in
     if (total == 0) return DGX_OK;
     hipLaunchKernelGGL(graph_feature_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream), x, sB, sC,
                        sN, B, C, N, idx, k, mode, out);
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_graph_feature_bwd_csr_f32(const float* dout, int B, int C, int N, int k, int mode, const int32_t* rowptr,
+                                  const int32_t* edges, float* dx, void* stream) {
+    if (!dout || !rowptr || !edges || !dx || B < 0 || C < 1 || N < 1 || k < 1 || k > 64 || mode < 0 || mode > 3)
+        return DGX_EINVAL;
+    const int64_t total = (int64_t)B * C * N;
+    if (total == 0) return DGX_OK;
+    hipLaunchKernelGGL(graph_feature_bwd_csr_kernel, dim3(grid_for(total, 256)), dim3(256), 0, dgx_stream(stream),
+                       dout, B, C, N, k, mode, rowptr, edges, dx);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

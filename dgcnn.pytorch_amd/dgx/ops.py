@@ -226,9 +226,17 @@ class _GraphFeature(torch.autograd.Function):
         B, C, N = ctx.shape
         dout = dout.contiguous().float()
         dx = torch.zeros((B, C, N), dtype=torch.float32, device=dout.device)
+        k = idx32.shape[-1]
         with torch.cuda.device(dout.device):
-            rc = nat.lib().dgx_graph_feature_bwd_f32(nat.f32(dout), B, C, N, nat.i32(idx32), idx32.shape[-1],
-                                                     ctx.mode, nat.f32(dx), nat.stream_of(dout))
+            if k <= 64 and B * N < (1 << 25):
+                # deterministic: pull over the reverse kNN graph (no float atomics)
+                from .edgeconv import _reverse_graphs
+                (rowptr, edges), = _reverse_graphs([idx32.contiguous()], B, N, k, dout.device)
+                rc = nat.lib().dgx_graph_feature_bwd_csr_f32(nat.f32(dout), B, C, N, k, ctx.mode, nat.i32(rowptr),
+                                                             nat.i32(edges), nat.f32(dx), nat.stream_of(dout))
+            else:
+                rc = nat.lib().dgx_graph_feature_bwd_f32(nat.f32(dout), B, C, N, nat.i32(idx32), k,
+                                                         ctx.mode, nat.f32(dx), nat.stream_of(dout))
         nat.check(rc, "graph_feature backward")
         return dx, None, None
 

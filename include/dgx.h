@@ -111,10 +111,18 @@ int dgx_graph_feature_f32(const float* x, int64_t sB, int64_t sC, int64_t sN,
                           int B, int C, int N, const int32_t* idx, int k,
                           int mode, float* out, void* stream);
 /* Backward of dgx_graph_feature_f32 (autograd of dgcnn.py:31-44): adds into
- * dx (B,C,N) contiguous. Uses float atomics. */
+ * dx (B,C,N) contiguous. Uses float atomics (summation order not fixed); the
+ * CSR form below is the deterministic one, this one serves k > 64. */
 int dgx_graph_feature_bwd_f32(const float* dout, int B, int C, int N,
                               const int32_t* idx, int k, int mode, float* dx,
                               void* stream);
+/* The same gradient, deterministic: every dx element summed by one thread
+ * over the point's in-edges in the reverse graph's order (rowptr / edges from
+ * dgx_graph_reverse of the same idx, k <= 64), then its own row's centre
+ * terms; no atomics. */
+int dgx_graph_feature_bwd_csr_f32(const float* dout, int B, int C, int N, int k,
+                                  int mode, const int32_t* rowptr, const int32_t* edges,
+                                  float* dx, void* stream);
 
 /* ---- a3: decomposed EdgeConv block, replaces
  *   get_graph_feature -> Conv2d(2C,Co,1,bias=False) -> BatchNorm2d -> LeakyReLU

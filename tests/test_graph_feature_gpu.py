@@ -35,3 +35,33 @@ def test_graph_feature_backward(cuda, mode):
     ref.backward(gout)
     np.testing.assert_array_equal(out.detach().cpu().numpy(), ref.detach().numpy())
     assert rel_err(xg.grad.cpu(), xc.grad) < 1e-6
+
+
+@pytest.mark.parametrize("mode", ["cat", "disp", "knn", "diff"])
+def test_graph_feature_backward_deterministic(cuda, mode):
+    """The backward pulls over the reverse kNN graph (dgx_graph_feature_bwd_csr_f32):
+    bitwise repeatable, equal to the atomic scatter form up to summation order,
+    at a hub-heavy graph (neighbours drawn mostly from 4 points)."""
+    from dgx import _native as nat
+    from dgx import ops
+    torch.manual_seed(1)
+    B, C, N, k = 3, 7, 300, 12
+    x = torch.randn(B, C, N, device=cuda)
+    idx = torch.where(torch.rand(B, N, k, device=cuda) < 0.6, torch.randint(0, 4, (B, N, k), device=cuda),
+                      torch.randint(0, N, (B, N, k), device=cuda)).to(torch.int32)
+    kw = {"knn_only": mode == "knn", "disp_only": mode == "disp", "mode": "diff" if mode == "diff" else "cat"}
+    grads = []
+    for _ in range(2):
+        xg = x.clone().requires_grad_(True)
+        out = ops.graph_feature(xg, k=k, idx=idx, **kw)
+        out.backward(torch.ones_like(out) * torch.linspace(-1, 1, out.numel(), device=cuda).view(out.shape))
+        grads.append(xg.grad)
+    assert torch.equal(grads[0], grads[1])
+    gm = {"cat": nat.GF_CAT, "disp": nat.GF_DISP, "knn": nat.GF_KNN_ONLY, "diff": nat.GF_DIFFCAT}[mode]
+    out = ops.graph_feature(x, k=k, idx=idx, **kw)
+    dout = (torch.ones_like(out) * torch.linspace(-1, 1, out.numel(), device=cuda).view(out.shape)).contiguous()
+    dx = torch.zeros(B, C, N, device=cuda)
+    nat.check(nat.lib().dgx_graph_feature_bwd_f32(nat.f32(dout), B, C, N, nat.i32(idx), k, gm, nat.f32(dx),
+                                                  nat.stream_of(dx)), "atomic bwd")
+    torch.cuda.synchronize()
+    assert rel_err(grads[0].cpu(), dx.cpu()) < 1e-6
