@@ -60,7 +60,7 @@ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // A/B switches of the schedule (dgx.edgeconv / dgx.gemm environment flags), one word
 struct Opts {
-  bool packed = true;        // bf16: backward scatter reads packed dz|slot words
+  bool packed = true;        // bf16 / split fp32: backward scatter reads packed dz|slot words
   bool fold_bwd = true;      // BN backward finalize in the scatter's prologue
   bool fuse_image = true;    // blocks' apply writes the next kNN's operand image
   bool fuse_edge_dz = true;  // bf16: block l-1's dz from block l's dX GEMM epilogue
@@ -834,7 +834,10 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
     check(dgx_graph_reverse_multi(m, ip.data(), B, N, k, rp.data(), ep.data(), d.stream), "reverse graphs");
   }
   const double count = (double)M * k;
-  const bool packed = bf16 && o.packed;
+  // packed dz|slot words (18 significant bits of dz) in bf16 mode, and in the
+  // fp32 mode whose conv5 GEMMs are split bf16 (2^-16 per product: the same
+  // precision class); exact dz + slot bytes with exact fp32 products
+  const bool packed = (bf16 || o.split32) && o.packed;
   Tensor pre_dz, pre_part;
   int pre_rows = 0;
   bool have_pre = false;

@@ -39,8 +39,9 @@ from .ops import knn_raw, reduction_order
 
 _tls = threading.local()
 
-# bf16 mode: the backward scatter reads packed dz|slot words (DGX_SCATTER_PACKED=0:
-# separate dz and slot arrays, A/B only; cfg2 step 1.4178 -> 1.4131 ms)
+# bf16 mode (and the fp32 mode with split-bf16 conv5 GEMMs, SPLIT32): the
+# backward scatter reads packed dz|slot words (DGX_SCATTER_PACKED=0: separate dz
+# and slot arrays, A/B only; cfg2 step 1.4178 -> 1.4131 ms)
 SCATTER_PACKED = os.environ.get("DGX_SCATTER_PACKED", "1") == "1"
 # BN backward finalize folded into the scatter's prologue (DGX_FOLD_BN_BWD=0: a
 # separate finalize launch, A/B only; cfg2 step 1.4131 -> 1.4065 ms)
