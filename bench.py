@@ -78,8 +78,9 @@ def parse(argv=None):
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse several ranks "
                         "on one GPU)")
-    p.add_argument("--sgd", choices=["fused", "foreach"], default="fused",
-                   help="torch.optim.SGD implementation (both stock PyTorch; the same update)")
+    p.add_argument("--sgd", choices=["fused", "foreach", "dgx"], default="dgx",
+                   help="SGD implementation: torch.optim.SGD fused / foreach, or dgx.optim.SGD (one HIP "
+                        "launch); the same update")
     p.add_argument("--sync-bn", action="store_true",
                    help="N>1: SyncBatchNorm (global-batch BN statistics, main_partseg_dist.py:189) instead of "
                         "per-replica BN (main_cls.py:62 DataParallel semantics)")
@@ -543,7 +544,10 @@ def main():
         else:
             net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
     opt = None
-    if args.sgd == "fused":
+    if args.sgd == "dgx":   # the same update in one HIP launch (dgx/optim.py)
+        from dgx.optim import SGD as DgxSGD
+        opt = DgxSGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    elif args.sgd == "fused":
         try:  # one fused kernel for the whole parameter list (same math as the foreach form)
             opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, fused=True)
         except (RuntimeError, TypeError, ValueError):
@@ -673,7 +677,10 @@ def main():
                    "model": "DGCNN", "global_batch": total, "batch_per_gpu": per_gpu, "points": args.points,
                    "seq_len": args.points, "k": args.k, "emb_dim": args.emb, "in_channels": args.in_dims,
                    "parallelism": f"dp{world}" + ("+syncbn" if (args.sync_bn and world > 1) else ""),
-                   "backend": ("rccl" if args.backend == "nccl" else "gloo") if world > 1 else "none"},
+                   "backend": ("rccl" if args.backend == "nccl" else "gloo") if world > 1 else "none",
+                   "optimizer": {"dgx": "dgx.optim.SGD (one launch)", "fused": "torch.optim.SGD fused",
+                                 "foreach": "torch.optim.SGD foreach"}[args.sgd]
+                   + " lr 0.1 momentum 0.9 wd 1e-4"},
     }
     if not args.no_roofline_leg:
         # the same K steps again with HIP events around ONLY the kNN selection

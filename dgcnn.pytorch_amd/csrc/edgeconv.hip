@@ -353,8 +353,9 @@ __global__ __launch_bounds__(EC_THREADS) void edge_gather_lds_kernel(
     }
 }
 
-// one block per channel: fp64 tree reduction of the partial rows (fp32 per-block
-// partials, or fp64 global sums after a SyncBatchNorm all-reduce)
+// one wave per channel (4 channels per block): fp64 sums of the partial rows
+// (fp32 per-block partials, or fp64 global sums after a SyncBatchNorm
+// all-reduce), lanes strided over the rows then a shuffle tree — no barriers
 template <typename T>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ partials, int nrows, int Co,
                                                           double count, const float* __restrict__ gamma,
@@ -365,20 +366,18 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ 
                                                           float* __restrict__ invstd_out,
                                                           const int64_t* nbt,
                                                           float* rmean_new, float* rvar_new, int64_t* nbt_new) {
-    __shared__ double r1[256], r2[256];
-    const int o = blockIdx.x, t = threadIdx.x;
+    const int t = threadIdx.x & 63, o = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (nbt && o == 0 && t == 0) *nbt_new = *nbt + 1;  // BatchNorm.num_batches_tracked, no extra launch
+    if (o >= Co) return;
     double s1 = 0.0, s2 = 0.0;
-    for (int i = t; i < nrows; i += 256) {
+    for (int i = t; i < nrows; i += 64) {
         s1 += (double)partials[(int64_t)i * 2 * Co + o];
         s2 += (double)partials[(int64_t)i * 2 * Co + Co + o];
     }
-    r1[t] = s1;
-    r2[t] = s2;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (t < w) { r1[t] += r1[t + w]; r2[t] += r2[t + w]; }
-        __syncthreads();
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        s1 += __shfl_xor(s1, m);
+        s2 += __shfl_xor(s2, m);
     }
     if (t != 0) return;
     // count < 0: the element count follows the sums on the device (SyncBatchNorm:
@@ -388,8 +387,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const T* __restrict__ 
     // 1 / (num_batches_tracked + 1) read here instead of on the host (the
     // counter input is only read: the caller passes a separate nbt_new)
     if (momentum < 0.0) momentum = nbt ? 1.0 / (double)(*nbt + 1) : 0.0;
-    const double mean = r1[0] / count;
-    double var = r2[0] / count - mean * mean;
+    const double mean = s1 / count;
+    double var = s2 / count - mean * mean;
     if (var < 0.0) var = 0.0;
     const double invstd = 1.0 / sqrt(var + eps);
     const double a = (gamma ? (double)gamma[o] : 1.0) * invstd;
@@ -557,23 +556,19 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const T* __restric
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ c0, float* __restrict__ c1,
                                                               int accumulate) {
-    __shared__ double r1[256], r2[256];
-    const int o = blockIdx.x, t = threadIdx.x;
+    const int t = threadIdx.x & 63, o = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per channel
+    if (o >= Co) return;
     double s1 = 0.0, s2 = 0.0;
-    for (int i = t; i < nrows; i += 256) {
+    for (int i = t; i < nrows; i += 64) {
         s1 += (double)partials[(int64_t)i * 2 * Co + o];
         s2 += (double)partials[(int64_t)i * 2 * Co + Co + o];
     }
-    r1[t] = s1;
-    r2[t] = s2;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (t < w) { r1[t] += r1[t + w]; r2[t] += r2[t + w]; }
-        __syncthreads();
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        s1 += __shfl_xor(s1, m);
+        s2 += __shfl_xor(s2, m);
     }
     if (t != 0) return;
-    s1 = r1[0];
-    s2 = r2[0];
     if (count < 0.0) count = (double)partials[(int64_t)nrows * 2 * Co];   // device-side count, as above
     if (dbeta) dbeta[o] = (float)(accumulate ? (double)dbeta[o] + s1 : s1);
     if (dgamma) dgamma[o] = (float)(accumulate ? (double)dgamma[o] + s2 : s2);
@@ -1453,7 +1448,7 @@ int dgx_bn_finalize_out_f32(const float* partials, int nrows, int Co, double cou
         return DGX_EINVAL;
     // cumulative average: every block reads the counter, so it may not be updated in place
     if (momentum < 0.0 && num_batches_tracked && num_batches_tracked == num_batches_tracked_new) return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((Co + 3) / 4), dim3(256), 0, dgx_stream(stream), partials, nrows, Co,
                        count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
                        num_batches_tracked, running_mean_new, running_var_new, num_batches_tracked_new);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
@@ -1479,7 +1474,7 @@ int dgx_bn_finalize_out_f64(const double* sums, int nrows, int Co, double count,
         return DGX_EINVAL;
     // cumulative average: every block reads the counter, so it may not be updated in place
     if (momentum < 0.0 && num_batches_tracked && num_batches_tracked == num_batches_tracked_new) return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
+    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3((Co + 3) / 4), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, mean, invstd,
                        num_batches_tracked, running_mean_new, running_var_new, num_batches_tracked_new);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
@@ -1561,7 +1556,7 @@ int dgx_bn_bwd_finalize_f32(const float* partials, int nrows, int Co, double cou
                             float* c1, int accumulate, void* stream) {
     if (!partials || nrows < 1 || Co < 1 || count <= 0.0 || !scale || !mean || !invstd || !c0 || !c1)
         return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(Co), dim3(256), 0, dgx_stream(stream), partials, nrows,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3((Co + 3) / 4), dim3(256), 0, dgx_stream(stream), partials, nrows,
                        Co, count, scale, mean, invstd, dgamma, dbeta, c0, c1, accumulate);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
@@ -1571,7 +1566,7 @@ int dgx_bn_bwd_finalize_f64(const double* sums, int nrows, int Co, double count,
                             float* c1, int accumulate, void* stream) {
     if (!sums || nrows < 1 || Co < 1 || count == 0.0 || !scale || !mean || !invstd || !c0 || !c1)
         return DGX_EINVAL;
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(Co), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3((Co + 3) / 4), dim3(256), 0, dgx_stream(stream), sums, nrows, Co,
                        count, scale, mean, invstd, dgamma, dbeta, c0, c1, accumulate);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }

@@ -364,6 +364,51 @@ __global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi_kernel(SlabJobs
     }
 }
 
+// The same reduction with four consecutive elements per lane (16-byte slab
+// loads, a quarter of the workgroups) when every job's columns are a multiple
+// of 4: each element keeps slab_reduce_kernel's groups and order (identical
+// results). Job j owns blocks [first[j], first[j+1]) of SR_E * 4 elements.
+__global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi4_kernel(SlabJobs jobs) {
+    __shared__ float4 red[SR_G][SR_E];
+    int j = 0;
+    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+    const float* __restrict__ slab = jobs.slab[j];
+    const int S = jobs.S[j], cols = jobs.cols[j], split = jobs.split[j];
+    const int64_t total = (int64_t)jobs.rows[j] * cols;   // a multiple of 4
+    const int el = threadIdx.x % SR_E, g = threadIdx.x / SR_E;
+    const int64_t e = ((int64_t)(blockIdx.x - jobs.first[j]) * SR_E + el) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) {
+        int s = g;
+        for (; s + (SR_U - 1) * SR_G < S; s += SR_U * SR_G) {
+            float4 v[SR_U];
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (int64_t)(s + u * SR_G) * total + e);
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) {
+                acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+            }
+        }
+        for (; s < S; s += SR_G) {
+            const float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)s * total + e);
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+    }
+    red[g][el] = acc;
+    __syncthreads();
+    if (g == 0 && e < total) {
+        const float4 a = red[0][el], b = red[1][el], c = red[2][el], d = red[3][el];
+        const float sum[4] = {((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
+                              ((a.w + b.w) + c.w) + d.w};
+        const int r = (int)(e / cols), c0 = (int)(e - (int64_t)r * cols);
+        const int orow = r < split ? r : r - split;
+        const int ocol = r < split ? c0 : c0 + cols;
+        float* dst = jobs.out[j] + (int64_t)orow * jobs.ldo[j] + ocol;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dst[u] = sum[u];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // bf16-operand GEMMs staged by LDS-DMA (global_load_lds_dwordx4).
 // Both operands bf16 in HBM, either both k-contiguous ("NT": C = A B^T, the
@@ -1624,8 +1669,22 @@ int dgx_slab_reduce_multi_f32(int n, const float* const* slab, const int* S, con
     }
     jobs.first[n] = blocks;
     if (blocks == 0) return DGX_OK;
-    hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3((unsigned)blocks), dim3(SR_E * SR_G), 0, dgx_stream(stream),
-                       jobs);
+    bool vec4 = true;   // 4 consecutive elements per lane: whole 4-groups in one row, 16-byte slab loads
+    for (int j = 0; j < n; ++j)
+        vec4 = vec4 && cols[j] % 4 == 0 && (reinterpret_cast<uintptr_t>(slab[j]) & 15) == 0;
+    if (vec4) {
+        int b4 = 0;
+        for (int j = 0; j < n; ++j) {
+            jobs.first[j] = b4;
+            b4 += (int)(((int64_t)rows[j] * cols[j] / 4 + SR_E - 1) / SR_E);
+        }
+        jobs.first[n] = b4;
+        hipLaunchKernelGGL(slab_reduce_multi4_kernel, dim3((unsigned)b4), dim3(SR_E * SR_G), 0, dgx_stream(stream),
+                           jobs);
+    } else {
+        hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3((unsigned)blocks), dim3(SR_E * SR_G), 0,
+                           dgx_stream(stream), jobs);
+    }
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -40,6 +40,7 @@ _SIGS = {
     "dgx_graph_feature_f32": [_vp, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_f32": [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp],
     "dgx_graph_feature_bwd_csr_f32": [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp],
+    "dgx_sgd_step_f32": [_i32, _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _i32, _i32, _i32, _vp],
     "dgx_edge_partials_rows": [_i32, _i32, _i32],
     "dgx_edge_fwd_gather_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "dgx_edge_fwd_eval_f32": [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _i32, _vp],

@@ -577,6 +577,17 @@ int dgx_attn_bwd(int dtype, const void* q, int64_t qsP, int64_t qsB, int64_t qsN
 /* The keep mask (rows = B*H*Nq, Nk) the kernels draw for (p, seed), u8 0/1. */
 int dgx_attn_dropout_mask(int64_t rows, int Nk, float dropout_p, uint64_t seed, uint8_t* out, void* stream);
 
+
+/* ---- training-step utility: torch.optim.SGD's update (lr, momentum,
+ * dampening, weight_decay, nesterov, maximize) over n <= 48 fp32 tensors in
+ * one launch (torch's fused form runs ~22 workgroups for a DGCNN's ~0.6 M
+ * parameters); first != 0 sets the momentum buffers to the step's gradient
+ * (torch's first step). torch/optim/sgd.py's arithmetic in fp32 (last-bit
+ * differences from FMA contraction possible). */
+int dgx_sgd_step_f32(int n, float* const* params, const float* const* grads, float* const* momentum_bufs,
+                     const int64_t* numels, float lr, float weight_decay, float momentum, float dampening,
+                     int nesterov, int maximize, int first, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

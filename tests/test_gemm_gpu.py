@@ -320,3 +320,37 @@ def test_gemm_edge_dz_epilogue(cuda, M, N, K):
     s, s_ref = part.double().sum(0), part_ref.double().sum(0)
     scale = part_ref.double().abs().sum(0)
     assert float(((s - s_ref).abs() / scale.clamp_min(1e-30)).max()) < 1e-5
+
+
+def test_slab_reduce_multi_matches_single(cuda):
+    """dgx_slab_reduce_multi_f32 (the backward's one weight-gradient reduce; the
+    4-elements-per-lane kernel when every job's columns are a multiple of 4)
+    sums every element exactly as dgx_slab_reduce_f32 does: bitwise equal,
+    including stacked [W1 | W2] outputs (split) and a strided destination."""
+    import ctypes
+
+    from dgx import _native as nat
+    L = nat.lib()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    for shapes in ([(16, 1024, 512, 0), (4, 128, 64, 64), (37, 64, 6, 32)],     # cols % 4 == 0 -> vec kernel
+                   [(16, 130, 66, 0), (3, 20, 3, 10)]):                          # scalar kernel
+        jobs = []
+        for S, rows, cols, split in shapes:
+            slab = torch.randn(S, rows, cols, generator=g).to(cuda)
+            orows, ocols = (rows - split, 2 * cols) if split else (rows, cols)
+            out = torch.full((orows, ocols + 4), float("nan"), device=cuda)
+            ref = torch.full_like(out, float("nan"))
+            nat.check(L.dgx_slab_reduce_f32(nat.f32(slab), S, rows, cols, split, nat.f32(ref), ocols + 4,
+                                            nat.stream_of(slab)), "slab single")
+            jobs.append((slab, S, rows, cols, split, out, ocols + 4, ref))
+        n = len(jobs)
+        arr = ctypes.c_void_p * n
+        ints = ctypes.c_int * n
+        nat.check(L.dgx_slab_reduce_multi_f32(n, arr(*[j[0].data_ptr() for j in jobs]), ints(*[j[1] for j in jobs]),
+                                              ints(*[j[2] for j in jobs]), ints(*[j[3] for j in jobs]),
+                                              ints(*[j[4] for j in jobs]), arr(*[j[5].data_ptr() for j in jobs]),
+                                              (ctypes.c_int64 * n)(*[j[6] for j in jobs]), nat.stream_of(jobs[0][0])),
+                  "slab multi")
+        torch.cuda.synchronize()
+        for j in jobs:
+            assert torch.equal(j[5].nan_to_num(7.0), j[7].nan_to_num(7.0))
