@@ -330,12 +330,11 @@ struct SlabJobs {
     float* out[SRM_MAXJ];
     int64_t ldo[SRM_MAXJ];
     int S[SRM_MAXJ], rows[SRM_MAXJ], cols[SRM_MAXJ], split[SRM_MAXJ], first[SRM_MAXJ + 1];
+    int vec4[SRM_MAXJ];   // job reduced 4 consecutive elements per lane (slab_reduce_block4)
     int n;
 };
-__global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi_kernel(SlabJobs jobs) {
-    __shared__ float red[SR_G][SR_E];
-    int j = 0;
-    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+// one job's block, one element per lane (slab_reduce_kernel's groups and order)
+__device__ __forceinline__ void slab_reduce_block1(const SlabJobs& jobs, int j, float (*red)[SR_E]) {
     const float* __restrict__ slab = jobs.slab[j];
     const int S = jobs.S[j], cols = jobs.cols[j], split = jobs.split[j];
     const int64_t total = (int64_t)jobs.rows[j] * cols;
@@ -364,14 +363,10 @@ __global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi_kernel(SlabJobs
     }
 }
 
-// The same reduction with four consecutive elements per lane (16-byte slab
-// loads, a quarter of the workgroups) when every job's columns are a multiple
-// of 4: each element keeps slab_reduce_kernel's groups and order (identical
-// results). Job j owns blocks [first[j], first[j+1]) of SR_E * 4 elements.
-__global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi4_kernel(SlabJobs jobs) {
-    __shared__ float4 red[SR_G][SR_E];
-    int j = 0;
-    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+// one job's block, four consecutive elements per lane (16-byte slab loads, a
+// quarter of the workgroups; columns a multiple of 4): every element keeps
+// slab_reduce_kernel's groups and order, so the results are identical
+__device__ __forceinline__ void slab_reduce_block4(const SlabJobs& jobs, int j, float4 (*red)[SR_E]) {
     const float* __restrict__ slab = jobs.slab[j];
     const int S = jobs.S[j], cols = jobs.cols[j], split = jobs.split[j];
     const int64_t total = (int64_t)jobs.rows[j] * cols;   // a multiple of 4
@@ -407,6 +402,14 @@ __global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi4_kernel(SlabJob
 #pragma unroll
         for (int u = 0; u < 4; ++u) dst[u] = sum[u];
     }
+}
+
+__global__ __launch_bounds__(SR_E * SR_G) void slab_reduce_multi_kernel(SlabJobs jobs) {
+    __shared__ float4 red[SR_G][SR_E];
+    int j = 0;
+    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+    if (jobs.vec4[j]) slab_reduce_block4(jobs, j, red);
+    else slab_reduce_block1(jobs, j, reinterpret_cast<float (*)[SR_E]>(red));
 }
 
 // ---------------------------------------------------------------------------
@@ -1664,27 +1667,16 @@ int dgx_slab_reduce_multi_f32(int n, const float* const* slab, const int* S, con
         jobs.rows[j] = rows[j];
         jobs.cols[j] = cols[j];
         jobs.split[j] = split[j];
+        // 4 consecutive elements per lane: whole 4-groups in one row, 16-byte slab loads
+        jobs.vec4[j] = cols[j] % 4 == 0 && (reinterpret_cast<uintptr_t>(slab[j]) & 15) == 0;
         jobs.first[j] = blocks;
-        blocks += (int)(((int64_t)rows[j] * cols[j] + SR_E - 1) / SR_E);
+        const int64_t units = (int64_t)rows[j] * cols[j] / (jobs.vec4[j] ? 4 : 1);
+        blocks += (int)((units + SR_E - 1) / SR_E);
     }
     jobs.first[n] = blocks;
     if (blocks == 0) return DGX_OK;
-    bool vec4 = true;   // 4 consecutive elements per lane: whole 4-groups in one row, 16-byte slab loads
-    for (int j = 0; j < n; ++j)
-        vec4 = vec4 && cols[j] % 4 == 0 && (reinterpret_cast<uintptr_t>(slab[j]) & 15) == 0;
-    if (vec4) {
-        int b4 = 0;
-        for (int j = 0; j < n; ++j) {
-            jobs.first[j] = b4;
-            b4 += (int)(((int64_t)rows[j] * cols[j] / 4 + SR_E - 1) / SR_E);
-        }
-        jobs.first[n] = b4;
-        hipLaunchKernelGGL(slab_reduce_multi4_kernel, dim3((unsigned)b4), dim3(SR_E * SR_G), 0, dgx_stream(stream),
-                           jobs);
-    } else {
-        hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3((unsigned)blocks), dim3(SR_E * SR_G), 0,
-                           dgx_stream(stream), jobs);
-    }
+    hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3((unsigned)blocks), dim3(SR_E * SR_G), 0, dgx_stream(stream),
+                       jobs);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

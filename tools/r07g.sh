@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 5, session r07g: per-job vectorised slab reduce: gemm tests, weight-gradient suites, bench, trace
+set -o pipefail
+export PYTHONDONTWRITEBYTECODE=1
+mkdir -p gpurun_out
+T="--timeout 300 --timeout-method thread"
+timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_host_ext_gpu.py tests/test_edgeconv_gpu.py -q $T > gpurun_out/r07g_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/r07g_tests.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-eager-baseline --no-edgeconv-leg --no-posemb-leg --no-attention-leg > gpurun_out/r07g_bench.log 2>&1 || { tail -30 gpurun_out/r07g_bench.log; exit 1; }
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/r07g_bench.log | head -2
+KT_ONLY=1 timeout -k 10 400 bash tools/profile.sh r07g_cfg2 --steps 10 --warmup 3 > gpurun_out/r07g_prof_cfg2.log 2>&1 || { tail -20 gpurun_out/r07g_prof_cfg2.log; exit 1; }
+grep -E "slab_reduce|sgd_kernel" gpurun_out/prof_r07g_cfg2/kt_summary.txt
