@@ -324,7 +324,7 @@ def test_gemm_edge_dz_epilogue(cuda, M, N, K):
 
 def test_slab_reduce_multi_matches_single(cuda):
     """dgx_slab_reduce_multi_f32 (the backward's one weight-gradient reduce; the
-    4-elements-per-lane kernel when every job's columns are a multiple of 4)
+    4-elements-per-lane path for every job whose columns are a multiple of 4)
     sums every element exactly as dgx_slab_reduce_f32 does: bitwise equal,
     including stacked [W1 | W2] outputs (split) and a strided destination."""
     import ctypes
@@ -332,12 +332,14 @@ def test_slab_reduce_multi_matches_single(cuda):
     from dgx import _native as nat
     L = nat.lib()
     g = torch.Generator(device="cpu").manual_seed(11)
-    for shapes in ([(16, 1024, 512, 0), (4, 128, 64, 64), (37, 64, 6, 32)],     # cols % 4 == 0 -> vec kernel
-                   [(16, 130, 66, 0), (3, 20, 3, 10)]):                          # scalar kernel
+    # (S, rows, cols, split): split == rows is an unstacked output; split < rows
+    # puts rows [split, rows) beside rows [0, split) (the [W1 | W2] layout)
+    for shapes in ([(16, 1024, 512, 1024), (4, 128, 64, 64), (37, 64, 6, 32)],   # per-job 4-wide / scalar
+                   [(16, 130, 66, 130), (3, 20, 3, 10)]):                         # scalar only
         jobs = []
         for S, rows, cols, split in shapes:
             slab = torch.randn(S, rows, cols, generator=g).to(cuda)
-            orows, ocols = (rows - split, 2 * cols) if split else (rows, cols)
+            orows, ocols = (rows - split, 2 * cols) if split < rows else (rows, cols)
             out = torch.full((orows, ocols + 4), float("nan"), device=cuda)
             ref = torch.full_like(out, float("nan"))
             nat.check(L.dgx_slab_reduce_f32(nat.f32(slab), S, rows, cols, split, nat.f32(ref), ocols + 4,
