@@ -3,7 +3,9 @@
 
 One step = DGCNN(emb=1024, k=20) forward + backward + SGD update on one batch of
 synthetic clouds (BASELINE configs[1], "cfg2": 32 clouds of 1024 points per
-GPU), inputs resident in HBM.
+GPU), inputs resident in HBM. The SGD update (lr 0.1, momentum 0.9, weight
+decay 1e-4) is dgx.optim.SGD — torch.optim.SGD's update in one launch;
+``--sgd fused`` runs torch's own fused kernel instead.
 
 N GPUs: one process per GPU over RCCL (torch.distributed "nccl"), DDP gradient
 all-reduce. ``python bench.py --gpus N`` with no WORLD_SIZE in the environment
