@@ -244,7 +244,8 @@ def test_lds_xwt_split_weight(cuda, M, N, K):
 @pytest.mark.parametrize("M,N,K,ta,tb", [(32768, 128, 64, False, True), (32768, 64, 128, False, False),
                                          (130, 70, 33, True, False), (1, 5, 17, False, False),
                                          (256, 512, 32768, True, True), (64, 3, 2048, True, True),
-                                         (4096, 1024, 512, False, True)])
+                                         (4096, 1024, 512, False, True), (33000, 200, 77, False, False),
+                                         (513, 130, 40960, True, True), (40000, 130, 64, True, False)])
 def test_mm32_fp32_mfma(cuda, M, N, K, ta, tb):
     """The parity mode's engine GEMM (dgx_gemm_f32, v_mfma_f32_16x16x4_f32):
     a (M,K) @ b (K,N) for row-major and transposed views read in place,
