@@ -502,6 +502,25 @@ Tensor mm32(const Dev& d, const Tensor& a, const Tensor& b, Tensor* out_view, bo
   return out;
 }
 
+// out (M, N) = a^T b over the R rows of a (R, M) and b (R, N) on the fp32 MFMA
+// GEMM (the parity mode's weight gradients): split-K slabs summed in a fixed
+// order — deferred into the backward's one multi-job reduce — with split_rows
+// un-stacking [W1; W2] into the reference layout [W1 | W2] (no cat)
+void mm32_atb(const Dev& d, const Tensor& a, const Tensor& b, Tensor& out, int split_rows, SlabJobs* defer) {
+  const int R = (int)a.size(0), M = (int)a.size(1), N = (int)b.size(1);
+  TORCH_CHECK(b.size(0) == R, "dgx mm32_atb: row counts differ");
+  Op32 A = op32(a.t(), 1), Bo = op32(b, 0);
+  const int S = dgx_gemm_f32_splits(M, N, R);
+  int64_t kchunk = cdiv(R, S);
+  kchunk = cdiv(kchunk, 16) * 16;
+  const int used = (int)cdiv(R, kchunk);
+  Tensor slab = at::empty({used, M, N}, d.f32);
+  check(dgx_gemm_f32(P(A.t), A.ic, (int)A.ld, P(Bo.t), Bo.ic, (int)Bo.ld, M, N, R, kEpiSlab, S, P(slab), N, nullptr, 0,
+                     d.stream),
+        "gemm f32 (split-K)");
+  reduce_slab(d, slab, used, M, N, split_rows > 0 ? split_rows : M, out, defer);
+}
+
 // reference conv weight (Co, 2C[,1,1]) = [W1 | W2] -> stacked [W1; W2] (2Co, C) (dgx.edgeconv.split_weight)
 Tensor split_weight(const Tensor& w, int cin, int co) {
   Tensor r = w.reshape({co, 2 * cin});
@@ -976,8 +995,9 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
       }
     } else {
       Tensor wcat = split_weight(ly.w, cin, co);
-      Tensor dwcat = mm32(d, dPQ.t(), X, nullptr, false);   // (2Co, C)
-      g.dw[li] = at::cat({dwcat.narrow(0, 0, co), dwcat.narrow(0, co, co)}, 1).reshape(ly.w.sizes());
+      Tensor gw = at::empty({co, 2 * cin}, d.f32);   // dW = dPQ^T X, un-stacked to [W1 | W2] by the reduce
+      mm32_atb(d, dPQ, X, gw, co, slabs);
+      g.dw[li] = gw.view(ly.w.sizes());
       if (li > 0) {
         Tensor dst = dxcat.narrow(1, prev, cin);
         mm32(d, dPQ, wcat, &dst, true);
