@@ -994,15 +994,14 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
         g.dx = dx.view({B, N, C0}).permute({0, 2, 1});
       }
     } else {
-      Tensor wcat = split_weight(ly.w, cin, co);
       Tensor gw = at::empty({co, 2 * cin}, d.f32);   // dW = dPQ^T X, un-stacked to [W1 | W2] by the reduce
       mm32_atb(d, dPQ, X, gw, co, slabs);
       g.dw[li] = gw.view(ly.w.sizes());
       if (li > 0) {
         Tensor dst = dxcat.narrow(1, prev, cin);
-        mm32(d, dPQ, wcat, &dst, true);
+        mm32(d, dPQ, split_weight(ly.w, cin, co), &dst, true);
       } else if (x_needs_grad) {
-        g.dx = mm32(d, dPQ, wcat, nullptr, false).view({B, N, C0}).permute({0, 2, 1});
+        g.dx = mm32(d, dPQ, split_weight(ly.w, cin, co), nullptr, false).view({B, N, C0}).permute({0, 2, 1});
       }
     }
   }
