@@ -652,6 +652,37 @@ struct Layer {
   int cin = 0, co = 0;
 };
 
+// the fp32 mode's stacked weights [W1; W2] of the blocks `need` selects, in one
+// launch (dgx_weight_stack_multi_f32; <= 8 per launch); others stay undefined
+std::vector<Tensor> stack_weights_f32(const Dev& d, const std::vector<Layer>& L, const std::vector<bool>& need) {
+  std::vector<Tensor> out(L.size());
+  std::vector<const float*> W;
+  std::vector<float*> O;
+  std::vector<int> Co, C;
+  auto flush = [&]() {
+    if (W.empty()) return;
+    check(dgx_weight_stack_multi_f32((int)W.size(), W.data(), Co.data(), C.data(), O.data(), d.stream),
+          "weight stack");
+    W.clear();
+    O.clear();
+    Co.clear();
+    C.clear();
+  };
+  for (size_t l = 0; l < L.size(); ++l) {
+    if (!need[l]) continue;
+    const Layer& ly = L[l];
+    TORCH_CHECK(ly.w.is_contiguous(), "dgx: contiguous conv weights expected");
+    out[l] = at::empty({2 * ly.co, ly.cin}, d.f32);
+    W.push_back(P(ly.w));
+    O.push_back(P(out[l]));
+    Co.push_back(ly.co);
+    C.push_back(ly.cin);
+    if (W.size() == 8) flush();
+  }
+  flush();
+  return out;
+}
+
 constexpr int kPerLayer = 9;   // saved per block: idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd
 
 struct ChainOut {
@@ -698,6 +729,12 @@ ChainOut chain_forward_impl(const Dev& d, const Tensor& x_in, int k, std::vector
     preps = pw.second;
   }
   const double count = (double)M * k;
+  std::vector<Tensor> w32;   // fp32 mode: every block's stacked weight, one launch
+  if (!bf16) {
+    std::vector<bool> need(n);
+    for (int l = 0; l < n; ++l) need[l] = L[l].cin > kSmallKMax;
+    w32 = stack_weights_f32(d, L, need);
+  }
   bool have16 = false, prev_selecting = false;
   std::pair<Tensor, Tensor> next_prepared;
   bool have_prepared = false;
@@ -742,8 +779,7 @@ ChainOut chain_forward_impl(const Dev& d, const Tensor& x_in, int k, std::vector
         PQ = mm_xwt(d, X, split_weight(ly.w, cin, co), nullptr);   // fp32 operands rounded while staged
       }
     } else {
-      Tensor wt = split_weight(ly.w, cin, co).t();
-      PQ = mm32(d, X, wt, nullptr, false);
+      PQ = mm32(d, X, w32[li].t(), nullptr, false);
     }
     (void)used_prep;
     Tensor out_view = r.xcat.narrow(1, off, co);
@@ -857,6 +893,12 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
   // fp32 mode whose conv5 GEMMs are split bf16 (2^-16 per product: the same
   // precision class); exact dz + slot bytes with exact fp32 products
   const bool packed = (bf16 || o.split32) && o.packed;
+  std::vector<Tensor> w32;   // fp32 mode: stacked weights of the blocks whose input gradient is formed
+  if (!bf16) {
+    std::vector<bool> need(n);
+    for (int l = 0; l < n; ++l) need[l] = l > 0 || x_needs_grad;
+    w32 = stack_weights_f32(d, L, need);
+  }
   Tensor pre_dz, pre_part;
   int pre_rows = 0;
   bool have_pre = false;
@@ -999,9 +1041,9 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
       g.dw[li] = gw.view(ly.w.sizes());
       if (li > 0) {
         Tensor dst = dxcat.narrow(1, prev, cin);
-        mm32(d, dPQ, split_weight(ly.w, cin, co), &dst, true);
+        mm32(d, dPQ, w32[li], &dst, true);
       } else if (x_needs_grad) {
-        g.dx = mm32(d, dPQ, split_weight(ly.w, cin, co), nullptr, false).view({B, N, C0}).permute({0, 2, 1});
+        g.dx = mm32(d, dPQ, w32[li], nullptr, false).view({B, N, C0}).permute({0, 2, 1});
       }
     }
   }

@@ -1197,6 +1197,26 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
     }
 }
 
+constexpr int WP_MAXJ_S = 8;
+// fp32 stacked EdgeConv weights [W1; W2] (2 Co x C) of several blocks in one
+// launch (the parity mode's GEMM operands; the reference layout is [W1 | W2],
+// Co x 2C): job j owns blocks [first[j], first[j+1]), 256 elements each.
+struct WeightStackJobs {
+    const float* W[WP_MAXJ_S];
+    float* out[WP_MAXJ_S];
+    int Co[WP_MAXJ_S], C[WP_MAXJ_S], first[WP_MAXJ_S + 1];
+    int n;
+};
+__global__ __launch_bounds__(256) void weight_stack_multi_kernel(WeightStackJobs jobs) {
+    int j = 0;
+    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+    const int Co = jobs.Co[j], C = jobs.C[j];
+    const int64_t e = (int64_t)(blockIdx.x - jobs.first[j]) * 256 + threadIdx.x;
+    if (e >= (int64_t)2 * Co * C) return;
+    const int r = (int)(e / C), c = (int)(e - (int64_t)r * C);
+    jobs.out[j][e] = jobs.W[j][(int64_t)(r % Co) * 2 * C + (r / Co) * C + c];
+}
+
 // Several weights in one launch (the EdgeConv blocks of one forward): job j
 // owns blocks [first[j], first[j+1]) of the 1-D grid, tiles row-major in it.
 constexpr int WP_MAXJ = 8;
@@ -1625,6 +1645,26 @@ int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt, v
     const dim3 grid((unsigned)((C + WP_T - 1) / WP_T), (unsigned)((rows + WP_T - 1) / WP_T));
     hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, dgx_stream(stream), W, Co, C, stacked,
                        static_cast<bf16*>(nt), static_cast<bf16*>(tn));
+    return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+}
+
+int dgx_weight_stack_multi_f32(int n, const float* const* W, const int* Co, const int* C, float* const* out,
+                               void* stream) {
+    if (n < 1 || n > WP_MAXJ_S || !W || !Co || !C || !out) return DGX_EINVAL;
+    WeightStackJobs jobs;
+    jobs.n = n;
+    int blocks = 0;
+    for (int j = 0; j < n; ++j) {
+        if (!W[j] || !out[j] || Co[j] < 1 || C[j] < 1) return DGX_EINVAL;
+        jobs.W[j] = W[j];
+        jobs.out[j] = out[j];
+        jobs.Co[j] = Co[j];
+        jobs.C[j] = C[j];
+        jobs.first[j] = blocks;
+        blocks += (int)(((int64_t)2 * Co[j] * C[j] + 255) / 256);
+    }
+    jobs.first[n] = blocks;
+    hipLaunchKernelGGL(weight_stack_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, dgx_stream(stream), jobs);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

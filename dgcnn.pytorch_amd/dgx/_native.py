@@ -93,6 +93,7 @@ _SIGS = {
                           _i64, _vp],
     "dgx_weight_prep_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_weight_prep_multi_bf16": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dgx_weight_stack_multi_f32": [_i32, _vp, _vp, _vp, _vp, _vp],
     "dgx_pointconv_bf16_rows": [_i32, _i32],
     "dgx_pointconv_apply_bf16": [_vp, _i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp],
     "dgx_pointconv_bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _vp],

@@ -447,6 +447,11 @@ int dgx_weight_prep_bf16(const float* W, int Co, int C, int stacked, void* nt,
  * unless bit 2 (value 4) is set: then tn is [C][2 rows] = [hi^T | lo^T]. */
 int dgx_weight_prep_multi_bf16(int n, const float* const* W, const int* Co, const int* C, const int* stacked,
                                void* const* nt, void* const* tn, void* stream);
+/* fp32 stacked weights [W1; W2] (2 Co x C, row-major) of n <= 8 EdgeConv
+ * weights W (Co x 2C, the reference's [W1 | W2]) in one launch: the fp32
+ * parity mode's GEMM operands for all blocks of a forward / backward. */
+int dgx_weight_stack_multi_f32(int n, const float* const* W, const int* Co, const int* C, float* const* out,
+                               void* stream);
 
 /* ---- a6: PositionEmbedding's per-edge MLP, replaces
  *   get_graph_feature -> conv1 (Conv2d 2C->C1, BN, LeakyReLU, per edge)

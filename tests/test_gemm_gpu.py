@@ -357,3 +357,31 @@ def test_slab_reduce_multi_matches_single(cuda):
         torch.cuda.synchronize()
         for j in jobs:
             assert torch.equal(j[5].nan_to_num(7.0), j[7].nan_to_num(7.0))
+
+
+def test_weight_stack_multi(cuda):
+    """dgx_weight_stack_multi_f32 (the fp32 mode's per-pass [W1; W2] builder, one
+    launch for every block) equals the reference weight (Co, 2C) split into its
+    x_j / x_i halves and stacked: bit-exact, ragged shapes, and >8 jobs rejected."""
+    import ctypes
+
+    from dgx import _native as nat
+    L = nat.lib()
+    g = torch.Generator(device="cpu").manual_seed(12)
+    shapes = [(64, 64), (64, 64), (128, 64), (256, 128), (1024, 320), (5, 3), (7, 33)]
+    ws = [torch.randn(co, 2 * c, generator=g).to(cuda) for co, c in shapes]
+    outs = [torch.full((2 * co, c), float("nan"), device=cuda) for co, c in shapes]
+    n = len(shapes)
+    arr = ctypes.c_void_p * n
+    ints = ctypes.c_int * n
+    nat.check(L.dgx_weight_stack_multi_f32(n, arr(*[w.data_ptr() for w in ws]), ints(*[s[0] for s in shapes]),
+                                           ints(*[s[1] for s in shapes]), arr(*[o.data_ptr() for o in outs]),
+                                           nat.stream_of(ws[0])), "weight stack")
+    torch.cuda.synchronize()
+    for (co, c), w, o in zip(shapes, ws, outs):
+        assert torch.equal(o, torch.cat([w[:, :c], w[:, c:]], 0))
+    n9 = 9
+    rc = L.dgx_weight_stack_multi_f32(n9, (ctypes.c_void_p * n9)(*([ws[0].data_ptr()] * n9)),
+                                      (ctypes.c_int * n9)(*([64] * n9)), (ctypes.c_int * n9)(*([64] * n9)),
+                                      (ctypes.c_void_p * n9)(*([outs[0].data_ptr()] * n9)), nat.stream_of(ws[0]))
+    assert rc != 0
