@@ -618,21 +618,24 @@ struct RevGraphJobs {
     int32_t* edges[RG_MAX_GRAPHS];
 };
 
-__global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(RevGraphJobs jobs, int B, int N, int k, int P,
-                                                                   int cap) {
+__global__ __launch_bounds__(RG_THREADS) void rev_graph_par_kernel(RevGraphJobs jobs, int G, int B, int N, int k,
+                                                                   int P, int cap) {
     extern __shared__ int32_t rg[];
-    const int gi = blockIdx.x / (B * P);
+    // (graph, cloud) items with all P ranges of one item on one XCD
+    // (dgx_xcd_cloud_map): the item's index list, which every range scans twice,
+    // is fetched into that XCD's L2 once instead of once per range
+    int item, p;
+    if (!dgx_xcd_cloud_map(blockIdx.x, G * B, P, item, p)) return;
+    const int gi = item / B, b = item - gi * B;
     const int32_t* __restrict__ idx = jobs.idx[gi];
     int32_t* __restrict__ rowptr = jobs.rowptr[gi];
     int32_t* __restrict__ edges = jobs.edges[gi];
-    const int blk = blockIdx.x - gi * (B * P);
     const int R = (N + P - 1) / P;
     int32_t* cnt = rg;                 // [R] in-degree -> fill cursor
     int32_t* start = cnt + R;          // [R] local list starts
     int32_t* red = start + R;          // [RG_THREADS / 64 + 2]
     int32_t* list = red + RG_THREADS / 64 + 2;   // [cap] edge ids
     int32_t* ltg = list + cap;                    // [cap] local target of each slot
-    const int b = blk / P, p = blk - b * P;
     const int t = threadIdx.x;
     const int j0 = p * R, j1 = min(N, j0 + R), nr = max(0, j1 - j0);
     const int64_t base = (int64_t)b * N;
@@ -1595,8 +1598,8 @@ int dgx_graph_reverse_multi(int n, const int32_t* const* idx, int B, int N, int 
     const int cap = (int)std::min<int64_t>(RG_CAP, std::max<int64_t>(1024, 7 * ((int64_t)N * k / P) / 4));
     const size_t lds = ((size_t)2 * R + RG_THREADS / 64 + 2 + 2 * (size_t)cap) * sizeof(int32_t);
     if (lds > 160 * 1024) return DGX_EUNSUPPORTED;
-    hipLaunchKernelGGL(rev_graph_par_kernel, dim3((unsigned)(n * B * P)), dim3(RG_THREADS), lds, dgx_stream(stream),
-                       jobs, B, N, k, P, cap);
+    hipLaunchKernelGGL(rev_graph_par_kernel, dim3((unsigned)dgx_xcd_cloud_grid(n * B, P)), dim3(RG_THREADS), lds,
+                       dgx_stream(stream), jobs, n, B, N, k, P, cap);
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 

@@ -64,4 +64,6 @@ def test_graph_feature_backward_deterministic(cuda, mode):
     nat.check(nat.lib().dgx_graph_feature_bwd_f32(nat.f32(dout), B, C, N, nat.i32(idx), k, gm, nat.f32(dx),
                                                   nat.stream_of(dx)), "atomic bwd")
     torch.cuda.synchronize()
-    assert rel_err(grads[0].cpu(), dx.cpu()) < 1e-6
+    # both are fp32 sums in different orders over the hubs' ~540 in-edges each
+    # (the atomic order varies per run; 1.04e-6 seen once): a few fp32 ulps
+    assert rel_err(grads[0].cpu(), dx.cpu()) < 4e-6
