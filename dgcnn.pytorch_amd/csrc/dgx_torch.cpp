@@ -67,6 +67,7 @@ struct Opts {
   int64_t slab_cap_mb = 8;   // split-K slab cap of small weight gradients (0 = off)
   bool split32 = true;       // fp32 mode: conv5 GEMMs as 3-pass split bf16 (hi.hi + hi.lo + lo.hi)
   bool push = false;         // backward scatter: selected-edge dz pushed from the sources (fixed-point LDS sums)
+  bool split_edge = false;   // fp32 mode: EdgeConv dW / dX as 3-pass split bf16 on the scatter's split dPQ planes
 };
 Opts decode(int64_t o) {
   Opts r;
@@ -77,6 +78,7 @@ Opts decode(int64_t o) {
   r.slab_cap_mb = (o >> 8) & 0xff;
   r.split32 = o & 16;
   r.push = o & 32;
+  r.split_edge = o & 64;
   return r;
 }
 
@@ -425,7 +427,8 @@ void lds_atb(const Dev& d, const Tensor& a16, const Tensor& b16, Tensor& out, in
 
 // out = sum_i a_i^T b_i over the pairs (same shapes): every pair's split-K slabs in
 // one buffer, summed by one fixed-order reduce (the fp32 mode's 3-pass weight gradients)
-void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab, Tensor& out, SlabJobs* defer) {
+void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab, Tensor& out, SlabJobs* defer,
+                 int split_rows = 0) {
   const int R = (int)ab[0].first.size(0), M = (int)ab[0].first.size(1), N = (int)ab[0].second.size(1);
   const int S = dgx_gemm_splits(M, N, R);
   int64_t chunk = cdiv(R, S);
@@ -439,7 +442,7 @@ void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab,
                             P(slab) + (int64_t)i * used * M * N, N, nullptr, nullptr, 0, d.stream),
           "gemm lds tn");
   }
-  reduce_slab(d, slab, n * used, M, N, M, out, defer);
+  reduce_slab(d, slab, n * used, M, N, split_rows > 0 ? split_rows : M, out, defer);
 }
 
 // fp32 -> (hi, lo) bf16 planes (dgx_split_bf16)
@@ -894,9 +897,29 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
   // precision class); exact dz + slot bytes with exact fp32 products
   const bool packed = (bf16 || o.split32) && o.packed;
   std::vector<Tensor> w32;   // fp32 mode: stacked weights of the blocks whose input gradient is formed
+  // fp32 mode, split class: blocks whose dW / dX run as 3-pass split bf16 GEMMs on
+  // the scatter's (hi, lo) dPQ planes, with [W1; W2]^T as [hi^T | lo^T] (one prep launch)
+  std::vector<bool> esplit(n, false);
+  std::vector<Tensor> wsplit(n);
+  Tensor wsplit_buf;
   if (!bf16) {
+    std::vector<PrepJob> jobs;
+    std::vector<int> at;
+    for (int l = 1; l < n; ++l) {
+      esplit[l] = o.split32 && o.split_edge && packed && !o.push && L[l].cin % 64 == 0 && L[l].co % 32 == 0 &&
+                  L[l].w.is_contiguous();
+      if (esplit[l]) {
+        jobs.push_back(PrepJob{L[l].w, L[l].co, L[l].cin, true, false, true});
+        at.push_back(l);
+      }
+    }
+    if (!jobs.empty()) {
+      auto pw = prep_weights(d, jobs);
+      wsplit_buf = pw.first;
+      for (size_t i = 0; i < at.size(); ++i) wsplit[at[i]] = pw.second[i].second;   // (cin, 4co)
+    }
     std::vector<bool> need(n);
-    for (int l = 0; l < n; ++l) need[l] = l > 0 || x_needs_grad;
+    for (int l = 0; l < n; ++l) need[l] = (l > 0 || x_needs_grad) && !esplit[l];
     w32 = stack_weights_f32(d, L, need);
   }
   Tensor pre_dz, pre_part;
@@ -946,8 +969,12 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
               "edge bwd dz");
       }
     }
-    // dPQ only feeds GEMMs: bf16 (what the GEMM would round it to) in bf16 mode
-    Tensor dPQ = at::empty({M, 2 * co}, bf16 ? d.bf16 : d.f32);
+    // dPQ only feeds GEMMs: bf16 (what the GEMM would round it to) in bf16 mode,
+    // its (hi, lo) bf16 planes in the fp32 mode's split class
+    const bool es = !bf16 && esplit[li];
+    const int out_mode = bf16 ? 1 : (es ? 3 : 0);
+    Tensor dPQs = es ? at::empty({3, M, 2 * co}, d.bf16) : Tensor();   // (hi, lo, hi)
+    Tensor dPQ = es ? dPQs[0] : at::empty({M, 2 * co}, bf16 ? d.bf16 : d.f32);
     Tensor dgamma, dbeta, c0, c1;
     const bool fold = st.group.empty() && o.fold_bwd;
     if (fold && o.push) {   // BN backward finalize in the push scatter's prologue (one launch)
@@ -959,7 +986,7 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
                                           P<int32_t>(edges[li]), P(dz), packed ? nullptr : P<uint8_t>(arg), P(sumP),
                                           B, N, k, co, P(partials), nblk, count, P(st.scale), P(st.mean),
                                           P(st.invstd), (int)st.eval, P(dgamma), P(dbeta), P(c0), P(c1),
-                                          dPQ.data_ptr(), (int)bf16, (int)packed, d.stream),
+                                          dPQ.data_ptr(), out_mode, (int)packed, d.stream),
             "edge bwd scatter");
     } else if (fold) {   // BN backward finalize in the scatter's prologue (one launch)
       dgamma = at::empty({co}, d.f32);
@@ -969,7 +996,7 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
       check(dgx_edge_bwd_scatter_fin_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(rowptr[li]), P<int32_t>(edges[li]), P(dz),
                                          packed ? nullptr : P<uint8_t>(arg), P(sumP), B, N, k, co, P(partials), nblk,
                                          count, P(st.scale), P(st.mean), P(st.invstd), (int)st.eval, P(dgamma), P(dbeta),
-                                         P(c0), P(c1), dPQ.data_ptr(), (int)bf16, (int)packed, d.stream),
+                                         P(c0), P(c1), dPQ.data_ptr(), out_mode, (int)packed, d.stream),
             "edge bwd scatter");
     } else {   // SyncBatchNorm: the all-reduce sits between the partials and the finalize
       auto r = backward_consts(d, partials, nblk, count, st);
@@ -981,17 +1008,17 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
         check(dgx_edge_bwd_scatter_push_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(s[0]), P<int32_t>(rowptr[li]),
                                             P<int32_t>(edges[li]), P(dz), packed ? nullptr : P<uint8_t>(arg), P(sumP),
                                             B, N, k, co, nullptr, 0, 0.0, P(st.scale), nullptr, nullptr, 0, nullptr,
-                                            nullptr, P(c0), P(c1), dPQ.data_ptr(), (int)bf16, (int)packed, d.stream),
+                                            nullptr, P(c0), P(c1), dPQ.data_ptr(), out_mode, (int)packed, d.stream),
               "edge bwd scatter");
       else if (packed)
         check(dgx_edge_bwd_scatter_packed_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(rowptr[li]), P<int32_t>(edges[li]),
                                               P(dz), P(sumP), B, N, k, co, P(st.scale), P(c0), P(c1), dPQ.data_ptr(),
-                                              (int)bf16, d.stream),
+                                              out_mode, d.stream),
               "edge bwd scatter");
       else
         check(dgx_edge_bwd_scatter_f32(P(PQ), (int)PQ.stride(0), P<int32_t>(rowptr[li]), P<int32_t>(edges[li]), P(dz),
                                        P<uint8_t>(arg), P(sumP), B, N, k, co, P(st.scale), P(c0), P(c1), dPQ.data_ptr(),
-                                       (int)bf16, d.stream),
+                                       out_mode, d.stream),
               "edge bwd scatter");
     }
     g.dgamma[li] = dgamma;
@@ -1035,6 +1062,22 @@ ChainGrads chain_backward_impl(const Dev& d, Tensor dxcat, bool dxcat_owned, con
         mm_xw(d, dPQ, split_weight(ly.w, cin, co), dx, false);
         g.dx = dx.view({B, N, C0}).permute({0, 2, 1});
       }
+    } else if (es) {
+      // 3-pass split bf16: dW = [hi; lo; hi]^T [X_hi; X_hi; X_lo] as ONE TN GEMM over
+      // 3 B*N rows (one set of split-K slabs, un-stacked to [W1 | W2] by the deferred
+      // reduce); dX += dPQ_hi (W_hi + W_lo) + dPQ_lo W_hi
+      const Tensor dPQl = dPQs[1];
+      Tensor xp = at::empty({3, M, cin}, d.bf16);
+      check(dgx_split_bf16(P(X), X.stride(0), M, cin, xp[0].data_ptr(), xp[2].data_ptr(), cin, d.stream),
+            "split bf16");
+      xp[1].copy_(xp[0]);
+      Tensor gw = at::empty({co, 2 * cin}, d.f32);
+      lds_atb(d, dPQs.view({3 * M, 2 * co}), xp.view({3 * M, cin}), gw, co, o.slab_cap_mb, slabs);
+      g.dw[li] = gw.view(ly.w.sizes());
+      Tensor dst = dxcat.narrow(1, prev, cin);
+      const Tensor& tn = wsplit[li];
+      lds_xwt(d, dPQ, tn, nullptr, false, &dst, &dst);
+      lds_xwt(d, dPQl, tn.narrow(1, 0, 2 * co), nullptr, false, &dst, &dst);
     } else {
       Tensor gw = at::empty({co, 2 * cin}, d.f32);   // dW = dPQ^T X, un-stacked to [W1 | W2] by the reduce
       mm32_atb(d, dPQ, X, gw, co, slabs);

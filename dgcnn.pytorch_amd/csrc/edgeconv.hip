@@ -890,7 +890,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
     const float* __restrict__ dz, const uint8_t* __restrict__ arg, const float* __restrict__ sumP, int B, int N,
     int k, int Co, int nparts, const float* __restrict__ scale, const float* __restrict__ c0,
-    const float* __restrict__ c1, void* __restrict__ dPQv, BnBwdFin fin) {
+    const float* __restrict__ c1, void* __restrict__ dPQv, BnBwdFin fin, int out_split) {
     static_assert(CS == 1 || CS == 2 || CS == 4 || CS == 8 || CS == 16, "slice width");
     constexpr int SW = (CS + 3) / 4;  // slot words per row
     float* __restrict__ dPQ = static_cast<float*>(dPQv);
@@ -1054,7 +1054,41 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
             dq[u] = fmaf(a[u], dn[u], fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
         }
-        if (OUT16 && vec) {
+        if (OUT16 && out_split) {
+            // the fp32 mode's split planes: hi = bf16(v) here, lo = bf16(v - hi) at
+            // + B*N*2Co (dgx_split_bf16's rounding), the 3-pass GEMMs' operands
+            const int64_t lo_off = (int64_t)B * N * 2 * Co;
+            float dph[CS], dpl[CS], dqh[CS], dql[CS];
+#pragma unroll
+            for (int u = 0; u < CS; ++u) {
+                dph[u] = (float)(__bf16)dp[u];
+                dpl[u] = dp[u] - dph[u];
+                dqh[u] = (float)(__bf16)dq[u];
+                dql[u] = dq[u] - dqh[u];
+            }
+            // out_split 2: hi again at + 2 B*N*2Co, so [hi; lo; hi] is one row-stacked
+            // operand of the 3-pass weight gradient (one TN GEMM over 3 B*N rows)
+            const int np = out_split == 2 ? 2 : 1;
+            if (vec) {
+                for (int pl = 0; pl < np; ++pl) {
+                    gst_bf16<CS>(dPQh + 2 * pl * lo_off + j * 2 * Co + o0, dph);
+                    gst_bf16<CS>(dPQh + 2 * pl * lo_off + j * 2 * Co + Co + o0, dqh);
+                }
+                gst_bf16<CS>(dPQh + lo_off + j * 2 * Co + o0, dpl);
+                gst_bf16<CS>(dPQh + lo_off + j * 2 * Co + Co + o0, dql);
+            } else {
+#pragma unroll
+                for (int u = 0; u < CS; ++u) {
+                    if (o0 + u >= Co) continue;
+                    for (int pl = 0; pl < np; ++pl) {
+                        dPQh[2 * pl * lo_off + j * 2 * Co + o0 + u] = (__bf16)dph[u];
+                        dPQh[2 * pl * lo_off + j * 2 * Co + Co + o0 + u] = (__bf16)dqh[u];
+                    }
+                    dPQh[lo_off + j * 2 * Co + o0 + u] = (__bf16)dpl[u];
+                    dPQh[lo_off + j * 2 * Co + Co + o0 + u] = (__bf16)dql[u];
+                }
+            }
+        } else if (OUT16 && vec) {
             gst_bf16<CS>(dPQh + j * 2 * Co + o0, dp);
             gst_bf16<CS>(dPQh + j * 2 * Co + Co + o0, dq);
         } else if (vec) {
@@ -1616,6 +1650,7 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
         return DGX_EINVAL;
     if (fin.partials && (fin.nrows < 1 || fin.count <= 0.0 || !fin.mean || !fin.invstd)) return DGX_EINVAL;
     if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
+    if (out_bf16 < 0 || out_bf16 > 3) return DGX_EINVAL;   // 2: split planes (hi, lo), 3: (hi, lo, hi)
     if (N > 65535) return DGX_EUNSUPPORTED;
     // slice channels: 9 (8 packed) bytes per (point, channel) within BW_LDS_BYTES
     // (16 measured slower: one workgroup per CU; 4 slower: per-edge work over fewer channels)
@@ -1634,7 +1669,7 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
     hipStream_t st = dgx_stream(stream);
 #define DGX_SCATTER_LAUNCH(CSV, O16, PK)                                                                      \
     hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin)
+                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 >= 2 ? out_bf16 - 1 : 0)
 #define DGX_SCATTER_CASE(CSV)                                       \
     case CSV:                                                      \
         if (packed) {                                              \
@@ -1690,6 +1725,7 @@ int launch_push(const float* PQ, int ldpq, const int32_t* idx, const int32_t* ro
         return DGX_EINVAL;
     if (fin.partials && (fin.nrows < 1 || fin.count <= 0.0 || !fin.mean || !fin.invstd)) return DGX_EINVAL;
     if (B < 1 || N < 1 || k < 1 || k > 64 || Co < 1 || ldpq < 2 * Co) return DGX_EINVAL;
+    if (out_bf16 < 0 || out_bf16 > 1) return out_bf16 <= 3 ? DGX_EUNSUPPORTED : DGX_EINVAL;
     if (N > 65535) return DGX_EUNSUPPORTED;
     int cs = 0, parts = 0;
     if (!push_geometry(B, N, Co, cs, parts)) return DGX_EUNSUPPORTED;

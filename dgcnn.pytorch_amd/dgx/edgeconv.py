@@ -59,6 +59,10 @@ FUSE_EDGE_DZ = os.environ.get("DGX_FUSE_EDGE_DZ", "1") == "1"
 # relative per product, fp32 sums) instead of the f32 MFMA, which runs at 1/16
 # of the bf16 rate (DGX_SPLIT32=0: the exact-product f32 MFMA GEMMs)
 SPLIT32 = os.environ.get("DGX_SPLIT32", "1") == "1"
+# ... and (with SPLIT32) the EdgeConv blocks' weight and input gradients too: the
+# backward scatter writes dPQ as its split planes and dW / dX run as the same
+# 3-pass GEMMs (DGX_SPLIT32_EDGE=0: those two on the f32 MFMA)
+SPLIT32_EDGE = os.environ.get("DGX_SPLIT32_EDGE", "1") == "1"
 # backward scatter in push form (dgx_edge_bwd_scatter_push_f32): each source's
 # selected dz is added to its target in exact 64-bit fixed point (order-free,
 # the exact sum rounded once), the in-edge loop reads only Q rows. Measured
@@ -135,7 +139,7 @@ def opts():
     ``opts`` word (csrc/dgx_torch.cpp ``decode``)."""
     cap = max(0, min(255, int(G.SLAB_CAP_MB)))
     return (int(SCATTER_PACKED) | 2 * int(FOLD_BN_BWD) | 4 * int(FUSE_KNN_IMAGE) | 8 * int(FUSE_EDGE_DZ)
-            | 16 * int(SPLIT32) | 32 * int(SCATTER_PUSH) | (cap << 8))
+            | 16 * int(SPLIT32) | 32 * int(SCATTER_PUSH) | 64 * int(SPLIT32 and SPLIT32_EDGE) | (cap << 8))
 
 
 PER_LAYER = 9   # saved per block: idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd

@@ -246,6 +246,10 @@ int dgx_graph_reverse(const int32_t* idx, int B, int N, int k,
  * DGCNN's blocks — in one launch (the graphs' workgroups share the chip). */
 int dgx_graph_reverse_multi(int n, const int32_t* const* idx, int B, int N, int k,
                             int32_t* const* rowptr, int32_t* const* edges, void* stream);
+/* dPQ output (out_bf16): 0 fp32, 1 bf16, 2 split bf16 planes — hi = bf16(v)
+ * at dPQ, lo = bf16(v - hi) at dPQ + B*N*2Co elements — or 3: (hi, lo, hi),
+ * hi again at dPQ + 2*B*N*2Co (the fp32 mode's 3-pass GEMM operands; the pull
+ * forms below, not the push form). */
 int dgx_edge_bwd_scatter_f32(const float* PQ, int ldpq, const int32_t* rowptr,
                              const int32_t* edges, const float* dz,
                              const uint8_t* arg, const float* sumP, int B, int N,

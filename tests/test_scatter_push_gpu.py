@@ -166,3 +166,33 @@ def test_push_nonfinite_channel(cuda):
     keep[5] = False
     keep[Co + 5] = False
     assert torch.equal(out[:, keep], ref[:, keep])
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("B,N,k,Co", [(8, 1024, 20, 64), (4, 777, 11, 20)])
+def test_pull_split_planes_output(cuda, packed, B, N, k, Co, mode):
+    """out_bf16 = 2 / 3 (the fp32 mode's split class): the pull scatter writes dPQ
+    as its (hi, lo) bf16 planes, lo at + B*N*2Co (mode 3: hi again at + 2 B*N*2Co)
+    — bitwise the fp32 output split by dgx_split_bf16's rounding (hi = bf16(v),
+    lo = bf16(v - hi)); the push form refuses both."""
+    S = _setup(cuda, B, N, k, Co, packed=packed, seed=5)
+    L, st = S["L"], S["st"]
+    ref = _pull(S, packed)
+    planes = torch.zeros(3, S["M"], 2 * Co, device=cuda, dtype=torch.bfloat16)
+    common = (B, N, k, Co, nat.f32(st.scale), nat.f32(S["c0"]), nat.f32(S["c1"]), nat.ptr(planes, nat.BF16), mode,
+              S["stream"])
+    if packed:
+        nat.check(L.dgx_edge_bwd_scatter_packed_f32(nat.f32(S["PQ"]), 2 * Co, nat.i32(S["rowptr"]), nat.i32(S["edges"]),
+                                                    nat.f32(S["dz"]), nat.f32(S["sumP"]), *common), "scatter split")
+    else:
+        nat.check(L.dgx_edge_bwd_scatter_f32(nat.f32(S["PQ"]), 2 * Co, nat.i32(S["rowptr"]), nat.i32(S["edges"]),
+                                             nat.f32(S["dz"]), nat.u8(S["arg"]), nat.f32(S["sumP"]), *common),
+                  "scatter split")
+    torch.cuda.synchronize()
+    hi = ref.to(torch.bfloat16)
+    lo = (ref - hi.float()).to(torch.bfloat16)
+    assert torch.equal(planes[0], hi) and torch.equal(planes[1], lo)
+    assert torch.equal(planes[2], hi if mode == 3 else torch.zeros_like(hi))
+    with pytest.raises(RuntimeError):
+        _push(S, packed, bf16=mode)
