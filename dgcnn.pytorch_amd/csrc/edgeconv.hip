@@ -885,7 +885,10 @@ __device__ __forceinline__ void scatter_consts(const BnBwdFin& fin, int b, int p
     }
 }
 
-template <int CS, bool OUT16, bool PACKED>
+// SPLIT (with OUT16): dPQ as split bf16 planes, out_split = planes after the
+// first (1: lo; 2: lo, hi) — a separate instantiation, so the bf16 and fp32
+// forms' code is untouched by the extra stores
+template <int CS, bool OUT16, bool PACKED, bool SPLIT = false>
 __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
     const float* __restrict__ dz, const uint8_t* __restrict__ arg, const float* __restrict__ sumP, int B, int N,
@@ -1054,7 +1057,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
             dq[u] = fmaf(a[u], dn[u], fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
         }
-        if (OUT16 && out_split) {
+        if constexpr (SPLIT) {
             // the fp32 mode's split planes: hi = bf16(v) here, lo = bf16(v - hi) at
             // + B*N*2Co (dgx_split_bf16's rounding), the 3-pass GEMMs' operands
             const int64_t lo_off = (int64_t)B * N * 2 * Co;
@@ -1068,7 +1071,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             }
             // out_split 2: hi again at + 2 B*N*2Co, so [hi; lo; hi] is one row-stacked
             // operand of the 3-pass weight gradient (one TN GEMM over 3 B*N rows)
-            const int np = out_split == 2 ? 2 : 1;
+            const int np = out_split >= 2 ? 2 : 1;
             if (vec) {
                 for (int pl = 0; pl < np; ++pl) {
                     gst_bf16<CS>(dPQh + 2 * pl * lo_off + j * 2 * Co + o0, dph);
@@ -1667,18 +1670,20 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
     const size_t lds = scatter_lds_bytes(N, cs, parts, packed);
     if (lds > (size_t)160 * 1024) return DGX_EUNSUPPORTED;
     hipStream_t st = dgx_stream(stream);
-#define DGX_SCATTER_LAUNCH(CSV, O16, PK)                                                                      \
-    hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 >= 2 ? out_bf16 - 1 : 0)
-#define DGX_SCATTER_CASE(CSV)                                       \
-    case CSV:                                                      \
-        if (packed) {                                              \
-            if (out_bf16) DGX_SCATTER_LAUNCH(CSV, true, true);     \
-            else DGX_SCATTER_LAUNCH(CSV, false, true);             \
-        } else {                                                   \
-            if (out_bf16) DGX_SCATTER_LAUNCH(CSV, true, false);    \
-            else DGX_SCATTER_LAUNCH(CSV, false, false);            \
-        }                                                          \
+#define DGX_SCATTER_LAUNCH(CSV, O16, PK, SP)                                                                      \
+    hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK, SP>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
+                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 - 1)
+#define DGX_SCATTER_CASE(CSV)                                                \
+    case CSV:                                                               \
+        if (packed) {                                                       \
+            if (out_bf16 >= 2) DGX_SCATTER_LAUNCH(CSV, true, true, true);   \
+            else if (out_bf16) DGX_SCATTER_LAUNCH(CSV, true, true, false);  \
+            else DGX_SCATTER_LAUNCH(CSV, false, true, false);               \
+        } else {                                                            \
+            if (out_bf16 >= 2) DGX_SCATTER_LAUNCH(CSV, true, false, true);  \
+            else if (out_bf16) DGX_SCATTER_LAUNCH(CSV, true, false, false); \
+            else DGX_SCATTER_LAUNCH(CSV, false, false, false);              \
+        }                                                                   \
         break;
     switch (cs) {
         DGX_SCATTER_CASE(8)
