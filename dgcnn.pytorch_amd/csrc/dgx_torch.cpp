@@ -427,8 +427,7 @@ void lds_atb(const Dev& d, const Tensor& a16, const Tensor& b16, Tensor& out, in
 
 // out = sum_i a_i^T b_i over the pairs (same shapes): every pair's split-K slabs in
 // one buffer, summed by one fixed-order reduce (the fp32 mode's 3-pass weight gradients)
-void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab, Tensor& out, SlabJobs* defer,
-                 int split_rows = 0) {
+void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab, Tensor& out, SlabJobs* defer) {
   const int R = (int)ab[0].first.size(0), M = (int)ab[0].first.size(1), N = (int)ab[0].second.size(1);
   const int S = dgx_gemm_splits(M, N, R);
   int64_t chunk = cdiv(R, S);
@@ -442,7 +441,7 @@ void lds_atb_sum(const Dev& d, const std::vector<std::pair<Tensor, Tensor>>& ab,
                             P(slab) + (int64_t)i * used * M * N, N, nullptr, nullptr, 0, d.stream),
           "gemm lds tn");
   }
-  reduce_slab(d, slab, n * used, M, N, split_rows > 0 ? split_rows : M, out, defer);
+  reduce_slab(d, slab, n * used, M, N, M, out, defer);
 }
 
 // fp32 -> (hi, lo) bf16 planes (dgx_split_bf16)
