@@ -25,9 +25,11 @@ Prints ONE JSON line on rank 0: whole-job clouds/s, plus
                 golden-pinned) for the same B-cloud batch on the host cores
                 this job is given, rank 0, N=1 only;
   edgeconv_fwd_bwd_ms  the 4-block EdgeConv chain alone (fwd+bwd), and per block;
-                       chain_fp32_mode: the same chain in the fp32 parity mode;
+                       chain_fp32_exact / chain_fp32_split: the same chain in the
+                       exact fp32 parity mode / the split-bf16 "fp32_split" mode;
+  fp32_exact_mode / fp32_split_mode  the step in those two precisions;
   torch_eager_gpu      the reference op sequence in stock PyTorch-ROCm eager on
-                       the same GPU, fp32 and under bf16 autocast (like for like).
+                       the same GPU, fp32 and under bf16 autocast.
 """
 import argparse
 import glob
@@ -67,9 +69,10 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-eager-baseline", action="store_true")
     p.add_argument("--cpu-reps", type=int, default=3)
-    p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
-                   help="GEMM operand precision (BASELINE cfg2 is bf16; fp32 is the parity mode)")
-    p.add_argument("--no-fp32-leg", action="store_true", help="skip the extra fp32-mode timing")
+    p.add_argument("--precision", choices=["bf16", "fp32", "fp32_split"], default="bf16",
+                   help="GEMM operand precision (BASELINE cfg2 is bf16; fp32 is the exact parity mode; "
+                        "fp32_split runs the fp32 GEMMs as 3-pass split bf16)")
+    p.add_argument("--no-fp32-leg", action="store_true", help="skip the extra fp32 / fp32_split timings")
     p.add_argument("--no-edgeconv-leg", action="store_true", help="skip the EdgeConv-only fwd+bwd timing")
     p.add_argument("--no-posemb-leg", action="store_true",
                    help="skip the PositionEmbedding edge-MLP timing (partseg geometry)")
@@ -83,6 +86,10 @@ def parse(argv=None):
     p.add_argument("--sgd", choices=["fused", "foreach", "dgx"], default="dgx",
                    help="SGD implementation: torch.optim.SGD fused / foreach, or dgx.optim.SGD (one HIP "
                         "launch); the same update")
+    p.add_argument("--rccl-world1", action="store_true",
+                   help="N=1: create a world-size-1 RCCL process group and take the N>1 step (flat-buffer "
+                        "all-reduce after the graph-replayed fwd+bwd; with --sync-bn the BN-statistics "
+                        "collectives too), so the multi-GPU code path runs on one GPU")
     p.add_argument("--sync-bn", action="store_true",
                    help="N>1: SyncBatchNorm (global-batch BN statistics, main_partseg_dist.py:189) instead of "
                         "per-replica BN (main_cls.py:62 DataParallel semantics)")
@@ -137,12 +144,13 @@ def reduce_elapsed(elapsed, world, dev):
     return float(t.item())
 
 
-def replicas_in_sync(model, world, dev):
-    """N > 1: every rank holds bitwise the same parameters after the timed steps
-    (fp64 checksum of all parameters, min == max over ranks). None at N = 1."""
+def replicas_in_sync(model, world, dev, distributed=None):
+    """N > 1 (or a world-size-1 process group): every rank holds bitwise the
+    same parameters after the timed steps (fp64 checksum of all parameters,
+    min == max over ranks, two collectives). None without a process group."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not (distributed if distributed is not None else world > 1):
         return None
     with torch.no_grad():
         c = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum().view(1)
@@ -512,11 +520,18 @@ def main():
         raise SystemExit(f"{world} RCCL ranks need {world} GPUs, this node has {ndev}")
     dev = torch.device("cuda", local % ndev)
     torch.cuda.set_device(dev)
+    pg1 = world == 1 and args.rccl_world1
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    elif pg1:   # RCCL accepts a one-rank communicator: the N>1 path on one GPU
+        from dgx import dist as dgx_dist
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=dev)
+        if args.sync_bn:
+            dgx_dist.sync_single_rank(True)   # torch would skip the sync at world 1; run the collective
     if args.scaling == "strong":
         if args.batch % world:
             raise SystemExit(f"--scaling strong: global batch {args.batch} does not split over {world} GPUs")
@@ -535,8 +550,9 @@ def main():
     # over RCCL the BN-statistics all-reduces (no host synchronisation, dgx.dist)
     # are captured inside that graph; over gloo (host collectives, not
     # capturable) or with --no-graph the step runs eagerly under DDP
-    flat_dp = world > 1 and not args.no_graph and (not args.sync_bn or args.backend == "nccl")
-    if world > 1:
+    distributed = world > 1 or pg1
+    flat_dp = distributed and not args.no_graph and (not args.sync_bn or args.backend == "nccl")
+    if distributed:
         if args.sync_bn:
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
         if flat_dp:
@@ -596,10 +612,11 @@ def main():
     launch = "eager"
     run = step
     elapsed_amp = None
-    if world == 1:
+    if world == 1 and not distributed:
         # the reference's own training configuration (main_partseg_dist.py:253): the
         # eager step under fp16 autocast with the engine's global mode at fp32 — the
-        # GEMMs follow autocast to the bf16 path (dgx.precision.effective), issued
+        # GEMMs follow autocast to the split-bf16 path (16 significant bits per
+        # operand, never narrower than fp16: dgx.precision.effective), issued
         # through the one-op C++ layer
         dgx_prec.set("fp32")
 
@@ -613,7 +630,7 @@ def main():
             amp_step()
         elapsed_amp = timed_region(amp_step, args.steps, world)
         dgx_prec.set(args.precision)
-    if world == 1 and not args.no_graph:
+    if world == 1 and not args.no_graph and not flat_dp:
         # one HIP graph per train step (fwd + bwd + SGD, the same kernels and
         # buffers as the eager step, captured once): replay issues the whole step
         # with one launch, independent of host speed. Grads are None when the
@@ -667,7 +684,7 @@ def main():
         "eager_launch_ms_per_step": round(elapsed_eager / args.steps * 1e3, 3),
         "autocast_eager_ms_per_step": (round(elapsed_amp / args.steps * 1e3, 3) if elapsed_amp is not None
                                        else None),
-        "replicas_in_sync": replicas_in_sync(model, world, dev),
+        "replicas_in_sync": replicas_in_sync(model, world, dev, distributed),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
@@ -678,8 +695,8 @@ def main():
         "config": {"workload": f"DGCNN(emb={args.emb},k={args.k}) train step fwd+bwd+SGD, {args.config}",
                    "model": "DGCNN", "global_batch": total, "batch_per_gpu": per_gpu, "points": args.points,
                    "seq_len": args.points, "k": args.k, "emb_dim": args.emb, "in_channels": args.in_dims,
-                   "parallelism": f"dp{world}" + ("+syncbn" if (args.sync_bn and world > 1) else ""),
-                   "backend": ("rccl" if args.backend == "nccl" else "gloo") if world > 1 else "none",
+                   "parallelism": f"dp{world}" + ("+syncbn" if (args.sync_bn and distributed) else ""),
+                   "backend": ("rccl" if args.backend == "nccl" or pg1 else "gloo") if distributed else "none",
                    "optimizer": {"dgx": "dgx.optim.SGD (one launch)", "fused": "torch.optim.SGD fused",
                                  "foreach": "torch.optim.SGD foreach"}[args.sgd]
                    + " lr 0.1 momentum 0.9 wd 1e-4"},
@@ -710,22 +727,29 @@ def main():
             "launches_timed": len(knn_ms), "knn_ms_by_layer": per_layer,
             "timed_region": "second K-step region, events around the kNN selection launches only "
                             "(ms_per_step %.3f)" % (elapsed_inst / args.steps * 1e3)}
-    if args.precision != "fp32" and not args.no_fp32_leg:
-        dgx_prec.set("fp32")  # same model, parity-mode GEMMs
+    if not args.no_fp32_leg:
+        # the same model in the exact fp32 parity mode and in the split-bf16
+        # "fp32_split" mode (NOT exact fp32: ~2^-16 per product), eager launch
         n32 = max(2, args.steps // 2)
-        for _ in range(3):  # warm-up (first fp32 GEMM calls pick their library kernels)
-            step()
-        el32 = reduce_elapsed(timed_region(step, n32, world), world, dev)
-        result["fp32_mode"] = {"ms_per_step": round(el32 / n32 * 1e3, 3),
-                               "value": round(total * n32 / el32, 2)}
+        for mode in ("fp32", "fp32_split"):
+            if mode == args.precision:
+                continue
+            dgx_prec.set(mode)
+            for _ in range(3):  # warm-up
+                step()
+            el32 = reduce_elapsed(timed_region(step, n32, world), world, dev)
+            result[{"fp32": "fp32_exact_mode", "fp32_split": "fp32_split_mode"}[mode]] = {
+                "ms_per_step": round(el32 / n32 * 1e3, 3), "value": round(total * n32 / el32, 2),
+                "launch": "eager"}
         dgx_prec.set(args.precision)
     if rank == 0 and world == 1:
         if not args.no_edgeconv_leg:
             legs = edgeconv_legs(model, x)
-            if args.precision != "fp32":   # the parity mode's chain beside stock fp32 eager
-                dgx_prec.set("fp32")
-                legs["chain_fp32_mode"] = edgeconv_legs(model, x, chain_only=True)["chain"]
-                dgx_prec.set(args.precision)
+            for mode in ("fp32", "fp32_split"):   # the fp32 modes' chains beside stock fp32 eager
+                dgx_prec.set(mode)
+                legs[f"chain_{'fp32_exact' if mode == 'fp32' else mode}"] = edgeconv_legs(
+                    model, x, chain_only=True)["chain"]
+            dgx_prec.set(args.precision)
             if not args.no_eager_baseline:
                 # the same 4-block chain in stock PyTorch-ROCm eager (the metric's EdgeConv ratio)
                 for name, dt in (("fp32", None), ("bf16_autocast", torch.bfloat16)):
@@ -734,11 +758,16 @@ def main():
                     except RuntimeError as e:
                         legs[f"torch_eager_{name}"] = {"error": str(e)[:200]}
                     torch.cuda.empty_cache()
-                ref = legs.get(f"torch_eager_{'fp32' if args.precision == 'fp32' else 'bf16_autocast'}")
+                ref = legs.get(f"torch_eager_{'bf16_autocast' if args.precision == 'bf16' else 'fp32'}")
                 if isinstance(ref, float):
                     legs["engine_speedup_vs_eager"] = round(ref / legs["chain"], 2)
-                if isinstance(legs.get("torch_eager_fp32"), float) and "chain_fp32_mode" in legs:
-                    legs["fp32_mode_speedup_vs_eager_fp32"] = round(legs["torch_eager_fp32"] / legs["chain_fp32_mode"], 2)
+                if isinstance(legs.get("torch_eager_fp32"), float):
+                    # exact fp32 vs torch fp32: the same arithmetic class
+                    legs["fp32_exact_speedup_vs_eager_fp32"] = round(legs["torch_eager_fp32"] /
+                                                                     legs["chain_fp32_exact"], 2)
+                    # split-bf16 products (~2^-16) vs torch's exact fp32: NOT the same precision
+                    legs["fp32_split_speedup_vs_eager_fp32"] = round(legs["torch_eager_fp32"] /
+                                                                     legs["chain_fp32_split"], 2)
             result["edgeconv_fwd_bwd_ms"] = legs
         if not args.no_posemb_leg:
             result["posemb_edge_mlp"] = posemb_edge_leg(dev)
@@ -746,7 +775,7 @@ def main():
             result["net_attention"] = attention_leg(dev)
         if not args.no_eager_baseline:
             eager = {}
-            ours32 = result["ms_per_step"] if args.precision == "fp32" else result.get("fp32_mode", {}).get(
+            ours32 = result["ms_per_step"] if args.precision == "fp32" else result.get("fp32_exact_mode", {}).get(
                 "ms_per_step")
             ours16 = result["ms_per_step"] if args.precision == "bf16" else None
             for name, dt, ours in (("fp32", None, ours32), ("bf16_autocast", torch.bfloat16, ours16)):
@@ -758,14 +787,14 @@ def main():
                 except RuntimeError as e:  # e.g. out of memory: report, don't hide
                     eager[name] = {"error": str(e)[:200]}
                 torch.cuda.empty_cache()
-            eager["note"] = ("engine_speedup compares like with like: fp32 eager vs the engine's fp32 mode, "
-                             "bf16-autocast eager vs the engine's bf16 mode")
+            eager["note"] = ("engine_speedup: fp32 eager vs the engine's exact fp32 mode (fp32_exact_mode, eager "
+                             "launch), bf16-autocast eager vs the engine's bf16 mode (the headline step)")
             result["torch_eager_gpu"] = eager
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args, per_gpu)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

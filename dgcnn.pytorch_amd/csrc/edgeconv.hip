@@ -1734,8 +1734,14 @@ int launch_push(const float* PQ, int ldpq, const int32_t* idx, const int32_t* ro
     if (N > 65535) return DGX_EUNSUPPORTED;
     int cs = 0, parts = 0;
     if (!push_geometry(B, N, Co, cs, parts)) return DGX_EUNSUPPORTED;
-    const char* probe = getenv("DGX_PUSH_SKIP");   // phase-timing probe of tools/push_lab.py (unset: 0)
+#ifdef DGX_PUSH_LAB
+    // phase-timing probe of tools/push_lab.py: only in a lab build (-DDGX_PUSH_LAB),
+    // never in the product library, where a stray variable would drop phases
+    const char* probe = getenv("DGX_PUSH_SKIP");
     const uint32_t skip = probe ? (uint32_t)strtoul(probe, nullptr, 0) : 0u;
+#else
+    const uint32_t skip = 0u;
+#endif
     const int slices = (Co + cs - 1) / cs;
     const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
     const size_t lds = push_lds_bytes(N, cs, parts);

@@ -177,14 +177,46 @@ __device__ __forceinline__ int knn_cand(int row) { return ((row & 3) << 2) | (ro
 // ------------------------------------------------------------ operand image --
 // The MFMA A operand of every 16-candidate tile, in lane order: for tile s of
 // cloud b, lane l = 16*kk + i holds channels 4t + kk (t = 0..NSTEP-1) of
-// candidate 16 s + knn_cand(i), NSTEP consecutive floats:
-//     img[((b*ntile + s)*64 + l)*NSTEP + t]
-// so one wave fetches a whole tile as NSTEP*256 contiguous bytes with 16-byte
-// loads straight from L2, without staging through LDS or synchronising with
-// other waves. Zero rows pad N to a multiple of 16 and zero channels pad C to
+// candidate 16 s + knn_cand(i), NSTEP floats per lane. Within a tile the
+// floats are CHUNK-MAJOR when NSTEP % 4 == 0: 16-byte chunk u = t / 4 of lane l
+// at chunk index u*64 + l,
+//     img[(b*ntile + s)*64*NSTEP + ((t/4)*64 + l)*4 + t%4]
+// so each 16-byte wave load (one chunk u of all 64 lanes) is 1 KiB of
+// contiguous bytes = 8 whole 128-B lines. (Lane-major NSTEP floats per lane —
+// the layout before r09 — made every such load touch 32 lines for 16 B each
+// of the lane's 64 / 128 B: 4x the L1 tag traffic of the bytes used, which
+// capped the operand stream.) NSTEP = 1 / 3: lane-major, l*NSTEP + t. A wave
+// fetches a whole tile straight from L2, without staging through LDS or
+// synchronising with other waves. Zero rows pad N to a multiple of 16 and zero channels pad C to
 // 4*NSTEP (they add exact zeros to the fmaf chain). xximg holds |x_j|^2 in the
 // same row order: xximg[(b*ntile + s)*16 + i]. A query's own operand (the B
 // side) is read from the same image.
+// offset of float t of image lane l inside its tile
+template <int NSTEP>
+__device__ __forceinline__ int img_off(int l, int t) {
+    if constexpr (NSTEP % 4 == 0) return ((t >> 2) * 64 + l) * 4 + (t & 3);
+    else return l * NSTEP + t;
+}
+
+// lane l's floats t0 .. t0+V-1 of a tile (t0 % 4 == 0 in the chunk-major form)
+template <int NSTEP, int V>
+__device__ __forceinline__ void ld_lane(const float* __restrict__ tile, int l, int t0, float (&r)[V]) {
+    if constexpr (NSTEP % 4 == 0) {
+        static_assert(V % 4 == 0, "whole chunks");
+#pragma unroll
+        for (int u = 0; u < V / 4; ++u) {
+            const float4 q = *reinterpret_cast<const float4*>(tile + (((t0 >> 2) + u) * 64 + l) * 4);
+            r[4 * u] = q.x;
+            r[4 * u + 1] = q.y;
+            r[4 * u + 2] = q.z;
+            r[4 * u + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < V; ++u) r[u] = tile[l * NSTEP + t0 + u];
+    }
+}
+
 constexpr int KI_TILES = 1;  // tiles per image-builder block
 // One pass over x per layer: the operand image, the |x|^2 image and xx itself
 // (|x_i|^2 in the reference's rounding order, sqnorm_sum on the staged row).
@@ -212,10 +244,17 @@ __global__ __launch_bounds__(256) void knn_image_kernel(const float* __restrict_
     __syncthreads();
     const int ntl = min(KI_TILES, ntile - s0);
     float* __restrict__ dst = img + ((int64_t)b * ntile + s0) * 64 * NSTEP;
-    for (int e = t; e < ntl * 64 * NSTEP; e += 256) {
+    for (int e = t; e < ntl * 64 * NSTEP; e += 256) {   // coalesced stores in image order
         const int tl = e / (64 * NSTEP);
         const int r = e - tl * 64 * NSTEP;
-        const int l = r / NSTEP, st = r - l * NSTEP;
+        int l, st;
+        if constexpr (NSTEP % 4 == 0) {   // chunk-major: r = ((st/4)*64 + l)*4 + st%4
+            l = (r >> 2) & 63;
+            st = ((r >> 8) << 2) | (r & 3);
+        } else {
+            l = r / NSTEP;
+            st = r - l * NSTEP;
+        }
         dst[e] = rows[tl * 16 + knn_cand(l & 15)][4 * st + (l >> 4)];
     }
     __syncthreads();
@@ -289,7 +328,7 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
     if (tid == 0) cnt[0] = 0;
     for (int w = tid; w < nw; w += KQ_THREADS) bits[w] = 0u;
     float bq[NSTEP];
-    ld_vec<NSTEP>(ib + ((int64_t)(qf >> 4) * 64 + g * 16 + knn_row(qf & 15)) * NSTEP, bq);
+    ld_lane<NSTEP, NSTEP>(ib + (int64_t)(qf >> 4) * 64 * NSTEP, g * 16 + knn_row(qf & 15), 0, bq);
 #pragma unroll
     for (int t = 0; t < NSTEP; ++t) bq[t] *= 2.0f;
     const float xxq = xxb[qf];
@@ -298,7 +337,7 @@ __device__ void knn_fix_row(float* fixa, const float* __restrict__ ib, const flo
     auto stream = [&](auto&& act) {
         for (int s = wave; s < ntile; s += KQ_WAVES) {
             float a[NSTEP];
-            ld_vec<NSTEP>(ib + ((int64_t)s * 64 + lane) * NSTEP, a);
+            ld_lane<NSTEP, NSTEP>(ib + (int64_t)s * 64 * NSTEP, lane, 0, a);
             const float4 xc = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -477,7 +516,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
         // partial sum of the fmaf chain doubles exactly, so the MFMA returns
         // fl(2 * dot) (dgcnn.py:7) directly.
         const int qs = min(S.q, N - 1);
-        ld_vec<NSTEP>(ib + ((int64_t)(qs >> 4) * 64 + g * 16 + knn_row(qs & 15)) * NSTEP, S.bq);
+        ld_lane<NSTEP, NSTEP>(ib + (int64_t)(qs >> 4) * 64 * NSTEP, g * 16 + knn_row(qs & 15), 0, S.bq);
 #pragma unroll
         for (int t = 0; t < NSTEP; ++t) S.bq[t] *= 2.0f;
         S.xxq = S.q < N ? xx[(int64_t)b * N + S.q] : 0.f;
@@ -682,7 +721,7 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     // SPT is a compile-time constant at every call.
     auto load = [&](int slot, int u, int sl) {
         const int s = min(h + KQ_HALVES * (u / SPT), ntile - 1);
-        ld_vec<SW>(ib + ((int64_t)s * 64 + lane) * NSTEP + sl * SW, a[slot]);
+        ld_lane<NSTEP, SW>(ib + (int64_t)s * 64 * NSTEP, lane, sl * SW, a[slot]);
         if (sl == 0) xq[slot] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
     };
 #pragma unroll
@@ -891,9 +930,9 @@ __global__ __launch_bounds__(256) void apply_image_kernel(const float* __restric
             *reinterpret_cast<h4*>(out16 + i * ldo + 4 * q) = h4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
         }
         // image lane 16 u + ii of tile st holds channels 4 t + u: here t = q
-        float* __restrict__ ib = img + (((int64_t)b * ntile + st) * 64 + ii) * NSTEP + q;
+        float* __restrict__ ib = img + ((int64_t)b * ntile + st) * 64 * NSTEP;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) ib[16 * u * NSTEP] = v[u];
+        for (int u = 0; u < 4; ++u) ib[img_off<NSTEP>(16 * u + ii, q)] = v[u];
     }
     float sq[4];
 #pragma unroll

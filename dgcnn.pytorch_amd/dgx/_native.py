@@ -111,6 +111,7 @@ _SIGS = {
     "dgx_gemm_h1bwd_bf16": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp,
                             _vp, _i32, _vp],
     "dgx_hog_1x1_f32": [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    "dgx_hog_1x1_sem_f32": [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp],
     "dgx_attn_fwd": [_i32] + [_vp, _i64, _i64, _i64, _i64] * 3 + [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32,
                                                                    _i32, _i32, _f32, _f32, ctypes.c_uint64, _vp,
                                                                    _vp],

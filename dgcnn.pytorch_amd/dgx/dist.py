@@ -19,6 +19,19 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+# Smallest process-group size at which a SyncBatchNorm synchronises. torch's
+# SyncBatchNorm skips the collective on a single rank (need_sync = world > 1);
+# the engine does the same by default. ``sync_single_rank(True)`` lowers it to
+# 1 so the collective path (fp64 sums all-reduced over RCCL, inside a HIP graph
+# or from the C++ op) runs on a one-GPU box with a world-size-1 RCCL group
+# (tests/test_rccl_gpu.py, bench.py --rccl-world1).
+_MIN_WORLD = 2
+
+
+def sync_single_rank(on):
+    global _MIN_WORLD
+    _MIN_WORLD = 1 if on else 2
+
 
 def sync_group(bn):
     """(True, group) when ``bn`` is a SyncBatchNorm that must synchronise now
@@ -28,7 +41,7 @@ def sync_group(bn):
     if not (dist.is_available() and dist.is_initialized()):
         return False, None
     group = bn.process_group if bn.process_group is not None else dist.group.WORLD
-    if dist.get_world_size(group) < 2:
+    if dist.get_world_size(group) < _MIN_WORLD:
         return False, None
     return True, group
 

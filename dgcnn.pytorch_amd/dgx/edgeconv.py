@@ -54,12 +54,14 @@ FUSE_KNN_IMAGE = os.environ.get("DGX_FUSE_KNN_IMAGE", "1") == "1"
 # in its epilogue and writes that block's packed dz + BN partials
 # (dgx_gemm_edge_dz_bf16) instead of dY (DGX_FUSE_EDGE_DZ=0: dY + a dz pass)
 FUSE_EDGE_DZ = os.environ.get("DGX_FUSE_EDGE_DZ", "1") == "1"
-# fp32 parity mode: conv5's GEMMs as 3 passes of the bf16 MFMA on split operands
+# split-bf16 fp32 GEMMs (precision "fp32_split", or fp16 autocast: see
+# dgx.precision): conv5's GEMMs as 3 passes of the bf16 MFMA on split operands
 # (x = hi + lo, 16 significant bits each: hi.W_hi + hi.W_lo + lo.W_hi, ~2^-16
 # relative per product, fp32 sums) instead of the f32 MFMA, which runs at 1/16
-# of the bf16 rate (DGX_SPLIT32=0: the exact-product f32 MFMA GEMMs)
-SPLIT32 = os.environ.get("DGX_SPLIT32", "1") == "1"
-# ... and (with SPLIT32) the EdgeConv blocks' weight and input gradients too: the
+# of the bf16 rate. DGX_SPLIT32=1 forces it in the plain "fp32" mode too (A/B);
+# the "fp32" default keeps exact products and exact dz.
+SPLIT32 = os.environ.get("DGX_SPLIT32", "0") == "1"
+# ... and (when split) the EdgeConv blocks' weight and input gradients too: the
 # backward scatter writes dPQ as its split planes and dW / dX run as the same
 # 3-pass GEMMs (DGX_SPLIT32_EDGE=0: those two on the f32 MFMA)
 SPLIT32_EDGE = os.environ.get("DGX_SPLIT32_EDGE", "1") == "1"
@@ -134,12 +136,17 @@ def edge_select(PQ, idx, B, N, k, co, gamma, stream):
     return ysel, arg, sumP, partials, prow
 
 
-def opts():
+def opts(split=None):
     """The A/B switches above and gemm.SLAB_CAP_MB as the C++ schedule's
-    ``opts`` word (csrc/dgx_torch.cpp ``decode``)."""
+    ``opts`` word (csrc/dgx_torch.cpp ``decode``). ``split``: whether the op's
+    fp32 GEMMs run as split bf16 — decided at the op's entry
+    (``precision.split()``, which sees autocast); None = the global mode's."""
+    if split is None:
+        split = prec.get() == "fp32_split"
+    split = bool(split or SPLIT32)
     cap = max(0, min(255, int(G.SLAB_CAP_MB)))
     return (int(SCATTER_PACKED) | 2 * int(FOLD_BN_BWD) | 4 * int(FUSE_KNN_IMAGE) | 8 * int(FUSE_EDGE_DZ)
-            | 16 * int(SPLIT32) | 32 * int(SCATTER_PUSH) | 64 * int(SPLIT32 and SPLIT32_EDGE) | (cap << 8))
+            | 16 * int(split) | 32 * int(SCATTER_PUSH) | 64 * int(split and SPLIT32_EDGE) | (cap << 8))
 
 
 PER_LAYER = 9   # saved per block: idx, PQ, ysel, arg, sumP, scale, shift, mean, invstd
@@ -182,7 +189,7 @@ class _EdgeConvStack(torch.autograd.Function):
 
     @staticmethod
     @prec.no_autocast
-    def forward(ctx, x, k, layers, prep, idx0, bf16, need_grad, *params):
+    def forward(ctx, x, k, layers, prep, idx0, bf16, op_opts, need_grad, *params):
         from . import host
         host.load()
         x = x.float()
@@ -190,12 +197,12 @@ class _EdgeConvStack(torch.autograd.Function):
         bn_t, bn_f, bn_i, groups, slopes = _bn_lists(layers)
         xcat, xcat16, saved, prep_out = torch.ops.dgx_host.chain_forward(
             x, k, weights, gammas, betas, bn_t, bn_f, bn_i, groups, slopes, bool(bf16), bool(need_grad), prep, idx0,
-            opts())
+            op_opts)
         dbg = debug_capture()
         if dbg is not None:
             capture_decisions(dbg, saved, xcat, xcat16)
         ctx.meta = (k, tuple(x.shape), bool(bf16), [int(not bn_.mode(ly.bn)[0]) for ly in layers], groups, slopes,
-                    len(saved))
+                    len(saved), op_opts)
         # x itself is saved: its version counter guards the point-major rows (a view of x)
         ctx.save_for_backward(x, xcat, xcat16, prep_out, *saved, *weights)
         ctx.mark_non_differentiable(xcat16)
@@ -205,18 +212,18 @@ class _EdgeConvStack(torch.autograd.Function):
     @staticmethod
     @prec.no_autocast
     def backward(ctx, dxcat, _unused):
-        k, shape, bf16, evals, groups, slopes, ns = ctx.meta
+        k, shape, bf16, evals, groups, slopes, ns, op_opts = ctx.meta
         n = len(slopes)
         if dxcat is None:
-            return (None,) * (7 + 3 * n)
+            return (None,) * (8 + 3 * n)
         t = ctx.saved_tensors
         xcat, xcat16, prep = t[1], t[2], t[3]
         saved, weights = list(t[4:4 + ns]), list(t[4 + ns:])
         dx, dws, dgs, dbs = torch.ops.dgx_host.chain_backward(
             dxcat, xcat, xcat16, saved, weights, prep if prep.numel() else None, list(shape), k, evals, groups, slopes,
-            bf16, ctx.needs_input_grad[0], opts())
+            bf16, ctx.needs_input_grad[0], op_opts)
         grads = [g for trip in zip(dws, dgs, dbs) for g in trip]
-        return (dx if dx.numel() else None, None, None, None, None, None, None, *grads)
+        return (dx if dx.numel() else None, None, None, None, None, None, None, None, *grads)
 
 
 def _layers_and_params(convs, weights=None):
@@ -250,7 +257,8 @@ def edgeconv_stack_pair(x, k, convs, training=None, preps=None, weights=None):
     if x.dtype != torch.float32:
         x = x.float()
     layers, params = _layers_and_params(convs, weights)
-    bf16 = prec.effective() == "bf16"
+    eff = prec.effective()
+    bf16 = eff == "bf16"
     # whether this forward will be differentiated (inside Function.forward grad
     # mode is always off, so it is decided here)
     need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
@@ -260,7 +268,7 @@ def edgeconv_stack_pair(x, k, convs, training=None, preps=None, weights=None):
         idx0 = knn_raw(x.detach(), k, order=reduction_order(x), out_dtype=torch.int32)
     if isinstance(preps, (list, tuple)):
         preps = None
-    return _EdgeConvStack.apply(x, k, layers, preps, idx0, bf16, need_grad, *params)
+    return _EdgeConvStack.apply(x, k, layers, preps, idx0, bf16, opts(eff == "fp32_split"), need_grad, *params)
 
 
 def edgeconv_stack(x, k, convs, training=None):

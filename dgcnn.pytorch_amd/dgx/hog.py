@@ -1,7 +1,16 @@
 """compute_hog_1x1's work after the kNN call, on the device (SURVEY §8 row f1;
-reference models/model_partseg.py:28-92): one C-ABI call (dgx_hog_1x1_f32,
+reference models/model_partseg.py:28-92): one C-ABI call (dgx_hog_1x1_sem_f32,
 csrc/hog.hip) replaces the D2H copy, np.linalg.svd over B*N neighbourhoods,
-the H2D copy and the histogram votes. No host round trip; host tensors take the CPU path."""
+the H2D copy and the histogram votes. No host round trip; host tensors take
+the CPU path.
+
+The reference runs its stages on different devices depending on the caller
+(model_partseg.py:32 the mean on x's device; :42-47 the votes on the GPU
+unless use_cpu without LOCAL_RANK), and torch's CPU and GPU kernels round
+differently (scalar division, acos / atan, reduction order). ``mean_device``
+/ ``votes_device`` say which of torch's kernels the engine reproduces for each
+stage; the default is the reference's path for a GPU cloud in Net.forward
+(both on the GPU)."""
 import torch
 
 from . import _native as N
@@ -13,10 +22,17 @@ from . import cpu
 HOG_K_MIN, HOG_K_MAX = 5, 64
 
 
-def hog_1x1(x, idx):
+def semantics(mean_device, votes_device):
+    """The C ABI's `sem` mask (DGX_HOG_MEAN_DEVICE | DGX_HOG_VOTES_DEVICE)."""
+    return int(bool(mean_device)) | 2 * int(bool(votes_device))
+
+
+def hog_1x1(x, idx, mean_device=True, votes_device=True):
     """x (B, 3, N) fp32 on the device, idx (B, N, k) int64 local kNN ids ->
-    (B, N, 18) histograms, as the reference computes them from the same idx.
-    Host tensors take the reference's own host path (dgx.cpu.hog_1x1)."""
+    (B, N, 18) histograms, as the reference computes them from the same idx
+    with its mean on the GPU (``mean_device``) or the host, and its votes on
+    the GPU (``votes_device``) or the host. Host tensors take the reference's
+    own host path (dgx.cpu.hog_1x1)."""
     if torch.compiler.is_compiling():   # traced as one dgx::hog_1x1 op (dgx.library)
         from . import library  # noqa: F401
         return torch.ops.dgx.hog_1x1(x, idx)
@@ -36,6 +52,6 @@ def hog_1x1(x, idx):
     idx = idx.contiguous()
     axis = torch.empty((P, 4), device=x.device, dtype=torch.float32)
     out = torch.empty((B, P, 18), device=x.device, dtype=torch.float32)
-    N.check(N.lib().dgx_hog_1x1_f32(N.f32(x), N.ptr(idx, N.I64), B, P, k, N.f32(axis), N.f32(out),
-                                    N.stream_of(x)), "hog_1x1")
+    N.check(N.lib().dgx_hog_1x1_sem_f32(N.f32(x), N.ptr(idx, N.I64), B, P, k, semantics(mean_device, votes_device),
+                                        N.f32(axis), N.f32(out), N.stream_of(x)), "hog_1x1")
     return out

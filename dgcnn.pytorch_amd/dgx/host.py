@@ -7,10 +7,11 @@ instead of one Python dispatch each.
 It is the same schedule the engine's autograd Functions (dgx.edgeconv,
 dgx.pointconv) and torch.library ops (dgx.library) call, one C++
 implementation for every configuration the reference's scripts run:
-precision bf16 or fp32 (and fp16/bf16 autocast -> bf16 GEMMs, dgx.precision
-.effective), BatchNorm in training or eval mode, momentum or cumulative
-running statistics, plain BatchNorm2d or SyncBatchNorm (main_partseg_dist.py:
-189: the statistics all-reduce is issued from C++ over the module's process
+precision bf16, fp32 or fp32_split (bf16 autocast -> bf16 GEMMs, fp16
+autocast -> split-bf16 fp32 GEMMs, dgx.precision.effective), BatchNorm in
+training or eval mode, momentum or cumulative running statistics, plain
+BatchNorm2d or SyncBatchNorm (main_partseg_dist.py:189: the statistics
+all-reduce is issued from C++ over the module's process
 group), any (B, C, N, k). The Function path is taken only while tests capture
 routing decisions (dgx.edgeconv.set_debug_capture), while torch.compile traces
 (dgx.library ops), or with ``DGX_HOST_EXT=0`` (A/B runs).
@@ -64,7 +65,8 @@ def applies(model, x):
 def dgcnn_forward(model, x):
     """DGCNN.forward through torch.ops.dgx_host.dgcnn."""
     load()
-    bf16 = prec.effective() == "bf16"
+    eff = prec.effective()
+    bf16 = eff == "bf16"
     if x.dtype != torch.float32:
         x = x.float()
     params, bufs, bn_f, bn_i, groups = [], [], [], [], []
@@ -81,4 +83,5 @@ def dgcnn_forward(model, x):
     if getattr(ops._tls, "cache", None) is not None:
         # inside a kNN-sharing scope (Net.forward): block 1's kNN is the scope's entry
         idx0 = ops.knn_raw(x.detach(), model.k, order=ops.reduction_order(x), out_dtype=torch.int32)
-    return torch.ops.dgx_host.dgcnn(x, params, bufs, bn_f, bn_i, groups, idx0, model.k, bf16, E.opts())
+    return torch.ops.dgx_host.dgcnn(x, params, bufs, bn_f, bn_i, groups, idx0, model.k, bf16,
+                                    E.opts(eff == "fp32_split"))

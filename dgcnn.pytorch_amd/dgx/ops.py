@@ -262,6 +262,18 @@ def graph_feature(x, k=20, knn_only=False, disp_only=False, idx=None, mode="cat"
     x = _as_f32(x)
     if idx is None:
         idx = knn_raw(x.detach(), k, out_dtype=torch.int32)
-    elif idx.dtype != torch.int32:
-        idx = idx.to(torch.int32)
+    else:
+        # caller-given ids (an engine extension): every kernel of the forward and
+        # the reverse-graph backward assumes 0 <= id < N, so check once (one host
+        # sync, only on this path); the reference's indexing raises likewise
+        B, _, N = x.shape
+        if idx.dim() != 3 or idx.shape[0] != B or idx.shape[1] != N:
+            raise RuntimeError(f"get_graph_feature: idx of shape {tuple(idx.shape)} does not match x "
+                               f"{tuple(x.shape)} (expected (B, N, k))")
+        if idx.numel():
+            lo, hi = torch.aminmax(idx.detach())
+            if int(lo) < 0 or int(hi) >= N:
+                raise IndexError(f"get_graph_feature: neighbour ids must lie in [0, {N}), got [{int(lo)}, {int(hi)}]")
+        if idx.dtype != torch.int32:
+            idx = idx.to(torch.int32)
     return _GraphFeature.apply(x, idx.contiguous(), mode)

@@ -8,7 +8,11 @@ run on ~22 workgroups, ~28 us per step at cfg2; here the whole list is one
 grid-stride launch (48 tensors per launch). The training scripts of the
 reference construct torch.optim.SGD / Adam (main_partseg.py); this class is a
 drop-in for the SGD case. Capturable in a HIP graph once the momentum buffers
-exist (after the first step)."""
+exist (after the first step), with FIXED hyper-parameters: lr, momentum,
+dampening and weight decay are kernel arguments, so a scheduler's change to
+them reaches eager steps but not an already captured graph (recapture after
+changing them). Parameters of one group may live on several devices: each
+launch takes one device's tensors."""
 import ctypes
 
 import torch
@@ -43,7 +47,7 @@ class SGD(torch.optim.Optimizer):
             mom = float(group["momentum"])
             # (first step of a buffer, parameter) lists: torch sets buf = d_p on a
             # parameter's first step, momentum * buf + (1 - dampening) * d_p after
-            jobs = {True: [], False: []}
+            jobs = {}   # (first step, device) -> [(param, buffer)]: one launch per device
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -62,8 +66,8 @@ class SGD(torch.optim.Optimizer):
                         buf = torch.empty_like(p, memory_format=torch.contiguous_format)
                         st["momentum_buffer"] = buf
                         first = True
-                jobs[first].append((p, buf))
-            for first, lst in jobs.items():
+                jobs.setdefault((first, p.device), []).append((p, buf))
+            for (first, dev), lst in jobs.items():
                 for c in range(0, len(lst), _MAX):
                     chunk = lst[c:c + _MAX]
                     n = len(chunk)
@@ -71,7 +75,6 @@ class SGD(torch.optim.Optimizer):
                     gs = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p, _ in chunk])
                     ms = (ctypes.c_void_p * n)(*[(b.data_ptr() if b is not None else 0) for _, b in chunk])
                     ns = (ctypes.c_int64 * n)(*[p.numel() for p, _ in chunk])
-                    dev = chunk[0][0].device
                     with torch.cuda.device(dev):
                         nat.check(lib.dgx_sgd_step_f32(n, ps, gs, ms if mom != 0.0 else None, ns, float(group["lr"]),
                                                        float(group["weight_decay"]), mom, float(group["dampening"]),

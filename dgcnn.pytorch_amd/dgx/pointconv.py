@@ -27,27 +27,25 @@ class _PointConvBNLReLU(torch.autograd.Function):
 
     @staticmethod
     @prec.no_autocast
-    def forward(ctx, X, X16, B, N, bn, slope, nt, tn, bf16, weight, gamma, beta):
+    def forward(ctx, X, X16, B, N, bn, slope, nt, tn, bf16, op_opts, weight, gamma, beta):
         from . import host
         host.load()
         t, f, i, g = bn_.op_args(bn)
         if X16 is None:
             X16 = torch.empty(0, dtype=torch.bfloat16, device=X.device)
-        from .edgeconv import opts
         out, saved = torch.ops.dgx_host.pointconv_forward(X.float(), X16, B, N, weight, gamma, beta, t,
-                                                          f + [float(slope)], i, g, bool(bf16), nt, tn, opts())
-        ctx.meta = (B, N, float(slope), not bn_.mode(bn)[0], g, bool(bf16))
+                                                          f + [float(slope)], i, g, bool(bf16), nt, tn, op_opts)
+        ctx.meta = (B, N, float(slope), not bn_.mode(bn)[0], g, bool(bf16), op_opts)
         ctx.save_for_backward(weight, *saved)
         return out
 
     @staticmethod
     @prec.no_autocast
     def backward(ctx, dout):
-        B, N, slope, ev, g, bf16 = ctx.meta
+        B, N, slope, ev, g, bf16, op_opts = ctx.meta
         weight, *saved = ctx.saved_tensors
-        from .edgeconv import opts
-        dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, saved, weight, B, N, slope, ev, g, bf16, opts())
-        return dX, None, None, None, None, None, None, None, None, dW, dg, db
+        dX, dW, dg, db = torch.ops.dgx_host.pointconv_backward(dout, saved, weight, B, N, slope, ev, g, bf16, op_opts)
+        return dX, None, None, None, None, None, None, None, None, None, dW, dg, db
 
 
 def pointconv_bn_lrelu(X, B, N, seq, training=None, X16=None, wprep=None):
@@ -66,6 +64,7 @@ def pointconv_bn_lrelu(X, B, N, seq, training=None, X16=None, wprep=None):
     if conv.bias is not None or bn.weight is None:
         raise NotImplementedError("dgx pointconv expects Conv(bias=False) + affine BatchNorm")
     nt, tn = wprep if wprep is not None else (None, None)
-    bf16 = prec.effective() == "bf16"
-    return _PointConvBNLReLU.apply(X, X16, B, N, bn, act.negative_slope, nt, tn, bf16, conv.weight, bn.weight,
-                                   bn.bias)
+    from .edgeconv import opts
+    eff = prec.effective()
+    return _PointConvBNLReLU.apply(X, X16, B, N, bn, act.negative_slope, nt, tn, eff == "bf16",
+                                   opts(eff == "fp32_split"), conv.weight, bn.weight, bn.bias)

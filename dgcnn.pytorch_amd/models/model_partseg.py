@@ -47,11 +47,30 @@ def _hist_device(use_cpu):
     return torch.device("cuda")
 
 
+def _votes_on_gpu(use_cpu):
+    # model_partseg.py:42-47: v and s (and every op after the SVD) go to the GPU
+    # when LOCAL_RANK is set or use_cpu is False
+    return "LOCAL_RANK" in os.environ or not use_cpu
+
+
 def compute_hog_1x1(x, k, use_cpu=False):
     """(B,3,N) -> (B,N,18) per-point 9-bin x 2-angle histogram of the dominant
     direction of each point's k-neighbourhood (reference model_partseg.py:15-92).
-    Engine kNN (:26), then one device call for :28-92."""
-    hist = hog_1x1(x, knn(x, k))
+    Engine kNN (:26), then one device call for :28-92 with the arithmetic of
+    the devices the reference runs each stage on: the mean on x's device, the
+    votes on the GPU unless ``use_cpu`` (without LOCAL_RANK). A host cloud
+    whose votes the reference moves to the GPU runs the same device call (mean
+    with the host's arithmetic); a host cloud with host votes takes the host
+    path."""
+    idx = knn(x, k)
+    votes_gpu = _votes_on_gpu(use_cpu)
+    if x.is_cuda:
+        hist = hog_1x1(x, idx, mean_device=True, votes_device=votes_gpu)
+    elif votes_gpu and torch.cuda.is_available():
+        dev = _hist_device(False)
+        hist = hog_1x1(x.to(dev), idx.to(dev), mean_device=False, votes_device=True)
+    else:
+        hist = hog_1x1(x, idx)
     return hist.to(_hist_device(use_cpu))
 
 

@@ -548,6 +548,19 @@ int dgx_edge_mlp_scatter_f32(const void* g, int g_bf16, const float* PQ, int ldp
  * 2 angles) L2-normalised histograms. 5 <= k <= 64 (DGX_EUNSUPPORTED else). */
 int dgx_hog_1x1_f32(const float* x, const int64_t* idx, int B, int N, int k, float* axis, float* out,
                     void* stream);
+/* The same, with the arithmetic of the device each reference stage runs on for
+ * the caller's configuration (`sem`, a mask): DGX_HOG_MEAN_DEVICE — x is a GPU
+ * tensor, so the neighbourhood mean (model_partseg.py:32) is torch's GPU mean
+ * (reduce-kernel order, times float(outputs)/numel); DGX_HOG_VOTES_DEVICE — v and
+ * s were moved to the GPU (model_partseg.py:42-47: LOCAL_RANK set or use_cpu
+ * False), so the angle / vote / bin-sum / normalize ops (:58-90) are torch's
+ * GPU kernels (ocml acosf / atanf, scalar division as a reciprocal multiply,
+ * reduce-kernel sum and norm order). sem 0 = dgx_hog_1x1_f32 (every stage as
+ * torch's CPU kernels, the reference's use_cpu run on a host cloud). */
+#define DGX_HOG_MEAN_DEVICE 1
+#define DGX_HOG_VOTES_DEVICE 2
+int dgx_hog_1x1_sem_f32(const float* x, const int64_t* idx, int B, int N, int k, int sem, float* axis, float* out,
+                        void* stream);
 
 /* ---- f2: attention in Net (nn.Transformer / nn.MultiheadAttention), replaces the
  * scaled_dot_product_attention call inside torch.nn.functional.

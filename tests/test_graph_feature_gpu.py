@@ -67,3 +67,22 @@ def test_graph_feature_backward_deterministic(cuda, mode):
     # both are fp32 sums in different orders over the hubs' ~540 in-edges each
     # (the atomic order varies per run; 1.04e-6 seen once): a few fp32 ulps
     assert rel_err(grads[0].cpu(), dx.cpu()) < 4e-6
+
+
+def test_graph_feature_rejects_out_of_range_ids(cuda):
+    """Caller-given neighbour ids outside [0, N) (or of the wrong shape) raise
+    before any kernel reads them, as the reference's indexing raises; nothing
+    is launched with them (the forward gather and the reverse-graph backward
+    both assume 0 <= id < N)."""
+    from dgx import ops
+    B, C, N, k = 2, 5, 64, 8
+    x = torch.randn(B, C, N, device=cuda)
+    idx = torch.randint(0, N, (B, N, k), device=cuda)
+    for bad in (N, -1):
+        b = idx.clone()
+        b[1, 7, 3] = bad
+        with pytest.raises(IndexError, match=r"\[0, 64\)"):
+            ops.graph_feature(x, k=k, idx=b)
+    with pytest.raises(RuntimeError, match="does not match"):
+        ops.graph_feature(x, k=k, idx=idx[:, :32])
+    assert ops.graph_feature(x, k=k, idx=idx).shape == (B, 2 * C, N, k)

@@ -1,10 +1,10 @@
 """The C++ op layer (libdgx_torch.so, dgx.host): DGCNN.forward as one custom
 op with a C++ autograd node serves every configuration the reference's
-scripts run (bf16 / fp32, fp16 autocast, train / eval / no_grad, momentum or
-cumulative running statistics, SyncBatchNorm) and equals the autograd
+scripts run (bf16 / fp32 / fp32_split, fp16 and bf16 autocast, train / eval /
+no_grad, momentum or cumulative running statistics, SyncBatchNorm) and equals the autograd
 Functions over the same C++ schedule bit for bit — output, every gradient,
 every BatchNorm buffer — at the BASELINE geometries (cfg2 B=32 N=1024 k=20
-emb 1024; the cfg5 9-channel S3DIS block; a shard with the input gradient),
+emb 1024; cfg3 B=32 N=2048 k=40; the cfg5 9-channel S3DIS block; a shard with the input gradient),
 and inside Net's kNN-sharing scope. Reference: models/dgcnn.py:84-103 and its
 autograd; main_partseg_dist.py:189, 253."""
 import copy
@@ -80,6 +80,9 @@ def _counting(monkeypatch):
 CASES = {   # B, N, k, emb, C, precision
     "cfg2": (32, 1024, 20, 1024, 3, "bf16"),
     "cfg2_fp32": (32, 1024, 20, 1024, 3, "fp32"),
+    "cfg2_fp32_split": (32, 1024, 20, 1024, 3, "fp32_split"),
+    "cfg3": (32, 2048, 40, 1024, 3, "bf16"),
+    "cfg3_fp32": (32, 2048, 40, 1024, 3, "fp32"),
     "cfg5_s3dis": (2, 4096, 20, 1024, 9, "bf16"),
     "shard_xgrad": (4, 1024, 20, 256, 3, "bf16"),
     "shard_xgrad_fp32": (4, 1024, 20, 256, 3, "fp32"),
@@ -158,31 +161,35 @@ def test_host_op_serves_every_configuration(cuda, monkeypatch):
 
 
 def test_host_op_follows_autocast(cuda, monkeypatch):
-    """Under torch.autocast(float16 | bfloat16) (main_partseg_dist.py:253) the
-    op's GEMMs take the bf16 path (SURVEY §8(b) "GEMMs follow autocast dtype"):
-    the step equals the same step in precision "bf16" without autocast, bit
-    for bit, through the C++ op; without autocast the fp32 mode stays fp32."""
+    """Under torch.autocast (main_partseg_dist.py:253) the op's GEMMs follow
+    the autocast dtype without computing narrower than it (SURVEY §8(b),
+    dgx.precision.effective): bf16 autocast = precision "bf16", fp16 autocast
+    = precision "fp32_split" (16 significant bits per operand, finer than
+    fp16's 11), each bit for bit through the C++ op; without autocast the
+    fp32 mode keeps exact products (differs from both)."""
     from dgx import precision as prec
     base = _model(256, 20, seed=4)
     x = _cloud(cuda, 4, 1024, seed=9)
     gout = torch.randn((4, 256, 1024), device=cuda)
     calls = _counting(monkeypatch)
     res = {}
-    for name in ("fp16_autocast", "bf16_autocast", "bf16_mode", "fp32_mode"):
+    for name in ("fp16_autocast", "bf16_autocast", "bf16_mode", "fp32_split_mode", "fp32_mode"):
         m = copy.deepcopy(base).to(cuda).train()
         if name.endswith("autocast"):
             dt = torch.float16 if name.startswith("fp16") else torch.bfloat16
             with torch.autocast("cuda", dtype=dt):
                 res[name] = _step(m, x, gout)
-        elif name == "bf16_mode":
-            with prec.mode("bf16"):
+        elif name != "fp32_mode":
+            with prec.mode(name[:-5]):
                 res[name] = _step(m, x, gout)
         else:
             res[name] = _step(m, x, gout)
-    assert len(calls) == 4
-    _assert_same(res["fp16_autocast"], res["bf16_mode"])
+    assert len(calls) == 5
+    _assert_same(res["fp16_autocast"], res["fp32_split_mode"])
     _assert_same(res["bf16_autocast"], res["bf16_mode"])
     assert not torch.equal(res["fp32_mode"][0], res["bf16_mode"][0])
+    # the forward EdgeConv GEMMs stay exact in the split mode; conv5's are split
+    assert not torch.equal(res["fp32_mode"][0], res["fp32_split_mode"][0])
 
 
 def test_host_op_in_net_knn_scope(cuda, monkeypatch):

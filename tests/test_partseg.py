@@ -50,50 +50,79 @@ def _hog_agreement(got, ref):
     return exact.mean(), close.mean()
 
 
-# f1 tolerance: the device HOG follows the reference op by op (torch CPU sum
-# order, fp64 SVD as numpy's dgesdd, fp32 angle ops), so points agree bit-for-bit
-# except where an fp32 acos/atan differs from the host libm's in the last ulp
-# right at an integer degree (.int() then moves the vote to the next cell).
-# Such a point differs by up to a whole vote; every other point is exact.
+# f1 tolerances. The reference runs the HOG votes with torch's kernels on the
+# device it moved v and s to (model_partseg.py:42-47).
+# * GPU votes (Net.forward's call on a GPU cloud, and any call without
+#   use_cpu): the engine reproduces torch's HIP kernels op for op (ocml acosf /
+#   atanf, reciprocal-multiply scalar division, the reduce kernel's sum and
+#   norm order, GPU mean): EVERY point within HOG_TOL of the oracle running the
+#   reference's op sequence on the GPU — every bin equal, no allowance.
+# * host votes (use_cpu=True, the golden fixture): torch's CPU acos / atan are
+#   glibc's scalar acosf (on the strided zenith input) and SLEEF's vectorised
+#   atanf_u10 on chunks whose boundaries follow the host's thread split; the
+#   engine rounds the fp64 function instead, so a point whose angle lands
+#   within an ulp of an integer degree can take the neighbouring cell (one
+#   whole vote): up to HOST_ALLOW of the points may differ.
 HOG_TOL = 1e-6
+HOST_ALLOW = 0.995
 
 
 @pytest.mark.gpu
 def test_hog_golden(golden, cuda):
-    from models.model_partseg import compute_hog_1x1
+    """The engine with host semantics (every stage as torch's CPU kernels)
+    against the reference's own CPU run (tests/golden/partseg_small.npz)."""
+    from dgx.hog import hog_1x1
+    from models.dgcnn import knn
     g = golden("partseg_small.npz")
     x = torch.from_numpy(g["x"]).to(cuda)
-    hog = compute_hog_1x1(x, 10)
+    hog = hog_1x1(x, knn(x, 10), mean_device=False, votes_device=False)
     assert hog.is_cuda
     hog = hog.cpu().numpy()
     ref = g["hog"]
     assert hog.shape == ref.shape
     exact, close = _hog_agreement(hog, ref)
-    assert exact >= 0.995 and close >= 0.995, (exact, close)
+    assert exact >= HOST_ALLOW and close >= HOST_ALLOW, (exact, close)
+
+
+def _oracle_semantics(x, idx, mean_dev, votes_dev, cuda):
+    """The oracle's op sequence on the devices of each stage."""
+    from oracle.hog import hog_1x1 as ref_hog
+    xs = x.to(cuda) if mean_dev else x.cpu()
+    return ref_hog(xs, idx.to(xs.device), cuda if votes_dev else "cpu").cpu().numpy()
+
+
+SEMANTICS = [(True, True), (False, True), (True, False), (False, False)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,N,k", [(4, 1024, 20), (2, 2048, 40), (3, 500, 5), (2, 256, 64)])
-def test_hog_device_vs_oracle(cuda, B, N, k):
-    """dgx_hog_1x1_f32 vs the oracle restatement on the same engine kNN ids."""
-    from oracle.hog import hog_1x1 as ref_hog
+@pytest.mark.parametrize("B,N,k", [(4, 1024, 20), (2, 2048, 40), (3, 500, 5), (2, 256, 64), (2, 777, 23)])
+@pytest.mark.parametrize("sem", SEMANTICS, ids=lambda s: f"mean{'GPU' if s[0] else 'CPU'}_votes{'GPU' if s[1] else 'CPU'}")
+def test_hog_device_vs_oracle(cuda, B, N, k, sem):
+    """dgx_hog_1x1_sem_f32 vs the oracle running the reference's op sequence
+    with each stage on the device the semantics name (mean: x's device; votes:
+    where v and s were moved), on the same engine kNN ids. GPU votes: every
+    point within 1e-6 (every bin equal); host votes: HOST_ALLOW."""
     from dgx.hog import hog_1x1
     from models.dgcnn import knn
     gen = torch.Generator().manual_seed(B * 1000 + k)
     x = torch.rand((B, 3, N), generator=gen) * 2 - 1
     xd = x.to(cuda)
     idx = knn(xd, k)
-    got = hog_1x1(xd, idx).cpu().numpy()
-    ref = ref_hog(x, idx.cpu()).numpy()
+    got = hog_1x1(xd, idx, mean_device=sem[0], votes_device=sem[1]).cpu().numpy()
+    ref = _oracle_semantics(x, idx, sem[0], sem[1], cuda)
     exact, close = _hog_agreement(got, ref)
-    assert exact >= 0.995 and close >= 0.995, (exact, close)
+    print(f"sem {sem}: exact {exact:.6f} close {close:.6f}")
+    if sem[1]:
+        assert close == 1.0, (exact, close)
+    else:
+        assert exact >= HOST_ALLOW and close >= HOST_ALLOW, (exact, close)
 
 
 @pytest.mark.gpu
 def test_hog_degenerate_neighbourhoods(cuda):
     """Repeated points: zero-spread neighbourhoods (SVD of a zero matrix) and
-    collinear ones take dgesdd's exact-zero branches."""
-    from oracle.hog import hog_1x1 as ref_hog
+    collinear ones take dgesdd's exact-zero branches (GPU semantics, the
+    reference's default path)."""
     from dgx.hog import hog_1x1
     from models.dgcnn import knn
     N, k = 256, 10
@@ -104,10 +133,10 @@ def test_hog_degenerate_neighbourhoods(cuda):
     xd = x.to(cuda)
     idx = knn(xd, k)
     got = hog_1x1(xd, idx).cpu().numpy()
-    ref = ref_hog(x, idx.cpu()).numpy()
-    assert np.isfinite(got).all() == np.isfinite(ref).all()
+    ref = _oracle_semantics(x, idx, True, True, cuda)
+    assert (np.isfinite(got) == np.isfinite(ref)).all()
     exact, close = _hog_agreement(np.nan_to_num(got), np.nan_to_num(ref))
-    assert close >= 0.99, (exact, close)
+    assert close == 1.0, (exact, close)
 
 
 @pytest.mark.gpu
@@ -126,16 +155,27 @@ def test_hog_k_range(cuda):
 
 @pytest.mark.gpu
 def test_hog_use_cpu_places_output(cuda, monkeypatch):
+    """compute_hog_1x1's devices follow the reference's (model_partseg.py:32,
+    42-47, 66-73): a GPU cloud with use_cpu=True takes the GPU mean and host
+    votes and returns a host histogram; a host cloud without use_cpu takes
+    the host mean and GPU votes and returns a GPU histogram — each equal to
+    the oracle run with the same placement."""
+    from models.dgcnn import knn
     from models.model_partseg import compute_hog_1x1
     monkeypatch.delenv("LOCAL_RANK", raising=False)
     x = torch.rand((2, 3, 128), device=cuda)
+    idx = knn(x, 8)
     h = compute_hog_1x1(x, 8, use_cpu=True)
     assert h.device.type == "cpu"
-    # a host cloud without use_cpu: the histogram lands on the GPU, as the
-    # reference's does (model_partseg.py:66-73), computed on the host path
+    exact, close = _hog_agreement(h.numpy(), _oracle_semantics(x, idx, True, False, cuda))
+    assert exact >= HOST_ALLOW and close >= HOST_ALLOW, (exact, close)
     hc = compute_hog_1x1(x.cpu(), 8)
     assert hc.device.type == "cuda"
-    torch.testing.assert_close(hc.cpu(), h, rtol=0, atol=1e-5)
+    exact, close = _hog_agreement(hc.cpu().numpy(), _oracle_semantics(x, idx, False, True, cuda))
+    assert close == 1.0, (exact, close)
+    # LOCAL_RANK moves the votes to the GPU even with use_cpu (model_partseg.py:42-44)
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    assert compute_hog_1x1(x, 8, use_cpu=False).is_cuda
 
 
 @pytest.mark.gpu
@@ -210,17 +250,18 @@ def test_hog_restatement_matches_reference_cpu(golden):
 # constant) are measured against the model-wide gradient scale.
 AMP_TOL = 2e-2
 RATIO = 1.5
-# fp32 mode with conv5's GEMMs as 3-pass split bf16 (dgx.edgeconv.SPLIT32, the
-# default): ~2^-16 relative per product instead of fp32's 2^-24, which the
+# precision "fp32_split" (opt-in): conv5's GEMMs and blocks 2-4's weight / input
+# gradients as 3-pass split bf16 (~2^-16 relative per product instead of fp32's
+# 2^-24) and dz packed with its slot (18 significant bits), which the
 # ill-conditioned gradients above amplify to ~2x stock fp32's error on a few
 # EdgeConv weights (r06u: conv4.0.weight 9.6e-3 vs stock 4.8e-3; 6.0e-3 vs
-# 6.0e-3 worst with exact products). Exact products are held to RATIO.
+# 6.0e-3 worst with exact products). The exact default is held to RATIO.
 RATIO_SPLIT = 3.0
-# amp: the engine's GEMMs run bf16 under autocast (unit roundoff 2^-9), the
-# stock layers fp16 (2^-11), so the engine's share of the error is up to ~4x
-# the stock step's: held to 4 x RATIO (r06v: worst pos_mlp.0.transform.weight
-# 1.55 vs stock 0.36 of an fp64 gradient that fp16 itself misses by 36 %)
-RATIO_AMP = 6.0
+# amp: under fp16 autocast the engine's DGCNN GEMMs run split-bf16 (16
+# significant bits per operand, dgx.precision.effective) and its edge MLP exact
+# fp32, never narrower than the stock layers' fp16 (11 bits): the engine's
+# share of the error stays below the stock fp16 step's
+RATIO_AMP = 2.0
 
 
 @pytest.mark.gpu
@@ -230,12 +271,14 @@ def test_net_cfg4_routed(cuda, mode, monkeypatch):
     stock fp64 modules (oracle.partseg.net_routed) on the same neighbours:
     every EdgeConv kNN / max slot / sign, the edge stage's kNN / conv2 slot /
     sign, PositionEmbedding's max over points and the HOG are validated, then
-    the output and EVERY parameter gradient are compared. fp32: exact fp32
-    GEMM products (DGX_SPLIT32=0); fp32_split: the fp32 mode's default conv5
-    GEMMs; amp: fp16 autocast as main_partseg_dist.py:253 trains."""
+    the output and EVERY parameter gradient are compared. fp32: the default
+    precision (exact fp32 GEMM products); fp32_split: the opt-in split-bf16
+    GEMMs; amp: fp16 autocast as main_partseg_dist.py:253 trains (the
+    engine's GEMMs then run split-bf16)."""
     import dgx.edgeconv as E
+    from dgx import precision as prec
     amp = mode == "amp"
-    monkeypatch.setattr(E, "SPLIT32", mode == "fp32_split")
+    monkeypatch.setattr(prec, "_mode", "fp32_split" if mode == "fp32_split" else "fp32")
     ratio = {"fp32": RATIO, "fp32_split": RATIO_SPLIT, "amp": RATIO_AMP}[mode]
     import oracle
     from conftest import edge_mlp_decisions, validate_dgcnn_decisions
@@ -273,20 +316,21 @@ def test_net_cfg4_routed(cuda, mode, monkeypatch):
         E.set_debug_capture(None)
         for h in hooks:
             h.remove()
-    # decisions: DGCNN blocks, edge stage, max over points, HOG. Under autocast
-    # the engine's DGCNN GEMMs run in bf16 (dgx.precision.effective): its
-    # decisions are checked against the bf16-operand recomputation
-    dec = validate_dgcnn_decisions(cap, src, k, init_emb, bf16=amp)
+    # decisions: DGCNN blocks, edge stage, max over points, HOG (the forward
+    # EdgeConv GEMMs are exact fp32 in every mode but bf16, so the decisions
+    # are checked against the fp32 recomputation)
+    dec = validate_dgcnn_decisions(cap, src, k, init_emb, bf16=False)
     dgcnn_dec = [(i.long(), a, z) for (i, a, z) in (cap[("fwd", l)] for l in range(4))]
     zpos1, arg2, zpos2, edec = edge_mlp_decisions(cap, B, N, k, net.pos_mlp[0].conv2[0].weight)
     eidx = cap["emlp"]["idx"].view(B, N, k).long()
     np.testing.assert_array_equal(eidx.cpu().numpy(), oracle.knn(src.cpu(), k))
     argmax_n = seen["t3"].max(dim=-1)[1]
-    # the HOG the engine fed grads_emb (model_partseg.py:179) vs the oracle's restatement
+    # the HOG the engine fed grads_emb (model_partseg.py:179) vs the reference's op
+    # sequence on the GPU (Net.forward's path for a GPU cloud): every point
     net_hog = compute_hog_1x1(src, k)
-    hog = ref_hog(src.cpu(), torch.from_numpy(oracle.knn(src.cpu(), k)))
+    hog = ref_hog(src, torch.from_numpy(oracle.knn(src.cpu(), k)).to(cuda), cuda).cpu()
     exact, close = _hog_agreement(net_hog.cpu().numpy(), hog.numpy())
-    assert exact >= 0.995 and close >= 0.995, (exact, close)
+    assert close == 1.0, (exact, close)
     runs = {}
     for name, m, dt in (("f64", net64, torch.float64), ("stock", net32, torch.float32)):
         with torch.autocast("cuda", dtype=torch.float16, enabled=amp and name == "stock"):
@@ -297,10 +341,10 @@ def test_net_cfg4_routed(cuda, mode, monkeypatch):
     t3 = runs["f64"][2]
     gap_n = float((t3.max(dim=-1)[0] - torch.gather(t3, 2, argmax_n.unsqueeze(-1)).squeeze(-1)).max()
                   / t3.abs().max())
-    # under autocast the engine's DGCNN and edge-MLP GEMMs run in bf16 (8 significant
-    # bits, unit roundoff 2^-9): a near-tied max over points may pick a point whose
-    # fp64 value trails the maximum by a few bf16 ulps of the scale
-    assert gap_n <= (1e-2 if amp else 1e-5), ("max over points", gap_n)
+    # under autocast the stock conv3 before the max over points runs fp16 (unit
+    # roundoff 2^-11): a near-tied max may pick a point whose fp64 value trails
+    # the maximum by a few fp16 ulps of the scale
+    assert gap_n <= (2e-3 if amp else 1e-5), ("max over points", gap_n)
     ref = runs["f64"][0].cpu()
     e_out = rel_err(out.detach().float().cpu(), ref)
     assert e_out < (AMP_TOL if amp else TOL), ("out", e_out)
