@@ -1038,7 +1038,11 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
         for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
             int32_t ids[BW_EB];
 #pragma unroll
+#ifndef SCATTER_PROBE_NOIDS
             for (int v = 0; v < BW_EB; ++v) ids[v] = u0 + v < end ? edges[u0 + v] : 0;
+#else   // timing probe (A/B builds only; wrong results): ids without the global loads
+            for (int v = 0; v < BW_EB; ++v) ids[v] = ((ibase + ((n * 7 + (u0 + v) * 13) & (N - 1))) << 6) | ((u0 + v) & 15);
+#endif
 #pragma unroll
             for (int v = 0; v < BW_EB; ++v)
                 if (u0 + v < end) edge(ids[v]);

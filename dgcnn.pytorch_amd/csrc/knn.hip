@@ -727,12 +727,24 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
 #pragma unroll
     for (int r = 0; r < RING; ++r) load(r, r, r % SPT);
     float4 xc = xq[0];
+    float probe_sum = 0.f;
+    (void)probe_sum;
 #pragma unroll 1
     for (int u = 0; u < nunits; u += UB) {
 #pragma unroll
         for (int ub = 0; ub < UB; ++ub) {
             const int slot = ub % RING, sl = ub % SPT;
-            const bool live = UB == SPT || u + ub < nunits;   // wave-uniform
+            // every unit of a trip runs: a unit past the end (only in the last
+            // trip, when nunits % UB != 0) re-reads the half's last tile and its
+            // candidates fail the j < N test (its tile index is past the cloud, so
+            // the TAIL form of consider runs). A wave-uniform `live` test here made
+            // the trip's control flow conditional and the compiler drained every
+            // operand load in flight (s_waitcnt vmcnt(0)) at each trip's start.
+#ifndef KNN_LIVE_TEST
+            constexpr bool live = true;
+#else
+            const bool live = UB == SPT || u + ub < nunits;   // (A/B builds only)
+#endif
             if (live) {
                 if (sl == 0) {
                     each([&](Grp& S, int) { S.acc = f32x4{0.f, 0.f, 0.f, 0.f}; });
@@ -745,7 +757,9 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                         S.acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[slot][t], S.bq[sl * SW + t], S.acc, 0, 0, 0);
                     });
             }
+#ifndef KNN_PROBE_NOLOAD
             load(slot, u + ub + RING, (ub + RING) % SPT);
+#endif
             if (live && sl == SPT - 1) {
                 // lane holds rows 4g..4g+3 = candidates g, g+4, g+8, g+12 of the tile
                 const int st = h + KQ_HALVES * ((u + ub) / SPT);
@@ -760,12 +774,22 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
                 };
                 // (the two-group kernel keeps the check everywhere: its split
                 // code measured 2 us slower, r04u)
+#ifdef KNN_PROBE_NOSEL   // timing probe (A/B builds only): the Gram stream without the selection
+                each([&](Grp& S, int) { probe_sum += S.acc[0] + S.acc[1] + S.acc[2] + S.acc[3] + xc.x; });
+                (void)j0;
+#else
                 if (QG == 2 || (st + 1) * 16 > N) cons4(std::true_type{});
                 else cons4(std::false_type{});
                 if (__any(cmax() > KQ_QCAP - 4)) flush();
+#endif
             }
         }
     }
+#if defined(KNN_PROBE_NOSEL) || defined(KNN_PROBE_NOLOAD)
+    // timing probes (A/B builds only; wrong results): skip the merge and fix-up
+    if (probe_sum == 1234.5f && vals) vals[tid] = probe_sum;
+    return;
+#endif
     flush();
 
     // Merge the wave's 4 lists of each query (lanes ql, ql+16, ql+32, ql+48)

