@@ -893,7 +893,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
     const float* __restrict__ dz, const uint8_t* __restrict__ arg, const float* __restrict__ sumP, int B, int N,
     int k, int Co, int nparts, const float* __restrict__ scale, const float* __restrict__ c0,
-    const float* __restrict__ c1, void* __restrict__ dPQv, BnBwdFin fin, int out_split) {
+    const float* __restrict__ c1, void* __restrict__ dPQv, BnBwdFin fin, int out_split, int idcap) {
     static_assert(CS == 1 || CS == 2 || CS == 4 || CS == 8 || CS == 16, "slice width");
     constexpr int SW = (CS + 3) / 4;  // slot words per row
     float* __restrict__ dPQ = static_cast<float*>(dPQv);
@@ -917,6 +917,24 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const bool full = o0 + CS <= Co;
     if (t < BW_BUCKETS) bucket[t] = 0;
     constexpr bool SWZ = CS == 8;
+    // the part's in-edge ids (a contiguous CSR range) staged in LDS as 16-bit
+    // (local source << 6 | slot) words when they fit idcap (block-uniform;
+    // idcap > 0 only for N <= 1024): the in-edge loop then waits on LDS instead
+    // of dependent global id batches
+    const int32_t ibase = (int32_t)base;
+    uint16_t* lid = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(bucket + BW_BUCKETS) + BW_FIN_LDS);
+    int32_t e_lo = 0;
+    bool idl = false;
+    if (idcap > 0 && np > 0) {
+        e_lo = rowptr[base + n_beg];
+        const int32_t e_cnt = rowptr[base + n_end] - e_lo;
+        idl = e_cnt <= idcap;
+        if (idl)
+            for (int e = t; e < e_cnt; e += EC_THREADS) {
+                const int32_t w = edges[e_lo + e];
+                lid[e] = (uint16_t)((((w >> 6) - ibase) << 6) | (w & 63));
+            }
+    }
     stage_slice<CS, EC_THREADS, SWZ>(qs, PQ + base * ldpq + Co, ldpq, N, o0, Co, (ldpq % 4) == 0 && (Co % 4) == 0);
     stage_slice<CS, EC_THREADS, SWZ>(ds, dz + base * Co, Co, N, o0, Co, (Co % 4) == 0);
     // row n of a swizzled slice: halves at 4 * (h ^ bit 2 of n)
@@ -986,7 +1004,6 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     scatter_consts<CS>(fin, b, part, o0, Co, scale, c0, c1, bucket + BW_BUCKETS, a, k0, k1);
     const bool vec = full && (CS % 4) == 0 && (Co % 4) == 0 && (ldpq % 4) == 0;
     const float kf = (float)k;
-    const int32_t ibase = (int32_t)base;
     __syncthreads();
     // boustrophedon deal of the degree-sorted points: pass 2p takes ranks
     // t, pass 2p+1 ranks from the far end, so a thread's in-degree total (and a
@@ -1011,9 +1028,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
         float sq[CS], sd[CS];
 #pragma unroll
         for (int u = 0; u < CS; ++u) { sq[u] = 0.f; sd[u] = 0.f; }
-        auto edge = [&](int32_t e) {
-            const int il = (e >> 6) - ibase;
-            const uint32_t slot = (uint32_t)(e & 63);
+        auto edge = [&](int il, uint32_t slot) {
             float q[CS];
             lds_row(qs, il, q);
 #pragma unroll
@@ -1033,19 +1048,26 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
                 for (int u = 0; u < CS; ++u) sd[u] += ((w[u >> 2] >> (8 * (u & 3))) & 0xffu) == slot ? d[u] : 0.f;
             }
         };
-        // in-edge ids EB at a time, all loads issued before the first is used
-        // (prefetching the next batch as well measured slower)
-        for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
-            int32_t ids[BW_EB];
+        if (idl) {   // ids from LDS, EB at a time
+            for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
+                uint32_t ids[BW_EB];
 #pragma unroll
-#ifndef SCATTER_PROBE_NOIDS
-            for (int v = 0; v < BW_EB; ++v) ids[v] = u0 + v < end ? edges[u0 + v] : 0;
-#else   // timing probe (A/B builds only; wrong results): ids without the global loads
-            for (int v = 0; v < BW_EB; ++v) ids[v] = ((ibase + ((n * 7 + (u0 + v) * 13) & (N - 1))) << 6) | ((u0 + v) & 15);
-#endif
+                for (int v = 0; v < BW_EB; ++v) ids[v] = u0 + v < end ? lid[u0 + v - e_lo] : 0u;
 #pragma unroll
-            for (int v = 0; v < BW_EB; ++v)
-                if (u0 + v < end) edge(ids[v]);
+                for (int v = 0; v < BW_EB; ++v)
+                    if (u0 + v < end) edge((int)(ids[v] >> 6), ids[v] & 63u);
+            }
+        } else {
+            // in-edge ids EB at a time, all loads issued before the first is used
+            // (prefetching the next batch as well measured slower)
+            for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
+                int32_t ids[BW_EB];
+#pragma unroll
+                for (int v = 0; v < BW_EB; ++v) ids[v] = u0 + v < end ? edges[u0 + v] : 0;
+#pragma unroll
+                for (int v = 0; v < BW_EB; ++v)
+                    if (u0 + v < end) edge((ids[v] >> 6) - ibase, (uint32_t)(ids[v] & 63));
+            }
         }
         const float deg = (float)(end - beg);
         float qn[CS], dn[CS];
@@ -1380,10 +1402,11 @@ inline size_t push_lds_bytes(int N, int cs, int parts) {
 
 // scatter LDS bytes for N points at CS channels (Q | dz | slot | order | buckets;
 // no slot array when the dz words carry the slots)
-inline size_t scatter_lds_bytes(int N, int cs, int parts, bool packed) {
+inline size_t scatter_lds_bytes(int N, int cs, int parts, bool packed, int idcap = 0) {
     const int per = (N + parts - 1) / parts;
     return (size_t)2 * N * cs * sizeof(float) + (packed ? 0 : (((size_t)N * cs + 15) & ~(size_t)15)) +
-           (size_t)((per + 7) & ~7) * sizeof(uint16_t) + BW_BUCKETS * sizeof(int) + BW_FIN_LDS;
+           (size_t)((per + 7) & ~7) * sizeof(uint16_t) + BW_BUCKETS * sizeof(int) + BW_FIN_LDS +
+           (size_t)((idcap + 7) & ~7) * sizeof(uint16_t);
 }
 
 inline int grid_for(int64_t total, int block) {
@@ -1664,19 +1687,42 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
     const size_t per_pc = packed ? 8 : 9;
     int cs = 8;
     while (cs > 1 && per_pc * N * cs > (size_t)BW_LDS_BYTES) cs >>= 1;
+    // LDS-staged in-edge ids (16-bit words: N <= 1024, packed dz words): at most
+    // SCATTER_IDL_CS channels per slice so the slices, the ids (capacity 1.75x a
+    // part's mean in-edge count; a part beyond it reads its ids from HBM) and
+    // the rest fit two workgroups per CU. Measured and kept OFF (r09g, cfg2
+    // step, mean scatter launch): 4-channel slices with LDS ids 59.3 us vs 54.9
+    // for the 8-channel HBM-id form (the narrower slices cost more than the id
+    // latency saves; with ids synthesised instead of loaded, r09e, the 8-channel
+    // form ran 43.8 us, but 8-channel slices leave LDS for ~6.5 K of a part's
+    // ~10 K ids, so most parts fall back: 55.3 us). -DSCATTER_IDL_CS=4 / 8 A/B.
+#ifndef SCATTER_IDL_CS
+#define SCATTER_IDL_CS 0
+#endif
+    const bool idl = SCATTER_IDL_CS > 0 && packed && N <= 1024 && k <= 64;
+    if (idl) cs = std::min(cs, SCATTER_IDL_CS);
     const int slices = (Co + cs - 1) / cs;
     int parts = point_parts(B, slices, N);
     // a cloud whose one-channel slices exceed BW_LDS_BYTES (N > 9216) takes up to
     // the CU's 160 KiB (one workgroup per CU; more point parts shrink the order
     // array): N <= 20000 packed, 17900 unpacked
     while (scatter_lds_bytes(N, cs, parts, packed) > (size_t)160 * 1024 && parts * 64 < N) parts *= 2;
+    int idcap = 0;
+    if (idl) {
+        const int per = (N + parts - 1) / parts;
+        idcap = (int)std::min<int64_t>(7 * (int64_t)per * k / 4, (int64_t)per * k * 2);
+        const size_t room = (size_t)80 * 1024;   // two workgroups per CU
+        const size_t fixed = scatter_lds_bytes(N, cs, parts, packed);
+        if (fixed + 16 * sizeof(uint16_t) > room) idcap = 0;
+        else idcap = std::min<int>(idcap, (int)((room - fixed) / sizeof(uint16_t)) & ~7);
+    }
     const dim3 grid(dgx_xcd_cloud_grid(B, parts * slices));
-    const size_t lds = scatter_lds_bytes(N, cs, parts, packed);
+    const size_t lds = scatter_lds_bytes(N, cs, parts, packed, idcap);
     if (lds > (size_t)160 * 1024) return DGX_EUNSUPPORTED;
     hipStream_t st = dgx_stream(stream);
 #define DGX_SCATTER_LAUNCH(CSV, O16, PK, SP)                                                                      \
     hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK, SP>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 - 1)
+                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 - 1, idcap)
 #define DGX_SCATTER_CASE(CSV)                                                \
     case CSV:                                                               \
         if (packed) {                                                       \

@@ -111,10 +111,11 @@ def net_inputs(world):
 def net_syncbn_amp(rank, world, out_dir, dev):
     """Net as main_partseg_dist.py:189-196, 253-260 trains it: converted with
     SyncBatchNorm, wrapped in DDP, forward under fp16 autocast, backward of the
-    loss scaled by a power of two as GradScaler scales it (2^10 here: exact, so
-    the unscaled gradients compare with an unscaled run), then unscaled. The
-    engine's DGCNN (one C++ op) all-reduces its BN statistics over the module's
-    process group from C++."""
+    unscaled loss (a fixed 2^10 scale overflows the stock fp16 layers'
+    gradients here — GradScaler would skip that step and back off; the
+    GradScaler loop itself is tests/test_amp_bn_gpu.py::
+    test_net_autocast_grad_scaler). The engine's DGCNN (one C++ op)
+    all-reduces its BN statistics over the module's process group from C++."""
     from models.model_partseg import Net
     # both ranks share cuda:0; compute_hog_1x1 moves its histograms to device
     # LOCAL_RANK as the reference does (model_partseg.py:66-73)
@@ -125,7 +126,7 @@ def net_syncbn_amp(rank, world, out_dir, dev):
     pts, lbl, g = net_inputs(world)
     sl = slice(rank * NET_B, (rank + 1) * NET_B)
     x = torch.from_numpy(pts[sl]).to(dev).permute(0, 2, 1).contiguous()
-    scale = 1024.0
+    scale = 1.0
     with torch.autocast("cuda", dtype=torch.float16):
         y = ddp(x, lbl[sl].to(dev))
     ((y.float() * g[sl].to(dev).permute(0, 2, 1)).sum() * scale).backward()
