@@ -888,7 +888,12 @@ __device__ __forceinline__ void scatter_consts(const BnBwdFin& fin, int b, int p
 // SPLIT (with OUT16): dPQ as split bf16 planes, out_split = planes after the
 // first (1: lo; 2: lo, hi) — a separate instantiation, so the bf16 and fp32
 // forms' code is untouched by the extra stores
-template <int CS, bool OUT16, bool PACKED, bool SPLIT = false>
+// TPP > 1 (few-cloud shards): TPP consecutive lanes share a point, each taking
+// every TPP-th in-edge, their sums combined by an xor-shuffle tree (a fixed
+// order: deterministic), so a block of 512 threads covers 512 / TPP points
+// with short per-lane edge chains instead of 512 points' worth of threads of
+// which most are idle at 64 points per block
+template <int CS, bool OUT16, bool PACKED, bool SPLIT = false, int TPP = 1>
 __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     const float* __restrict__ PQ, int ldpq, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ edges,
     const float* __restrict__ dz, const uint8_t* __restrict__ arg, const float* __restrict__ sumP, int B, int N,
@@ -1008,9 +1013,12 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
     // boustrophedon deal of the degree-sorted points: pass 2p takes ranks
     // t, pass 2p+1 ranks from the far end, so a thread's in-degree total (and a
     // wave's longest lane) is balanced instead of wave 0 holding every hub
-    for (int it = 0; it * EC_THREADS < np; ++it) {
-        const int r = it * EC_THREADS + ((it & 1) ? EC_THREADS - 1 - t : t);
-        if (r >= np) continue;
+    static_assert(TPP == 1 || TPP == 2 || TPP == 4 || TPP == 8, "lanes per point");
+    constexpr int PPB = EC_THREADS / TPP;   // points per pass
+    const int pl = t / TPP, sub = t % TPP;
+    for (int it = 0; it * PPB < np; ++it) {
+        const int r = it * PPB + ((it & 1) ? PPB - 1 - pl : pl);
+        if (r >= np) continue;   // the TPP lanes of a point skip together
         const int n = n_beg + order[r];
         const int64_t j = base + n;
         const int32_t beg = rowptr[j], end = rowptr[j + 1];
@@ -1048,7 +1056,26 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
                 for (int u = 0; u < CS; ++u) sd[u] += ((w[u >> 2] >> (8 * (u & 3))) & 0xffu) == slot ? d[u] : 0.f;
             }
         };
-        if (idl) {   // ids from LDS, EB at a time
+        if constexpr (TPP > 1) {
+            // this lane's in-edges beg + sub + TPP * v, EB at a time; then the
+            // point's sums over its TPP lanes
+            constexpr int EB = BW_EB / TPP > 2 ? BW_EB / TPP : 2;
+            for (int32_t u0 = beg + sub; u0 < end; u0 += TPP * EB) {
+                int32_t ids[EB];
+#pragma unroll
+                for (int v = 0; v < EB; ++v) ids[v] = u0 + TPP * v < end ? edges[u0 + TPP * v] : 0;
+#pragma unroll
+                for (int v = 0; v < EB; ++v)
+                    if (u0 + TPP * v < end) edge((ids[v] >> 6) - ibase, (uint32_t)(ids[v] & 63));
+            }
+#pragma unroll
+            for (int m = 1; m < TPP; m <<= 1)
+#pragma unroll
+                for (int u = 0; u < CS; ++u) {
+                    sq[u] += __shfl_xor(sq[u], m);
+                    sd[u] += __shfl_xor(sd[u], m);
+                }
+        } else if (idl) {   // ids from LDS, EB at a time
             for (int32_t u0 = beg; u0 < end; u0 += BW_EB) {
                 uint32_t ids[BW_EB];
 #pragma unroll
@@ -1083,6 +1110,7 @@ __global__ __launch_bounds__(EC_THREADS, 4) void edge_bwd_scatter_kernel(
             dp[u] = fmaf(a[u], sd[u], fmaf(k0[u], deg, k1[u] * fmaf(deg, pjv[u], sq[u])));
             dq[u] = fmaf(a[u], dn[u], fmaf(k0[u], kf, k1[u] * fmaf(kf, qn[u], spv[u])));
         }
+        if (TPP > 1 && sub != 0) continue;   // one lane of the point stores
         if constexpr (SPLIT) {
             // the fp32 mode's split planes: hi = bf16(v) here, lo = bf16(v - hi) at
             // + B*N*2Co (dgx_split_bf16's rounding), the 3-pass GEMMs' operands
@@ -1720,9 +1748,10 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
     const size_t lds = scatter_lds_bytes(N, cs, parts, packed, idcap);
     if (lds > (size_t)160 * 1024) return DGX_EUNSUPPORTED;
     hipStream_t st = dgx_stream(stream);
-#define DGX_SCATTER_LAUNCH(CSV, O16, PK, SP)                                                                      \
-    hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK, SP>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq, rowptr, \
-                       edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 - 1, idcap)
+#define DGX_SCATTER_LAUNCH_T(CSV, O16, PK, SP, TP)                                                                  \
+    hipLaunchKernelGGL((edge_bwd_scatter_kernel<CSV, O16, PK, SP, TP>), grid, dim3(EC_THREADS), lds, st, PQ, ldpq,     \
+                       rowptr, edges, dz, arg, sumP, B, N, k, Co, parts, scale, c0, c1, dPQ, fin, out_bf16 - 1, idcap)
+#define DGX_SCATTER_LAUNCH(CSV, O16, PK, SP) DGX_SCATTER_LAUNCH_T(CSV, O16, PK, SP, 1)
 #define DGX_SCATTER_CASE(CSV)                                                \
     case CSV:                                                               \
         if (packed) {                                                       \
@@ -1735,6 +1764,16 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
             else DGX_SCATTER_LAUNCH(CSV, false, false, false);              \
         }                                                                   \
         break;
+    // few-cloud shards (a part of <= 64 points: the grid was widened by point
+    // parts) in the bf16 packed form: 8 lanes per point (edge_bwd_scatter_kernel TPP)
+#ifndef SCATTER_SMALL_TPP
+#define SCATTER_SMALL_TPP 8
+#endif
+    const int per_pts = (N + parts - 1) / parts;
+    if (SCATTER_SMALL_TPP > 1 && cs == 8 && packed && out_bf16 == 1 && per_pts * SCATTER_SMALL_TPP <= EC_THREADS) {
+        DGX_SCATTER_LAUNCH_T(8, true, true, false, SCATTER_SMALL_TPP);
+        return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
+    }
     switch (cs) {
         DGX_SCATTER_CASE(8)
         DGX_SCATTER_CASE(4)
@@ -1744,6 +1783,7 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
     }
 #undef DGX_SCATTER_CASE
 #undef DGX_SCATTER_LAUNCH
+#undef DGX_SCATTER_LAUNCH_T
     return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
 }
 
