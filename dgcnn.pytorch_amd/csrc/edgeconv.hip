@@ -1764,14 +1764,21 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
             else DGX_SCATTER_LAUNCH(CSV, false, false, false);              \
         }                                                                   \
         break;
-    // few-cloud shards (a part of <= 64 points: the grid was widened by point
-    // parts) in the bf16 packed form: 8 lanes per point (edge_bwd_scatter_kernel TPP)
+    // few-cloud shards (the grid widened by point parts, so a part holds fewer
+    // points than the block has threads) in the bf16 packed form: up to
+    // SCATTER_SMALL_TPP lanes per point (edge_bwd_scatter_kernel TPP). 4-cloud
+    // shard (r09m, mean launch of the step's 4): 1 lane 20.3 us, 8 lanes for
+    // 64-point parts 14.4, 4 lanes for parts up to 128 points 14.1 us
 #ifndef SCATTER_SMALL_TPP
-#define SCATTER_SMALL_TPP 8
+#define SCATTER_SMALL_TPP 4
 #endif
     const int per_pts = (N + parts - 1) / parts;
-    if (SCATTER_SMALL_TPP > 1 && cs == 8 && packed && out_bf16 == 1 && per_pts * SCATTER_SMALL_TPP <= EC_THREADS) {
-        DGX_SCATTER_LAUNCH_T(8, true, true, false, SCATTER_SMALL_TPP);
+    int tpp = 1;
+    while (tpp < SCATTER_SMALL_TPP && per_pts * 2 * tpp <= EC_THREADS) tpp *= 2;
+    if (tpp > 1 && cs == 8 && packed && out_bf16 == 1) {
+        if (tpp >= 8) DGX_SCATTER_LAUNCH_T(8, true, true, false, 8);
+        else if (tpp == 4) DGX_SCATTER_LAUNCH_T(8, true, true, false, 4);
+        else DGX_SCATTER_LAUNCH_T(8, true, true, false, 2);
         return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
     }
     switch (cs) {
