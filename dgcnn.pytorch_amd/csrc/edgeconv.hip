@@ -1764,21 +1764,30 @@ int launch_scatter(const float* PQ, int ldpq, const int32_t* rowptr, const int32
             else DGX_SCATTER_LAUNCH(CSV, false, false, false);              \
         }                                                                   \
         break;
-    // few-cloud shards (the grid widened by point parts, so a part holds fewer
-    // points than the block has threads) in the bf16 packed form: up to
-    // SCATTER_SMALL_TPP lanes per point (edge_bwd_scatter_kernel TPP). 4-cloud
-    // shard (r09m, mean launch of the step's 4): 1 lane 20.3 us, 8 lanes for
-    // 64-point parts 14.4, 4 lanes for parts up to 128 points 14.1 us
+    // packed dz|slot words at 8-channel slices: TPP lanes per point
+    // (edge_bwd_scatter_kernel): 2 for parts of 256+ points, up to
+    // SCATTER_SMALL_TPP while a part's points x lanes fit the block (few-cloud
+    // shards, whose grids are widened by point parts). cfg2 (r09o, mean of the
+    // step's 4 bf16 launches): 1 lane 56.2 us, 2 lanes 52.5, 4 lanes 57.8;
+    // 4-cloud shard (r09m): 1 lane 20.3, 4 lanes 14.1, 8 lanes 14.4 us
 #ifndef SCATTER_SMALL_TPP
 #define SCATTER_SMALL_TPP 4
 #endif
     const int per_pts = (N + parts - 1) / parts;
-    int tpp = 1;
+    int tpp = 2;
     while (tpp < SCATTER_SMALL_TPP && per_pts * 2 * tpp <= EC_THREADS) tpp *= 2;
-    if (tpp > 1 && cs == 8 && packed && out_bf16 == 1) {
-        if (tpp >= 8) DGX_SCATTER_LAUNCH_T(8, true, true, false, 8);
-        else if (tpp == 4) DGX_SCATTER_LAUNCH_T(8, true, true, false, 4);
-        else DGX_SCATTER_LAUNCH_T(8, true, true, false, 2);
+#ifdef SCATTER_FORCE_TPP   // (A/B builds) the same lanes per point at any part size
+    tpp = SCATTER_FORCE_TPP;
+#endif
+    if (tpp > 1 && cs == 8 && packed) {
+#define DGX_SCATTER_TPP(O16, SP)                                             \
+    if (tpp >= 8) DGX_SCATTER_LAUNCH_T(8, O16, true, SP, 8);                 \
+    else if (tpp == 4) DGX_SCATTER_LAUNCH_T(8, O16, true, SP, 4);            \
+    else DGX_SCATTER_LAUNCH_T(8, O16, true, SP, 2);
+        if (out_bf16 >= 2) { DGX_SCATTER_TPP(true, true) }
+        else if (out_bf16) { DGX_SCATTER_TPP(true, false) }
+        else { DGX_SCATTER_TPP(false, false) }
+#undef DGX_SCATTER_TPP
         return hipGetLastError() == hipSuccess ? DGX_OK : DGX_ELAUNCH;
     }
     switch (cs) {
