@@ -719,10 +719,18 @@ void knn_kernel(const float* __restrict__ img, const float* __restrict__ xximg, 
     // last tile, unused): with a data-dependent skip the compiler cannot count
     // the loads in flight and drains them all (vmcnt(0)) every trip. sl = u %
     // SPT is a compile-time constant at every call.
+    // NSTEP <= 16: the loads of a unit are pinned as one group (sched_barrier)
+    // so the prologue and the loop issue them in the same order; the wait
+    // insertion then counts the ring's real distance at each trip's head
+    // instead of draining it (vmcnt(0)). C = 64 90.5 -> 89.8 us, 4-cloud
+    // shard 38.5 -> 37.8 us per call (r09q); at C = 128 (two groups) +1 %: off
+    constexpr bool PIN = NSTEP <= 16;
     auto load = [&](int slot, int u, int sl) {
         const int s = min(h + KQ_HALVES * (u / SPT), ntile - 1);
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
         ld_lane<NSTEP, SW>(ib + (int64_t)s * 64 * NSTEP, lane, sl * SW, a[slot]);
         if (sl == 0) xq[slot] = *reinterpret_cast<const float4*>(xib + s * 16 + 4 * g);
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
     };
 #pragma unroll
     for (int r = 0; r < RING; ++r) load(r, r, r % SPT);
